@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""Benchmark: batched DroneRL env step (+ fused windowed observation) on MI355X.
+
+Metric (BASELINE.json): env-steps/s (= obs/s, train_jax.py:234) at
+num_envs = 65536 per GPU (config C3: 16x16 grid, 8 drones), 1/2/4/8 GPUs.
+
+One "step" = one drl_step launch over every env of the rank: moves,
+collisions, pickup/delivery, battery, rewards, dones, respawns (the CPython
+MT19937 streams included) and the fused observation of drone 0 (K=1, the
+window train_jax.py:55-56 feeds the DQN).  Actions are synthetic uniform
+{0..4}, generated before the timed region and resident in HBM.
+
+Launch:  python bench.py [--gpus 1] [--steps 500] [--warmup 50]
+         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Prints one JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md); ~6300 achievable
+CONFIGS = {
+    # name: (grid, drones, envs per GPU, obs_k)
+    "c2": (16, 8, 4096, 1),
+    "c3": (16, 8, 65536, 1),
+    "c4": (32, 16, 65536, 1),      # 262144 over 4 GPUs
+    "c5": (64, 32, 131072, 1),     # 2**20 over 8 GPUs
+}
+
+
+def algorithmic_bytes(G: int, N: int, K: int, W: int = 7):
+    """read R = G^2 + 4N + N per env-step; writes
+    W = G^2 + 4N + 4N + N + obs (K * W*W*6 f32)."""
+    R = G * G + 4 * N + N
+    Wb = G * G + 4 * N + 4 * N + N + K * W * W * 6 * 4
+    return R, Wb
+
+
+def dist_init():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    return rank, world, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(v: float, world: int) -> float:
+    if world == 1:
+        return v
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def load_traffic(cfg_name: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/),
+    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, or None."""
+    path = os.path.join(REPO, "profiles", f"pmc_{cfg_name}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(G, N, K, seconds: float):
+    """The oracle (C restatement of torch_impl step + WindowedGridView) on host
+    cores, bounded sample; 'port' baseline."""
+    from oracle.oracle import Params, rollout
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    p = Params(side=G, n_drones=N)
+    E = 4096
+    t0 = time.perf_counter()
+    rollout(p, E, 10, nthreads=threads, want_state=False, obs_k=K)
+    dt = time.perf_counter() - t0
+    steps = max(10, int(10 * seconds / max(dt, 1e-3)))
+    t0 = time.perf_counter()
+    rollout(p, E, steps, nthreads=threads, want_state=False, obs_k=K, action_seed=1)
+    dt = time.perf_counter() - t0
+    return {"value": E * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{E} envs x {steps} steps of step()+obs(K={K}) at {G}x{G}/{N} drones, "
+                      f"{threads} host threads, {dt:.1f}s wall"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--envs", type=int, default=0, help="override envs per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-reset-bench", action="store_true")
+    args = ap.parse_args()
+
+    rank, world, local = dist_init()
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+
+    from dronerl_amd import BatchedDeliveryDrones, EnvParams
+    from dronerl_amd._native import lib
+
+    G, N, E, K = CONFIGS[args.config]
+    if args.envs:
+        E = args.envs
+    p = EnvParams(n_drones=N, grid_size=G)
+    dev = torch.device("cuda", local)
+    env = BatchedDeliveryDrones(p, E, device=dev, env_offset=rank * E)
+    env.reset(seed=0)
+    T = args.warmup + args.steps
+    # synthetic actions for every step, resident in HBM before timing
+    actions = torch.empty((T, E, N), dtype=torch.int32, device=dev)
+    for t in range(T):
+        env.synth_actions(seed=2024, step=t, out=actions[t])
+    W = env.layout.obs_window
+    rewards = torch.empty((E, N), dtype=torch.float32, device=dev)
+    dones = torch.empty((E, N), dtype=torch.uint8, device=dev)
+    obs = torch.empty((E, K, W, W, 6), dtype=torch.float32, device=dev)
+
+    # fast path: ctypes arguments built once; only the actions pointer moves
+    L = lib()
+    cp = ctypes.byref(env._cp)
+    st = env.state.c()
+    sp = ctypes.byref(st)
+    a_ptrs = [ctypes.c_void_p(actions[t].data_ptr()) for t in range(T)]
+    r_p, d_p, o_p = (ctypes.c_void_p(x.data_ptr()) for x in (rewards, dones, obs))
+    e_p = ctypes.c_void_p(env.err.data_ptr())
+    stream = torch.cuda.current_stream(dev)
+    s_p = ctypes.c_void_p(stream.cuda_stream)
+
+    def run(t):
+        rc = L.drl_step(cp, sp, a_ptrs[t], r_p, d_p, o_p, K, e_p, s_p)
+        if rc:
+            raise RuntimeError(L.drl_last_error().decode())
+
+    for t in range(args.warmup):
+        run(t)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for t in range(args.warmup, T):
+        run(t)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ev_ms = ev0.elapsed_time(ev1)
+    env.check_errors()
+    wall_max = max_over_ranks(wall, world)
+
+    total_env_steps = E * world * args.steps
+    value = total_env_steps / wall_max
+    launch_s = ev_ms / 1e3 / args.steps      # average drl_step duration on this stream
+    R, Wb = algorithmic_bytes(G, N, K, W)
+    achieved = E * R / launch_s / 1e9
+    achieved_rw = E * (R + Wb) / launch_s / 1e9
+
+    # resets (train_jax.py:101-113 resets every 100 steps in C5): timed separately
+    resets_per_s = None
+    if not args.no_reset_bench:
+        env.reset(seed=None)
+        torch.cuda.synchronize()
+        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        r0.record(stream)
+        nres = 3
+        for _ in range(nres):
+            env.reset(seed=None)
+        r1.record(stream)
+        torch.cuda.synchronize()
+        resets_per_s = E * world * nres / (r0.elapsed_time(r1) / 1e3)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(G, N, K, args.cpu_seconds)
+
+    traffic = load_traffic(args.config)
+    if rank == 0:
+        with open(os.path.join(REPO, "BASELINE.json")) as f:
+            metric = json.load(f)["metric"]
+        out = {
+            "metric": metric,
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic uniform random actions (counter hash), envs seeded random.seed(env index)",
+            "config": {"workload": f"{args.config.upper()}: {G}x{G} grid, {N} drones, {E} envs/GPU, "
+                                   f"step + fused obs(K={K})",
+                       "grid": G, "n_drones": N, "num_envs_per_gpu": E, "num_envs_total": E * world,
+                       "obs_k": K, "parallelism": f"env-shard x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBS,
+                         "traffic": traffic,
+                         "kernel": "drl_step_kernel", "avg_launch_us": launch_s * 1e6,
+                         "algorithmic_read_bytes_per_env_step": R,
+                         "algorithmic_write_bytes_per_env_step": Wb,
+                         "achieved_read_plus_write": achieved_rw,
+                         "frac_read_plus_write": achieved_rw / PEAK_HBM_GBS},
+            "cpu_baseline": cpu,
+            "resets_per_s": resets_per_s,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

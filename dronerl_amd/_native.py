@@ -1,0 +1,107 @@
+"""ctypes binding of libdronerl.so (include/dronerl.h).
+
+There is no CPU fallback: if the HIP library is missing or fails to load,
+every entry point raises.  Build it with ``python -m dronerl_amd.build``
+(``__graft_entry__.build()`` does this too).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdronerl.so")
+
+DRL_MT_WORDS = 640
+DRL_MAX_DRONES = 64
+DRL_MAX_SIDE = 128
+DRL_MAX_RADIUS = 8
+DRL_ERR_BAD_ACTION = 1
+DRL_ERR_NO_FREE_CELL = 2
+
+# Every symbol include/dronerl.h declares (tests check the .so exports them all).
+EXPORTS = ["drl_abi_version", "drl_last_error", "drl_side_from_density", "drl_layout_query", "drl_reset",
+           "drl_step", "drl_obs", "drl_decode", "drl_encode", "drl_synth_actions"]
+
+
+class DrlParams(ctypes.Structure):
+    _fields_ = [
+        ("side", ctypes.c_int32),
+        ("n_drones", ctypes.c_int32),
+        ("charge", ctypes.c_int32),
+        ("discharge", ctypes.c_int32),
+        ("packets_factor", ctypes.c_int32),
+        ("dropzones_factor", ctypes.c_int32),
+        ("stations_factor", ctypes.c_int32),
+        ("skyscrapers_factor", ctypes.c_int32),
+        ("window_radius", ctypes.c_int32),
+        ("pickup_reward", ctypes.c_float),
+        ("delivery_reward", ctypes.c_float),
+        ("crash_reward", ctypes.c_float),
+        ("charge_reward", ctypes.c_float),
+    ]
+
+
+class DrlLayout(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in [
+        "side", "n_drones", "cells", "ground_stride", "drone_stride", "mt_stride", "obs_window", "obs_floats",
+        "step_group_lanes", "step_lds_bytes"]]
+
+
+class DrlState(ctypes.Structure):
+    _fields_ = [
+        ("ground", ctypes.c_void_p),
+        ("drones", ctypes.c_void_p),
+        ("mt", ctypes.c_void_p),
+        ("num_envs", ctypes.c_int64),
+    ]
+
+
+class DroneRLError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libdronerl.so, raising loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise DroneRLError(f"{LIB_PATH} is missing: build the HIP extension with `python -m dronerl_amd.build` "
+                           "(there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
+    P = ctypes.POINTER(DrlParams)
+    S = ctypes.POINTER(DrlState)
+    L.drl_abi_version.restype = i32
+    L.drl_last_error.restype = ctypes.c_char_p
+    L.drl_side_from_density.argtypes = [i32, ctypes.c_double]
+    L.drl_side_from_density.restype = i32
+    L.drl_layout_query.argtypes = [P, ctypes.POINTER(DrlLayout)]
+    L.drl_reset.argtypes = [P, S, i32, u64, vp, vp]
+    L.drl_step.argtypes = [P, S, vp, vp, vp, vp, i32, vp, vp]
+    L.drl_obs.argtypes = [P, S, i32, vp, vp]
+    L.drl_decode.argtypes = [P, S, vp, vp, vp, vp, vp, vp]
+    L.drl_encode.argtypes = [P, S, vp, vp, vp, vp, vp, vp]
+    L.drl_synth_actions.argtypes = [u64, u64, i64, i64, i32, vp, vp]
+    for f in ["drl_layout_query", "drl_reset", "drl_step", "drl_obs", "drl_decode", "drl_encode",
+              "drl_synth_actions"]:
+        getattr(L, f).restype = ctypes.c_int
+    if L.drl_abi_version() != 1:
+        raise DroneRLError("libdronerl.so ABI version mismatch; rebuild it")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise DroneRLError(f"{what} failed ({rc}): {lib().drl_last_error().decode()}")
+
+
+def check_value(rc: int):
+    """Parameter errors surface as ValueError, like the reference's spawn checks."""
+    if rc != 0:
+        raise ValueError(lib().drl_last_error().decode())

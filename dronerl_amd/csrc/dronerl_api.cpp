@@ -1,0 +1,258 @@
+// dronerl_api.cpp — the C ABI (include/dronerl.h): parameter validation,
+// launch geometry, error reporting.  No allocation, no synchronisation.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "dronerl_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+int fail(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return -1;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    g_err = std::string(what) + ": " + hipGetErrorString(e);
+    return -2;
+}
+
+int next_pow2(int v) {
+    int p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+int bit_length(uint32_t n) {
+    int k = 0;
+    while (n) { ++k; n >>= 1; }
+    return k;
+}
+
+constexpr int kStepLdsTarget = 64 * 1024;   // aim for >= 2 blocks per CU
+constexpr int kLdsMax = 160 * 1024;
+constexpr int kResetLdsTarget = 64 * 1024;
+
+// lanes per env in drl_step: pow2 >= n_drones (>= 4), widened when a 256-thread
+// block of narrower groups would not fit the LDS target.
+int step_group_lanes(int n_drones, int gstride) {
+    int P = next_pow2(n_drones < 4 ? 4 : n_drones);
+    auto block_lds = [&](int p) { return 4 * (drl::TW_BYTES + (64 / p) * (2 * gstride + 128)); };
+    while (P < 64 && block_lds(P) > kStepLdsTarget) P <<= 1;
+    return P;
+}
+
+int validate(const drl_params* p, drl_layout* L) {
+    if (!p) return fail("params is NULL");
+    if (p->side < 2 || p->side > DRL_MAX_SIDE) return fail("side %d outside [2, %d]", p->side, DRL_MAX_SIDE);
+    if (p->n_drones < 1 || p->n_drones > DRL_MAX_DRONES)
+        return fail("n_drones %d outside [1, %d]", p->n_drones, DRL_MAX_DRONES);
+    if (p->charge < 0 || p->discharge < 0) return fail("charge/discharge must be >= 0");
+    if (p->window_radius < 1 || p->window_radius > DRL_MAX_RADIUS)
+        return fail("window_radius %d outside [1, %d]", p->window_radius, DRL_MAX_RADIUS);
+    if (p->packets_factor < 0 || p->dropzones_factor < 0 || p->stations_factor < 0 || p->skyscrapers_factor < 0)
+        return fail("object factors must be >= 0");
+    const int GG = p->side * p->side, N = p->n_drones;
+    const long sky = (long)p->skyscrapers_factor * N, pack = (long)p->packets_factor * N;
+    const long drop = (long)p->dropzones_factor * N, stat = (long)p->stations_factor * N;
+    // spawn_objects (env.py:59-60) and Random.sample ValueErrors
+    if (sky > GG) return fail("Not enough positions (%d) to spawn %ld objects", GG, sky);
+    if (N > GG - sky) return fail("Sample larger than population or is negative");
+    if (sky + pack + drop + stat > GG)
+        return fail("Not enough positions (%ld) to spawn %ld objects", GG - sky, pack + drop + stat);
+    if (L) {
+        L->side = p->side;
+        L->n_drones = N;
+        L->cells = GG;
+        L->ground_stride = (GG + 15) / 16 * 16;
+        L->drone_stride = N;
+        L->mt_stride = DRL_MT_WORDS;
+        L->obs_window = 2 * p->window_radius + 1;
+        L->obs_floats = L->obs_window * L->obs_window * 6;
+        L->step_group_lanes = step_group_lanes(N, L->ground_stride);
+        L->step_lds_bytes = 4 * (drl::TW_BYTES + (64 / L->step_group_lanes) * (2 * L->ground_stride + 128));
+        if (L->step_lds_bytes > kLdsMax) return fail("side %d needs %d B of LDS per block", p->side, L->step_lds_bytes);
+    }
+    return 0;
+}
+
+int check_state(const drl_state* s, const drl_layout& L) {
+    if (!s) return fail("state is NULL");
+    if (s->num_envs < 0) return fail("num_envs < 0");
+    if (s->num_envs > 0 && (!s->ground || !s->drones || !s->mt)) return fail("state has NULL buffers");
+    if ((uintptr_t)s->ground % 16) return fail("ground must be 16-byte aligned");
+    (void)L;
+    return 0;
+}
+
+drl::ObsGeom obs_geom(const drl_params* p, const drl_layout& L, int k) {
+    drl::ObsGeom g;
+    g.side = p->side;
+    g.radius = p->window_radius;
+    g.W = (uint32_t)L.obs_window;
+    g.per = (uint32_t)L.obs_floats;
+    g.env_floats = (uint32_t)(k > 0 ? k : 1) * g.per;
+    g.gstride = (uint32_t)L.ground_stride;
+    g.div_env = drl::make_fastdiv(g.env_floats);
+    g.div_per = drl::make_fastdiv(g.per);
+    g.div_6 = drl::make_fastdiv(6);
+    g.div_w = drl::make_fastdiv(g.W);
+    g.div_side = drl::make_fastdiv((uint32_t)p->side);
+    return g;
+}
+
+drl::StepArgs step_args(const drl_params* p, const drl_state* s, const drl_layout& L) {
+    drl::StepArgs a;
+    memset(&a, 0, sizeof a);
+    a.side = p->side;
+    a.n_drones = p->n_drones;
+    a.gstride = L.ground_stride;
+    a.kbits = bit_length((uint32_t)p->side);
+    a.charge = p->charge;
+    a.discharge = p->discharge;
+    a.r_pickup = p->pickup_reward;
+    a.r_delivery = p->delivery_reward;
+    a.r_crash = p->crash_reward;
+    a.r_charge = p->charge_reward;
+    a.E = s->num_envs;
+    a.ground = s->ground;
+    a.drones = s->drones;
+    a.mt = s->mt;
+    a.wave_lds = L.step_lds_bytes / 4;
+    a.max_rounds = 1u << 20;
+    a.div_side = drl::make_fastdiv((uint32_t)p->side);
+    return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t drl_abi_version(void) { return DRL_ABI_VERSION; }
+
+const char* drl_last_error(void) { return g_err.c_str(); }
+
+int32_t drl_side_from_density(int32_t n_drones, double drone_density) {
+    if (!(drone_density > 0.0)) return -1;
+    return (int32_t)ceil(sqrt((double)n_drones / drone_density));
+}
+
+int drl_layout_query(const drl_params* p, drl_layout* out) {
+    if (!out) return fail("layout is NULL");
+    return validate(p, out);
+}
+
+int drl_reset(const drl_params* p, const drl_state* s, int32_t reseed, uint64_t seed_base, const uint8_t* d_env_mask,
+              hipStream_t stream) {
+    drl_layout L;
+    if (validate(p, &L) || check_state(s, L)) return -1;
+    if (s->num_envs == 0) return 0;
+    drl::ResetArgs a;
+    memset(&a, 0, sizeof a);
+    const int N = p->n_drones, GG = L.cells;
+    a.side = p->side;
+    a.n_drones = N;
+    a.cells = GG;
+    a.gstride = L.ground_stride;
+    a.n_sky = p->skyscrapers_factor * N;
+    a.n_pack = p->packets_factor * N;
+    a.n_drop = p->dropzones_factor * N;
+    a.n_stat = p->stations_factor * N;
+    a.E = s->num_envs;
+    a.ground = s->ground;
+    a.drones = s->drones;
+    a.mt = s->mt;
+    a.reseed = reseed ? 1 : 0;
+    a.seed_base = seed_base;
+    a.mask = d_env_mask;
+    // Random.sample branch (random.py:496-504): pool when n <= setsize
+    const int n = GG - a.n_sky;
+    int setsize = 21;
+    if (N > 5) setsize += (int)pow(4.0, ceil(log((double)(N * 3)) / log(4.0)));
+    a.pool_branch = n <= setsize ? 1 : 0;
+    a.list_cap = (GG + 7) / 8 * 8;
+    a.lane_lds = (2 * a.list_cap + 128 + (a.pool_branch ? 2 * a.list_cap : 0) + 15) / 16 * 16;
+    int lanes = (kResetLdsTarget - drl::TW_BYTES) / a.lane_lds;
+    if (lanes < 1) lanes = (kLdsMax - drl::TW_BYTES) / a.lane_lds;
+    if (lanes < 1) return fail("side %d: reset list does not fit LDS", p->side);
+    a.lanes = lanes > 64 ? 64 : lanes;
+    a.block_lds = drl::TW_BYTES + a.lanes * a.lane_lds;
+    a.div_side = drl::make_fastdiv((uint32_t)p->side);
+    hipError_t e = drl::launch_reset(a, stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_reset launch");
+}
+
+int drl_step(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards, uint8_t* d_dones,
+             float* d_obs, int32_t obs_k, int32_t* d_err, hipStream_t stream) {
+    drl_layout L;
+    if (validate(p, &L) || check_state(s, L)) return -1;
+    if (s->num_envs == 0) return 0;
+    if (!d_actions || !d_rewards || !d_dones) return fail("actions/rewards/dones must be non-NULL");
+    if (d_obs && (obs_k < 1 || obs_k > p->n_drones)) return fail("obs_k %d outside [1, n_drones]", obs_k);
+    if (d_obs && ((uintptr_t)d_obs % 16)) return fail("obs must be 16-byte aligned");
+    drl::StepArgs a = step_args(p, s, L);
+    a.actions = d_actions;
+    a.rewards = d_rewards;
+    a.dones = d_dones;
+    a.obs = d_obs;
+    a.err = d_err;
+    a.og = obs_geom(p, L, d_obs ? obs_k : 1);
+    hipError_t e = drl::launch_step(a, L.step_group_lanes, stream, false);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_step launch");
+}
+
+int drl_obs(const drl_params* p, const drl_state* s, int32_t k, float* d_obs, hipStream_t stream) {
+    drl_layout L;
+    if (validate(p, &L) || check_state(s, L)) return -1;
+    if (s->num_envs == 0) return 0;
+    if (!d_obs) return fail("obs is NULL");
+    if (k < 1 || k > p->n_drones) return fail("k %d outside [1, n_drones]", k);
+    if ((uintptr_t)d_obs % 16) return fail("obs must be 16-byte aligned");
+    drl::StepArgs a = step_args(p, s, L);
+    a.obs = d_obs;
+    a.og = obs_geom(p, L, k);
+    hipError_t e = drl::launch_step(a, L.step_group_lanes, stream, true);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_obs launch");
+}
+
+int drl_decode(const drl_params* p, const drl_state* s, int32_t* d_order, int32_t* d_y, int32_t* d_x,
+               int32_t* d_charge, uint8_t* d_carry, hipStream_t stream) {
+    drl_layout L;
+    if (validate(p, &L) || check_state(s, L)) return -1;
+    if (s->num_envs == 0) return 0;
+    hipError_t e = drl::launch_decode(s->drones, s->num_envs, p->n_drones, d_order, d_y, d_x, d_charge, d_carry, stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_decode launch");
+}
+
+int drl_encode(const drl_params* p, const drl_state* s, const int32_t* d_order, const int32_t* d_y, const int32_t* d_x,
+               const int32_t* d_charge, const uint8_t* d_carry, hipStream_t stream) {
+    drl_layout L;
+    if (validate(p, &L) || check_state(s, L)) return -1;
+    if (s->num_envs == 0) return 0;
+    if (!d_order || !d_y || !d_x || !d_charge || !d_carry) return fail("encode inputs must be non-NULL");
+    hipError_t e = drl::launch_encode(s->drones, s->num_envs, p->n_drones, d_order, d_y, d_x, d_charge, d_carry, stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_encode launch");
+}
+
+int drl_synth_actions(uint64_t seed, uint64_t step, int64_t env_offset, int64_t num_envs, int32_t n_drones,
+                      int32_t* d_actions, hipStream_t stream) {
+    if (num_envs < 0 || n_drones < 1) return fail("bad sizes");
+    if (num_envs == 0) return 0;
+    if (!d_actions) return fail("actions is NULL");
+    hipError_t e = drl::launch_synth(seed, step, env_offset, num_envs, n_drones, d_actions, stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_synth_actions launch");
+}
+
+}  // extern "C"

@@ -1,0 +1,78 @@
+// Internal kernel argument blocks shared by dronerl_kernels.hip and dronerl_api.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dronerl.h"
+
+namespace drl {
+
+constexpr int MT_N = 624;
+constexpr int MT_M = 397;
+constexpr int MT_WORDS = DRL_MT_WORDS;
+constexpr int TW_BYTES = 2560;  // 624-word twist buffer, padded to 16 B multiple
+
+enum : int { OBJ_EMPTY = 0, OBJ_SKYSCRAPER = 2, OBJ_STATION = 3, OBJ_DROPZONE = 4, OBJ_PACKET = 5 };
+
+// n / d == umulhi(n, ceil(2^32 / d)) exactly for n * d < 2^32 (all our uses).
+struct FastDiv {
+    uint32_t m;
+    int one;
+};
+
+inline FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f;
+    f.one = (d == 1);
+    f.m = f.one ? 0u : (uint32_t)((((uint64_t)1 << 32) + d - 1) / d);
+    return f;
+}
+
+struct ObsGeom {
+    int side, radius;
+    uint32_t W, per, env_floats, gstride;
+    FastDiv div_env, div_per, div_6, div_w, div_side;
+};
+
+struct StepArgs {
+    int side, n_drones, gstride, kbits;
+    int charge, discharge;
+    float r_pickup, r_delivery, r_crash, r_charge;
+    int64_t E;
+    uint8_t* ground;
+    uint32_t* drones;
+    uint32_t* mt;
+    const int32_t* actions;
+    float* rewards;
+    uint8_t* dones;
+    float* obs;
+    int32_t* err;
+    int wave_lds;
+    uint32_t max_rounds;
+    FastDiv div_side;
+    ObsGeom og;
+};
+
+struct ResetArgs {
+    int side, n_drones, cells, gstride;
+    int n_sky, n_pack, n_drop, n_stat;
+    int64_t E;
+    uint8_t* ground;
+    uint32_t* drones;
+    uint32_t* mt;
+    int reseed;
+    uint64_t seed_base;
+    const uint8_t* mask;
+    int lanes, lane_lds, list_cap, block_lds, pool_branch;
+    FastDiv div_side;
+};
+
+hipError_t launch_step(const StepArgs& a, int P, hipStream_t s, bool obs_only);
+hipError_t launch_reset(const ResetArgs& a, hipStream_t s);
+hipError_t launch_decode(const uint32_t* drones, int64_t E, int N, int32_t* order, int32_t* y, int32_t* x,
+                         int32_t* c, uint8_t* k, hipStream_t s);
+hipError_t launch_encode(uint32_t* drones, int64_t E, int N, const int32_t* order, const int32_t* y,
+                         const int32_t* x, const int32_t* c, const uint8_t* k, hipStream_t s);
+hipError_t launch_synth(uint64_t seed, uint64_t step, int64_t env_offset, int64_t E, int N, int32_t* out,
+                        hipStream_t s);
+
+}  // namespace drl

@@ -1,0 +1,224 @@
+"""Batched DroneRL environment on MI355X (the hot path).
+
+API shape follows jax_impl's vmapped env (jax_impl/env/env.py: reset :89-135,
+step :137-250, get_obs :274-309; callers train_jax.py:52-56,186-193) with a
+leading env axis on PyTorch-ROCm tensors; semantics are torch_impl's
+(env.py:68-233, wrappers.py:10-73), bit-exact, each env carrying its own
+CPython-compatible MT19937 stream seeded like ``random.seed(seed + env)``.
+
+PyTorch is plumbing here (device memory and the current stream); every
+computation runs in libdronerl.so's HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from ._native import DRL_ERR_BAD_ACTION, DRL_ERR_NO_FREE_CELL, DRL_MT_WORDS, DroneRLError, DrlState, check, lib
+from .params import EnvParams
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+@dataclass
+class DroneEnvState:
+    """Device state of E envs (structure of arrays, env-major; include/dronerl.h).
+
+    ground : uint8 [E, ground_stride]  object code per cell, row-major (first side*side bytes)
+    drones : int32 [E, n_drones]       packed u32 records in dict order O
+    mt     : int32 [E, 640]            CPython MT19937 words 0..623, [624] = index
+    """
+    ground: torch.Tensor
+    drones: torch.Tensor
+    mt: torch.Tensor
+
+    @property
+    def num_envs(self) -> int:
+        return self.ground.shape[0]
+
+    def c(self) -> DrlState:
+        return DrlState(self.ground.data_ptr(), self.drones.data_ptr(), self.mt.data_ptr(), self.num_envs)
+
+    def clone(self) -> "DroneEnvState":
+        return DroneEnvState(self.ground.clone(), self.drones.clone(), self.mt.clone())
+
+    def narrow(self, start: int, length: int) -> "DroneEnvState":
+        """A view of envs [start, start+length) (used for sharding and subsets)."""
+        return DroneEnvState(self.ground.narrow(0, start, length), self.drones.narrow(0, start, length),
+                             self.mt.narrow(0, start, length))
+
+
+class BatchedDeliveryDrones:
+    """E independent torch_impl DeliveryDrones envs stepped by HIP kernels.
+
+    Global env index g = env_offset + e; env g's stream is seeded as
+    ``random.seed(seed + g)`` by ``reset(seed)``, so a sharded run is
+    bit-identical to the unsharded one.
+    """
+
+    def __init__(self, params: EnvParams, num_envs: int, device=None, env_offset: int = 0):
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise DroneRLError("BatchedDeliveryDrones runs on the GPU only (no CPU fallback)")
+        self.params = params
+        self.layout = params.layout()  # validates (ValueError like the reference)
+        self._cp = params.to_c()
+        self.num_envs = int(num_envs)
+        self.env_offset = int(env_offset)
+        self.n_drones = params.n_drones
+        self.side = params.side
+        L = self.layout
+        E = self.num_envs
+        dev = self.device
+        self.state = DroneEnvState(
+            ground=torch.zeros((E, L.ground_stride), dtype=torch.uint8, device=dev),
+            drones=torch.zeros((E, L.drone_stride), dtype=torch.int32, device=dev),
+            mt=torch.zeros((E, DRL_MT_WORDS), dtype=torch.int32, device=dev),
+        )
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    # ------------------------------------------------------------ core API --
+    def reset(self, seed: Optional[int] = 0, env_mask: Optional[torch.Tensor] = None) -> DroneEnvState:
+        """env.py:68-101 for every env (or where env_mask != 0).
+
+        seed is not None: re-seed env g as random.seed(seed + g) first
+        (set_seed, rl_helpers.py:18).  seed None: continue each env's stream.
+        """
+        if env_mask is not None:
+            env_mask = self._check(env_mask, torch.uint8, (self.num_envs,), "env_mask")
+        reseed = seed is not None
+        seed_base = (int(seed) + self.env_offset) if reseed else 0
+        s = self.state.c()
+        check(lib().drl_reset(ctypes.byref(self._cp), ctypes.byref(s), int(reseed), seed_base, _ptr(env_mask),
+                              _stream(self.device)), "drl_reset")
+        return self.state
+
+    def step(self, actions: torch.Tensor, obs_k: int = 0, rewards: Optional[torch.Tensor] = None,
+             dones: Optional[torch.Tensor] = None, obs: Optional[torch.Tensor] = None):
+        """env.py:112-215 for every env.  actions int32 [E, N] by drone index.
+
+        Returns (rewards f32 [E,N], dones bool-as-uint8 [E,N]) and, when
+        obs_k > 0, the fused observation f32 [E, obs_k, W, W, 6] of drone
+        indices 0..obs_k-1 after the step (train_jax.py:55-56 uses obs_k=1).
+        """
+        E, N = self.num_envs, self.n_drones
+        actions = self._check(actions, torch.int32, (E, N), "actions")
+        if rewards is None:
+            rewards = torch.empty((E, N), dtype=torch.float32, device=self.device)
+        if dones is None:
+            dones = torch.empty((E, N), dtype=torch.uint8, device=self.device)
+        if obs_k and obs is None:
+            W = self.layout.obs_window
+            obs = torch.empty((E, obs_k, W, W, 6), dtype=torch.float32, device=self.device)
+        s = self.state.c()
+        check(lib().drl_step(ctypes.byref(self._cp), ctypes.byref(s), _ptr(actions), _ptr(rewards), _ptr(dones),
+                             _ptr(obs) if obs_k else None, int(obs_k), _ptr(self.err), _stream(self.device)),
+              "drl_step")
+        if obs_k:
+            return rewards, dones, obs
+        return rewards, dones
+
+    def get_obs(self, k: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """WindowedGridView observation of drone indices 0..k-1: f32 [E, k, W, W, 6]."""
+        k = self.n_drones if k is None else int(k)
+        W = self.layout.obs_window
+        if out is None:
+            out = torch.empty((self.num_envs, k, W, W, 6), dtype=torch.float32, device=self.device)
+        s = self.state.c()
+        check(lib().drl_obs(ctypes.byref(self._cp), ctypes.byref(s), k, _ptr(out), _stream(self.device)), "drl_obs")
+        return out
+
+    def synth_actions(self, seed: int, step: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Uniform synthetic actions (counter hash; identical stream to the oracle's)."""
+        if out is None:
+            out = torch.empty((self.num_envs, self.n_drones), dtype=torch.int32, device=self.device)
+        check(lib().drl_synth_actions(seed, step, self.env_offset, self.num_envs, self.n_drones, _ptr(out),
+                                      _stream(self.device)), "drl_synth_actions")
+        return out
+
+    # ------------------------------------------------------ state plumbing --
+    def decode(self) -> dict:
+        """Per-index drone vectors (jax DroneEnvState fields) + dict order + grid."""
+        E, N, G = self.num_envs, self.n_drones, self.side
+        t = lambda dt: torch.empty((E, N), dtype=dt, device=self.device)
+        out = dict(order=t(torch.int32), y=t(torch.int32), x=t(torch.int32), charge=t(torch.int32),
+                   carrying=t(torch.uint8))
+        s = self.state.c()
+        check(lib().drl_decode(ctypes.byref(self._cp), ctypes.byref(s), _ptr(out["order"]), _ptr(out["y"]),
+                               _ptr(out["x"]), _ptr(out["charge"]), _ptr(out["carrying"]), _stream(self.device)),
+              "drl_decode")
+        out["ground"] = self.state.ground[:, :G * G].view(E, G, G)
+        out["mt_index"] = self.state.mt[:, 624]
+        return out
+
+    def set_state(self, ground, order, y, x, charge, carrying, mt_words=None):
+        """Hand-built states (as jax_tests/test_env.py:14-110 builds DroneEnvState)."""
+        E, N, G = self.num_envs, self.n_drones, self.side
+        dev = self.device
+        as_t = lambda a, dt: torch.as_tensor(a, dtype=dt).to(dev).reshape(E, -1).contiguous()
+        g = as_t(ground, torch.uint8)
+        assert g.shape[1] == G * G
+        self.state.ground.zero_()
+        self.state.ground[:, :G * G].copy_(g)
+        o, yy, xx, ch = (as_t(v, torch.int32) for v in (order, y, x, charge))
+        k = as_t(carrying, torch.uint8)
+        if not torch.equal(o.sort(1).values, torch.arange(N, device=dev, dtype=torch.int32).expand(E, N)):
+            raise ValueError("order must be a permutation of the drone indices in every env")
+        if (yy < 0).any() or (yy >= G).any() or (xx < 0).any() or (xx >= G).any():
+            raise ValueError("drone positions outside the grid")
+        if (ch < 0).any() or (ch > 100).any():
+            raise ValueError("charge must lie in [0, 100]")
+        s = self.state.c()
+        check(lib().drl_encode(ctypes.byref(self._cp), ctypes.byref(s), _ptr(o), _ptr(yy), _ptr(xx), _ptr(ch),
+                               _ptr(k), _stream(dev)), "drl_encode")
+        if mt_words is not None:
+            self.set_mt_words(mt_words)
+
+    def set_mt_words(self, words625):
+        """Load CPython getstate() words (624 state words + index) for every env."""
+        w = torch.as_tensor(words625, dtype=torch.int64).reshape(-1, 625)
+        w = (w & 0xFFFFFFFF).to(torch.int64)
+        w = torch.where(w >= 2**31, w - 2**32, w).to(torch.int32)
+        if w.shape[0] == 1:
+            w = w.expand(self.num_envs, 625)
+        self.state.mt[:, :625].copy_(w.to(self.device))
+
+    def mt_words(self):
+        """CPython-ordered MT words (uint32 values as Python ints) for every env."""
+        w = self.state.mt[:, :625].cpu().to(torch.int64) & 0xFFFFFFFF
+        return w
+
+    def check_errors(self):
+        """Synchronise and raise if a kernel flagged an error since the last check."""
+        e = int(self.err.item())
+        if e:
+            self.err.zero_()
+            msgs = []
+            if e & DRL_ERR_BAD_ACTION:
+                msgs.append("action index out of range (IndexError in the reference)")
+            if e & DRL_ERR_NO_FREE_CELL:
+                msgs.append("respawn found no free cell")
+            raise DroneRLError("; ".join(msgs))
+
+    # ------------------------------------------------------------- helpers --
+    def _check(self, t: torch.Tensor, dtype, shape, name):
+        if not isinstance(t, torch.Tensor):
+            t = torch.as_tensor(t)
+        if t.device != self.device:
+            t = t.to(self.device)
+        if t.dtype != dtype:
+            t = t.to(dtype)
+        if tuple(t.shape) != tuple(shape):
+            raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
+        return t.contiguous()

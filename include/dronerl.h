@@ -1,0 +1,154 @@
+/*
+ * dronerl.h — C ABI of the MI355X-native batched DroneRL environment
+ * (libdronerl.so, hand-written HIP kernels for gfx950).
+ *
+ * The reference (nyx-ai/droneRL) is pure Python and has no FFI; this ABI is
+ * what a Python (ctypes) or any other FFI binds to replace its env hot path:
+ *
+ *   reference                                            this ABI
+ *   torch_impl/env/env.py:68-101   DeliveryDrones.reset   drl_reset
+ *   torch_impl/env/env.py:112-215  DeliveryDrones.step    drl_step
+ *   torch_impl/env/wrappers.py:55-73 WindowedGridView     drl_obs (or drl_step's fused obs)
+ *   jax_impl/env/env.py:89-135     DeliveryDrones.reset   drl_reset (batched over envs)
+ *   jax_impl/env/env.py:137-250    DeliveryDrones.step    drl_step  (batched over envs)
+ *   jax_impl/env/env.py:274-309    DeliveryDrones.get_obs drl_obs
+ *   jax_impl/env/env.py:11-35      DroneEnvParams/State   drl_params / drl_state + drl_decode
+ *   torch_impl/helpers/rl_helpers.py:12-18 set_seed       drl_reset(reseed=1)
+ *
+ * Semantics are torch_impl's, bit-exact (state, dict order, done flags, RNG
+ * stream), with each env carrying its own CPython-compatible MT19937 stream:
+ * env e behaves exactly like `random.seed(seed_base + e); env.reset()` followed
+ * by env.step(...) calls in the reference.
+ *
+ * Conventions
+ *  - All data pointers are DEVICE pointers on the current HIP device.
+ *  - The caller owns every buffer (state included: size them with
+ *    drl_layout_query).  No call allocates, frees or synchronises, so every
+ *    call is hipGraph-capturable; all work is enqueued on `stream`.
+ *  - Return 0 on success, <0 on error (text: drl_last_error(), thread-local).
+ *  - Actions/rewards/dones are indexed by drone index [E][n_drones]; the
+ *    state's drone records are kept in dict order (the reference's hidden
+ *    iteration order O, env.py:124).
+ */
+#ifndef DRONERL_H
+#define DRONERL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* hipStream_t;
+
+#define DRL_ABI_VERSION 1
+#define DRL_MT_WORDS 640     /* per-env MT19937 record: words 0..623 state, [624] = index */
+#define DRL_MAX_DRONES 64
+#define DRL_MAX_SIDE 128
+#define DRL_MAX_RADIUS 8
+
+/* object codes (common/constants.py:15-19) */
+#define DRL_EMPTY 0
+#define DRL_SKYSCRAPER 2
+#define DRL_STATION 3
+#define DRL_DROPZONE 4
+#define DRL_PACKET 5
+
+/* error bits written to drl_step's optional err word */
+#define DRL_ERR_BAD_ACTION 1   /* action outside [-5, 4] (IndexError in the reference) */
+#define DRL_ERR_NO_FREE_CELL 2 /* respawn found no free cell (the reference loops forever) */
+
+/* Env parameters: torch_impl DEFAULT_CONFIG (env.py:28-42) / jax DroneEnvParams
+ * (jax env.py:11-26).  `side` is explicit; torch_impl derives it as
+ * ceil(sqrt(n_drones / drone_density)) (env.py:75): see drl_side_from_density. */
+typedef struct drl_params {
+    int32_t side;
+    int32_t n_drones;
+    int32_t charge;     /* >= 0 */
+    int32_t discharge;  /* >= 0 */
+    int32_t packets_factor;
+    int32_t dropzones_factor;
+    int32_t stations_factor;
+    int32_t skyscrapers_factor;
+    int32_t window_radius; /* 1..DRL_MAX_RADIUS */
+    float pickup_reward;
+    float delivery_reward;
+    float crash_reward;
+    float charge_reward;
+} drl_params;
+
+/* Buffer geometry for a params set. */
+typedef struct drl_layout {
+    int32_t side;
+    int32_t n_drones;
+    int32_t cells;          /* side*side */
+    int32_t ground_stride;  /* bytes per env in `ground` (cells rounded up to 16) */
+    int32_t drone_stride;   /* u32 records per env in `drones` (== n_drones) */
+    int32_t mt_stride;      /* u32 words per env in `mt` (== DRL_MT_WORDS) */
+    int32_t obs_window;     /* 2*radius+1 */
+    int32_t obs_floats;     /* floats per observed drone: window^2 * 6 */
+    int32_t step_group_lanes; /* wavefront lanes per env in drl_step */
+    int32_t step_lds_bytes;   /* dynamic LDS per 256-thread block of drl_step */
+} drl_layout;
+
+/* Device state of num_envs envs (structure of arrays, env-major).
+ *  ground : u8  [E][ground_stride]  object code per cell (row-major y*side+x)
+ *  drones : u32 [E][n_drones]       one record per drone in dict order:
+ *           bits 0-7 y, 8-15 x, 16-23 charge, 24 carrying, 25-31 drone index
+ *  mt     : u32 [E][DRL_MT_WORDS]   CPython MT19937 state; word 624 = index */
+typedef struct drl_state {
+    uint8_t* ground;
+    uint32_t* drones;
+    uint32_t* mt;
+    int64_t num_envs;
+} drl_state;
+
+int32_t drl_abi_version(void);
+const char* drl_last_error(void);
+
+/* ceil(sqrt(n_drones / drone_density)) in double, as env.py:75 computes it. */
+int32_t drl_side_from_density(int32_t n_drones, double drone_density);
+
+/* Validate params and fill the layout.  Errors mirror the reference's
+ * ValueErrors (spawn_objects env.py:59-60, sample, jax env.py:96-104). */
+int drl_layout_query(const drl_params* p, drl_layout* out);
+
+/* reset() for every env (or every env with d_env_mask[e] != 0).
+ * reseed != 0: first re-seed env e's stream as random.seed(seed_base + e)
+ * (rl_helpers.py:18), then draw the reset exactly like env.py:68-101.
+ * reseed == 0: continue each env's current stream (a plain env.reset()). */
+int drl_reset(const drl_params* p, const drl_state* s, int32_t reseed, uint64_t seed_base,
+              const uint8_t* d_env_mask, hipStream_t stream);
+
+/* step(actions) for every env (env.py:112-215).  d_actions int32 [E][n_drones]
+ * by drone index; d_rewards f32 [E][n_drones]; d_dones u8 [E][n_drones].
+ * d_obs (nullable): fused WindowedGridView observation of drone indices
+ * 0..obs_k-1 after the step, f32 [E][obs_k][W][W][6].
+ * d_err (nullable): OR-ed DRL_ERR_* bits. */
+int drl_step(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
+             uint8_t* d_dones, float* d_obs, int32_t obs_k, int32_t* d_err, hipStream_t stream);
+
+/* WindowedGridView observation (wrappers.py:10-31,55-73) of drone indices
+ * 0..k-1: f32 [E][k][W][W][6]. */
+int drl_obs(const drl_params* p, const drl_state* s, int32_t k, float* d_obs, hipStream_t stream);
+
+/* Decode drone records to per-index vectors (jax DroneEnvState fields):
+ * d_order[E][N] = drone index at dict position; y/x/charge/carry [E][N] by
+ * drone index.  Any output may be NULL. */
+int drl_decode(const drl_params* p, const drl_state* s, int32_t* d_order, int32_t* d_y, int32_t* d_x,
+               int32_t* d_charge, uint8_t* d_carry, hipStream_t stream);
+
+/* Inverse of drl_decode (hand-built states, as jax_tests/test_env.py:14-110 do).
+ * charge must lie in [0, 100]. */
+int drl_encode(const drl_params* p, const drl_state* s, const int32_t* d_order, const int32_t* d_y,
+               const int32_t* d_x, const int32_t* d_charge, const uint8_t* d_carry, hipStream_t stream);
+
+/* Synthetic uniform actions in {0..4} from a counter hash of
+ * (seed, step, env_offset + e, drone) — identical to the oracle's stream. */
+int drl_synth_actions(uint64_t seed, uint64_t step, int64_t env_offset, int64_t num_envs, int32_t n_drones,
+                      int32_t* d_actions, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DRONERL_H */

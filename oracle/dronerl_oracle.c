@@ -536,6 +536,8 @@ typedef struct {
     uint32_t* mt625;   /* [E][625] or NULL */
     double* reward_sum; /* [E] or NULL */
     int64_t* done_sum;  /* [E] or NULL */
+    int32_t obs_k, radius; /* >0: also compute the WindowedGridView obs of drones 0..obs_k-1 every step */
+    double obs_checksum;
     int status;
 } rollout_job;
 
@@ -546,7 +548,10 @@ static void* rollout_worker(void* arg) {
     int32_t* act = (int32_t*)malloc(sizeof(int32_t) * (size_t)N);
     double* rew = (double*)malloc(sizeof(double) * (size_t)N);
     uint8_t* dn = (uint8_t*)malloc((size_t)N);
+    const int32_t W = 2 * j->radius + 1;
+    float* ob = j->obs_k > 0 ? (float*)malloc(sizeof(float) * (size_t)j->obs_k * W * W * 6) : NULL;
     j->status = 0;
+    j->obs_checksum = 0.0;
     for (int64_t i = j->e0; i < j->e1; i++) {
         uint64_t genv = (uint64_t)(j->env_offset + i);
         orc_mt_seed(&e->rng, j->seed0 + genv);
@@ -557,6 +562,10 @@ static void* rollout_worker(void* arg) {
             for (int32_t d = 0; d < N; d++) act[d] = orc_synth_action(j->action_seed, (uint64_t)s, genv, (uint32_t)N, (uint32_t)d);
             orc_step(e, act, rew, dn);
             for (int32_t d = 0; d < N; d++) { rs += rew[d]; ds += dn[d]; }
+            if (ob) {
+                orc_obs(e, j->radius, j->obs_k, ob);
+                j->obs_checksum += ob[(s * 7) % (j->obs_k * W * W * 6)];
+            }
         }
         orc_get_state(e, j->ground ? j->ground + i * GG : NULL, j->order ? j->order + i * N : NULL,
                       j->y ? j->y + i * N : NULL, j->x ? j->x + i * N : NULL,
@@ -565,14 +574,15 @@ static void* rollout_worker(void* arg) {
         if (j->reward_sum) j->reward_sum[i] = rs;
         if (j->done_sum) j->done_sum[i] = ds;
     }
-    free(act); free(rew); free(dn);
+    free(act); free(rew); free(dn); free(ob);
     orc_env_destroy(e);
     return NULL;
 }
 
 int orc_rollout(const orc_params* p, int64_t E, int64_t env_offset, uint64_t seed0, uint64_t action_seed,
-                int64_t steps, int32_t nthreads, uint8_t* ground, int32_t* order, int32_t* y, int32_t* x,
-                int32_t* charge, uint8_t* packet, uint32_t* mt625, double* reward_sum, int64_t* done_sum) {
+                int64_t steps, int32_t nthreads, int32_t obs_k, int32_t radius, uint8_t* ground, int32_t* order,
+                int32_t* y, int32_t* x, int32_t* charge, uint8_t* packet, uint32_t* mt625, double* reward_sum,
+                int64_t* done_sum) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     pthread_t th[256];
@@ -588,6 +598,7 @@ int orc_rollout(const orc_params* p, int64_t E, int64_t env_offset, uint64_t see
         j->action_seed = action_seed;
         j->ground = ground; j->order = order; j->y = y; j->x = x; j->charge = charge; j->packet = packet;
         j->mt625 = mt625; j->reward_sum = reward_sum; j->done_sum = done_sum;
+        j->obs_k = obs_k; j->radius = radius;
         if (nthreads == 1) rollout_worker(j);
         else pthread_create(&th[t], NULL, rollout_worker, j);
     }
@@ -597,4 +608,104 @@ int orc_rollout(const orc_params* p, int64_t E, int64_t env_offset, uint64_t see
         if (jobs[t].status) st = jobs[t].status;
     }
     return st;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Multi-env container for per-step parity checks at thousands of envs.      */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    orc_params p;
+    int64_t E;
+    orc_env** envs;
+} orc_multi;
+
+orc_multi* orc_multi_create(const orc_params* p, int64_t E) {
+    orc_multi* m = (orc_multi*)calloc(1, sizeof(orc_multi));
+    m->p = *p;
+    m->E = E;
+    m->envs = (orc_env**)calloc((size_t)E, sizeof(orc_env*));
+    for (int64_t i = 0; i < E; i++) m->envs[i] = orc_env_create(p);
+    return m;
+}
+
+void orc_multi_destroy(orc_multi* m) {
+    if (!m) return;
+    for (int64_t i = 0; i < m->E; i++) orc_env_destroy(m->envs[i]);
+    free(m->envs);
+    free(m);
+}
+
+/* seeds[E] (NULL: continue streams); returns -1 if any reset fails */
+int orc_multi_reset(orc_multi* m, const uint64_t* seeds) {
+    int st = 0;
+    for (int64_t i = 0; i < m->E; i++) {
+        if (seeds) orc_mt_seed(&m->envs[i]->rng, seeds[i]);
+        if (orc_reset(m->envs[i])) st = -1;
+    }
+    return st;
+}
+
+typedef struct {
+    orc_multi* m;
+    int64_t e0, e1;
+    const int32_t* actions;
+    double* rewards;
+    uint8_t* dones;
+    int status;
+} multi_job;
+
+static void* multi_step_worker(void* arg) {
+    multi_job* j = (multi_job*)arg;
+    const int32_t N = j->m->p.n_drones;
+    j->status = 0;
+    for (int64_t i = j->e0; i < j->e1; i++)
+        if (orc_step(j->m->envs[i], j->actions + i * N, j->rewards + i * N, j->dones + i * N)) j->status = -1;
+    return NULL;
+}
+
+int orc_multi_step(orc_multi* m, const int32_t* actions, double* rewards, uint8_t* dones, int32_t nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 64) nthreads = 64;
+    pthread_t th[64];
+    multi_job jobs[64];
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t].m = m;
+        jobs[t].e0 = m->E * t / nthreads;
+        jobs[t].e1 = m->E * (t + 1) / nthreads;
+        jobs[t].actions = actions;
+        jobs[t].rewards = rewards;
+        jobs[t].dones = dones;
+        if (nthreads == 1) multi_step_worker(&jobs[t]);
+        else pthread_create(&th[t], NULL, multi_step_worker, &jobs[t]);
+    }
+    int st = 0;
+    for (int t = 0; t < nthreads; t++) {
+        if (nthreads > 1) pthread_join(th[t], NULL);
+        if (jobs[t].status) st = -1;
+    }
+    return st;
+}
+
+void orc_multi_get_state(const orc_multi* m, uint8_t* ground, int32_t* order, int32_t* y, int32_t* x,
+                         int32_t* charge, uint8_t* packet, uint32_t* mt625) {
+    const int32_t N = m->p.n_drones, GG = m->p.side * m->p.side;
+    for (int64_t i = 0; i < m->E; i++)
+        orc_get_state(m->envs[i], ground ? ground + i * GG : NULL, order ? order + i * N : NULL,
+                      y ? y + i * N : NULL, x ? x + i * N : NULL, charge ? charge + i * N : NULL,
+                      packet ? packet + i * N : NULL, mt625 ? mt625 + i * 625 : NULL);
+}
+
+void orc_multi_set_state(orc_multi* m, const uint8_t* ground, const int32_t* order, const int32_t* y,
+                         const int32_t* x, const int32_t* charge, const uint8_t* packet, const uint32_t* mt625) {
+    const int32_t N = m->p.n_drones, GG = m->p.side * m->p.side;
+    for (int64_t i = 0; i < m->E; i++)
+        orc_set_state(m->envs[i], ground ? ground + i * GG : NULL, order ? order + i * N : NULL,
+                      y ? y + i * N : NULL, x ? x + i * N : NULL, charge ? charge + i * N : NULL,
+                      packet ? packet + i * N : NULL, mt625 ? mt625 + i * 625 : NULL);
+}
+
+/* obs of drone indices 0..k-1 for every env: out[E][k][W][W][6] */
+void orc_multi_obs(const orc_multi* m, int32_t radius, int32_t k, float* out) {
+    const int32_t W = 2 * radius + 1;
+    for (int64_t i = 0; i < m->E; i++) orc_obs(m->envs[i], radius, k, out + i * (int64_t)k * W * W * 6);
 }

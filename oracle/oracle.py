@@ -78,7 +78,7 @@ def lib():
         L.orc_set_state.argtypes = [vp] + [vp] * 7
         L.orc_synth_action.argtypes = [u64, u64, u64, u32, u32]
         L.orc_synth_action.restype = i32
-        L.orc_rollout.argtypes = [ctypes.POINTER(OrcParams), i64, i64, u64, u64, i64, i32] + [vp] * 9
+        L.orc_rollout.argtypes = [ctypes.POINTER(OrcParams), i64, i64, u64, u64, i64, i32, i32, i32] + [vp] * 9
         L.orc_rollout.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -237,7 +237,7 @@ def synth_actions(seed: int, step: int, env_ids, n_drones: int) -> np.ndarray:
 
 
 def rollout(p: Params, E: int, steps: int, seed0: int = 0, action_seed: int = 0, env_offset: int = 0,
-            nthreads: int = 1, want_state: bool = True):
+            nthreads: int = 1, want_state: bool = True, obs_k: int = 0, radius: int = 3):
     """E independent envs, env e seeded random.seed(seed0 + env_offset + e),
     `steps` synthetic-action steps.  Returns a dict of final states + sums."""
     G, N = p.side, p.n_drones
@@ -249,7 +249,7 @@ def rollout(p: Params, E: int, steps: int, seed0: int = 0, action_seed: int = 0,
                    charge=np.zeros((E, N), dtype=np.int32), packet=np.zeros((E, N), dtype=np.uint8),
                    mt=np.zeros((E, 625), dtype=np.uint32))
     g = lambda k: _ptr(out.get(k))
-    st = lib().orc_rollout(ctypes.byref(cp), E, env_offset, seed0, action_seed, steps, nthreads,
+    st = lib().orc_rollout(ctypes.byref(cp), E, env_offset, seed0, action_seed, steps, nthreads, obs_k, radius,
                            g("ground"), g("order"), g("y"), g("x"), g("charge"), g("packet"), g("mt"),
                            g("reward_sum"), g("done_sum"))
     if st:
@@ -257,3 +257,69 @@ def rollout(p: Params, E: int, steps: int, seed0: int = 0, action_seed: int = 0,
     if want_state:
         out["packet"] = out["packet"].astype(bool)
     return out
+
+
+class OracleMulti:
+    """E oracle envs stepped together (C loop, optional threads)."""
+
+    def __init__(self, p: Params, E: int):
+        L = lib()
+        if not hasattr(L, "_multi_ready"):
+            vp = ctypes.c_void_p
+            L.orc_multi_create.argtypes = [ctypes.POINTER(OrcParams), ctypes.c_int64]
+            L.orc_multi_create.restype = vp
+            L.orc_multi_destroy.argtypes = [vp]
+            L.orc_multi_reset.argtypes = [vp, vp]
+            L.orc_multi_reset.restype = ctypes.c_int
+            L.orc_multi_step.argtypes = [vp, vp, vp, vp, ctypes.c_int32]
+            L.orc_multi_step.restype = ctypes.c_int
+            L.orc_multi_get_state.argtypes = [vp] * 8
+            L.orc_multi_set_state.argtypes = [vp] * 8
+            L.orc_multi_obs.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp]
+            L._multi_ready = True
+        self.p, self.E = p, E
+        self._cp = p.c()
+        self._m = L.orc_multi_create(ctypes.byref(self._cp), E)
+
+    def __del__(self):
+        try:
+            lib().orc_multi_destroy(self._m)
+        except Exception:
+            pass
+
+    def reset(self, seeds=None):
+        s = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint64)
+        if lib().orc_multi_reset(self._m, _ptr(s)):
+            raise ValueError("Not enough positions to spawn objects")
+
+    def step(self, actions, nthreads: int = 8):
+        N = self.p.n_drones
+        a = np.ascontiguousarray(actions, dtype=np.int32).reshape(self.E, N)
+        r = np.zeros((self.E, N), dtype=np.float64)
+        d = np.zeros((self.E, N), dtype=np.uint8)
+        if lib().orc_multi_step(self._m, _ptr(a), _ptr(r), _ptr(d), nthreads):
+            raise IndexError("list index out of range")
+        return r, d.astype(bool)
+
+    def state(self) -> dict:
+        E, G, N = self.E, self.p.side, self.p.n_drones
+        out = dict(ground=np.zeros((E, G, G), np.uint8), order=np.zeros((E, N), np.int32),
+                   y=np.zeros((E, N), np.int32), x=np.zeros((E, N), np.int32), charge=np.zeros((E, N), np.int32),
+                   packet=np.zeros((E, N), np.uint8), mt=np.zeros((E, 625), np.uint32))
+        lib().orc_multi_get_state(self._m, *(_ptr(out[k]) for k in
+                                             ["ground", "order", "y", "x", "charge", "packet", "mt"]))
+        out["packet"] = out["packet"].astype(bool)
+        return out
+
+    def set_state(self, ground, order, y, x, charge, packet, mt=None):
+        c = lambda a, t: None if a is None else np.ascontiguousarray(a, dtype=t)
+        lib().orc_multi_set_state(self._m, _ptr(c(ground, np.uint8)), _ptr(c(order, np.int32)),
+                                  _ptr(c(y, np.int32)), _ptr(c(x, np.int32)), _ptr(c(charge, np.int32)),
+                                  _ptr(c(packet, np.uint8)), _ptr(c(mt, np.uint32)))
+
+    def obs(self, radius: int = 3, k: int | None = None) -> np.ndarray:
+        k = self.p.n_drones if k is None else k
+        W = 2 * radius + 1
+        out = np.zeros((self.E, k, W, W, 6), dtype=np.float32)
+        lib().orc_multi_obs(self._m, radius, k, _ptr(out))
+        return out

@@ -1,0 +1,87 @@
+"""CPU-side checks of the C ABI and host logic (no GPU compute)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from dronerl_amd import EnvParams, side_from_density
+from dronerl_amd._native import EXPORTS, LIB_PATH, DrlLayout, lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "dronerl.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:const\s+)?\w+\*?\s+\*?(drl_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    lib()
+    fns = header_functions()
+    assert fns == sorted(EXPORTS)
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\s(drl_\w+)$", out, re.M))
+    missing = [f for f in fns if f not in exported]
+    assert not missing, missing
+    assert lib().drl_abi_version() == 1
+
+
+def test_library_is_gfx950_code_object():
+    out = subprocess.run(["strings", LIB_PATH], capture_output=True, text=True, check=True)
+    assert "amdgcn-amd-amdhsa--gfx950" in out.stdout
+
+
+def test_no_oracle_in_product():
+    """The product package never references the oracle."""
+    pkg = os.path.join(REPO, "dronerl_amd")
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".h")):
+                txt = open(os.path.join(root, f)).read()
+                assert not re.search(r"(import\s+oracle|from\s+oracle|liboracle|orc_\w+\()", txt), f
+
+
+@pytest.mark.parametrize("n,density,side", [(4, 4 / 64, 8), (8, 8 / 256, 16), (16, 16 / 1024, 32),
+                                            (32, 32 / 4096, 64), (1, 0.05, 5), (2, 0.05, 7), (6, 0.05, 11),
+                                            (8, 0.05, 13), (3, 0.05, 8)])
+def test_side_from_density_matches_reference_formula(n, density, side):
+    assert side_from_density(n, density) == side
+    assert lib().drl_side_from_density(n, density) == side
+
+
+def test_layout_and_validation():
+    L = EnvParams(n_drones=8, grid_size=16).layout()
+    assert (L.cells, L.ground_stride, L.drone_stride, L.mt_stride, L.obs_window, L.obs_floats) == \
+        (256, 256, 8, 640, 7, 294)
+    assert L.step_group_lanes == 8
+    L = EnvParams(n_drones=32, grid_size=64).layout()
+    assert L.step_group_lanes in (32, 64) and L.step_lds_bytes <= 160 * 1024
+    L = EnvParams(n_drones=1, grid_size=5).layout()
+    assert L.ground_stride == 32
+    with pytest.raises(ValueError, match="Not enough positions"):
+        EnvParams(n_drones=8, grid_size=8).layout()  # 80 objects on 64 cells
+    with pytest.raises(ValueError):
+        EnvParams(n_drones=65, grid_size=64).layout()
+    with pytest.raises(ValueError):
+        EnvParams(n_drones=4, grid_size=8, window_radius=0).layout()
+    with pytest.raises(ValueError):
+        EnvParams(n_drones=4, grid_size=8, discharge=-1).layout()
+
+
+def test_null_and_empty_calls_fail_cleanly():
+    from dronerl_amd._native import DrlState
+    p = EnvParams(n_drones=8, grid_size=16).to_c()
+    s = DrlState(None, None, None, 0)
+    assert lib().drl_step(ctypes.byref(p), ctypes.byref(s), None, None, None, None, 0, None, None) == 0
+    s = DrlState(None, None, None, 10)
+    assert lib().drl_step(ctypes.byref(p), ctypes.byref(s), None, None, None, None, 0, None, None) != 0
+    assert b"NULL" in lib().drl_last_error()
+
+
+def test_from_torch_config():
+    p = EnvParams.from_torch_config({'n_drones': 6})
+    assert p.side == 11 and p.charge_reward == -0.1
+    assert isinstance(DrlLayout(), ctypes.Structure)

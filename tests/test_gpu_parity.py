@@ -1,0 +1,415 @@
+"""GPU parity: libdronerl.so (HIP, gfx950) vs the oracle and the reference's fixtures.
+
+Bar (BASELINE.json north_star): grid state, dict order, done flags and the MT
+stream bit-exact; rewards equal to float32(reference double) (|err| <= 1e-6
+as stated, in practice 0); observations bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle.oracle import OracleMulti, Params as OParams
+from tests._golden import load_ref_tests, load_traj, traj_names, traj_params
+
+pytestmark = pytest.mark.gpu
+
+REWARD_ATOL = 1e-6  # north_star tolerance for float rewards
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dronerl_amd._native import lib
+    lib()  # must load: no fallback
+
+
+def EnvParams(**kw):
+    from dronerl_amd import EnvParams as P
+    return P(**kw)
+
+
+def Env(p, E, **kw):
+    from dronerl_amd import BatchedDeliveryDrones
+    return BatchedDeliveryDrones(p, E, **kw)
+
+
+def oparams(p) -> OParams:
+    return OParams(side=p.side, n_drones=p.n_drones, charge=p.charge, discharge=p.discharge,
+                   packets_factor=p.packets_factor, dropzones_factor=p.dropzones_factor,
+                   stations_factor=p.stations_factor, skyscrapers_factor=p.skyscrapers_factor,
+                   pickup_reward=p.pickup_reward, delivery_reward=p.delivery_reward, crash_reward=p.crash_reward,
+                   charge_reward=p.charge_reward)
+
+
+def gpu_state(env, envs=None):
+    d = env.decode()
+    out = {k: d[k] for k in ["ground", "order", "y", "x", "charge", "carrying"]}
+    out["mt"] = env.state.mt[:, :625]
+    if envs is not None:
+        idx = torch.as_tensor(envs, device=env.device)
+        out = {k: v.index_select(0, idx) for k, v in out.items()}
+    out = {k: v.cpu().numpy() for k, v in out.items()}
+    out["packet"] = out.pop("carrying").astype(bool)
+    out["mt"] = out["mt"].astype(np.uint32)
+    return out
+
+
+def assert_state(g, o, ctx, mt_full=True):
+    for k in ["ground", "order", "y", "x", "charge", "packet"]:
+        if not np.array_equal(g[k], o[k]):
+            bad = np.argwhere(np.asarray(g[k] != o[k]).reshape(len(g[k]), -1).any(1)).ravel()
+            raise AssertionError(f"{ctx}: '{k}' differs in envs {bad[:10]} (of {len(bad)})")
+    if mt_full:
+        np.testing.assert_array_equal(g["mt"], o["mt"], err_msg=f"{ctx}: mt")
+    else:
+        np.testing.assert_array_equal(g["mt"][:, 624], o["mt"][:, 624], err_msg=f"{ctx}: mt index")
+
+
+def assert_rewards(rg, ro, ctx):
+    rg = np.asarray(rg, dtype=np.float32)
+    np.testing.assert_array_equal(rg, ro.astype(np.float32), err_msg=f"{ctx}: rewards vs f32(ref)")
+    assert np.abs(rg.astype(np.float64) - ro).max(initial=0) <= REWARD_ATOL
+
+
+# --------------------------------------------------------------- fixtures --
+@pytest.mark.parametrize("name", traj_names())
+def test_reference_trajectory_on_gpu(name):
+    """Replay the reference's own seeded trajectories (oracle/gen_golden.py)."""
+    d = load_traj(name)
+    tp = traj_params(d)
+    p = EnvParams(n_drones=tp["n_drones"], grid_size=int(d["side"]), pickup_reward=tp["pickup_reward"],
+                  delivery_reward=tp["delivery_reward"], crash_reward=tp["crash_reward"],
+                  charge_reward=tp["charge_reward"], discharge=tp["discharge"], charge=tp["charge"],
+                  packets_factor=tp["packets_factor"], dropzones_factor=tp["dropzones_factor"],
+                  stations_factor=tp["stations_factor"], skyscrapers_factor=tp["skyscrapers_factor"])
+    E, S, N = d["actions"].shape
+    env = Env(p, E)
+    env.set_mt_words(d["mt0"])           # random.seed(s) words, as captured from CPython
+    env.reset(seed=None)                 # then env.reset() continues that stream
+    obs_steps = list(d["obs_steps"])
+    acts = torch.as_tensor(d["actions"].astype(np.int32)).cuda()
+    for t in range(S + 1):
+        if t > 0:
+            want_obs = t in obs_steps
+            out = env.step(acts[:, t - 1].contiguous(), obs_k=N if want_obs else 0)
+            r, dn = out[0].cpu().numpy(), out[1].cpu().numpy().astype(bool)
+            assert_rewards(r, d["rewards"][:, t - 1], f"{name} step {t}")
+            np.testing.assert_array_equal(dn, d["dones"][:, t - 1], err_msg=f"{name} step {t} dones")
+            if want_obs:
+                np.testing.assert_array_equal(out[2].cpu().numpy(), d["obs"][:, obs_steps.index(t)],
+                                              err_msg=f"{name} step {t} fused obs")
+        g = gpu_state(env)
+        ref = dict(ground=d["ground"][:, t], order=d["order"][:, t], y=d["y"][:, t], x=d["x"][:, t],
+                   charge=d["charge"][:, t], packet=d["packet"][:, t],
+                   mt=np.zeros((E, 625), np.uint32))
+        ref["mt"][:, 624] = d["mtidx"][:, t]
+        assert_state(g, ref, f"{name} step {t}", mt_full=False)
+        if t in obs_steps:
+            np.testing.assert_array_equal(env.get_obs().cpu().numpy(), d["obs"][:, obs_steps.index(t)],
+                                          err_msg=f"{name} step {t} obs")
+    env.check_errors()
+
+
+@pytest.mark.parametrize("name", ["c2_g16_n8", "t_g11_n6", "t_pool_n2"])
+def test_reseed_matches_cpython_seed(name):
+    """drl_reset(reseed) == random.seed(s) (init_by_array) for the fixture seeds."""
+    d = load_traj(name)
+    tp = traj_params(d)
+    p = EnvParams(n_drones=tp["n_drones"], grid_size=int(d["side"]), packets_factor=tp["packets_factor"],
+                  dropzones_factor=tp["dropzones_factor"], stations_factor=tp["stations_factor"],
+                  skyscrapers_factor=tp["skyscrapers_factor"])
+    for e, s in enumerate(d["seeds"]):
+        env = Env(p, 1)
+        env.reset(seed=int(s))
+        g = gpu_state(env)
+        np.testing.assert_array_equal(g["ground"][0], d["ground"][e, 0])
+        np.testing.assert_array_equal(g["y"][0], d["y"][e, 0])
+        np.testing.assert_array_equal(g["x"][0], d["x"][e, 0])
+        np.testing.assert_array_equal(g["packet"][0], d["packet"][e, 0])
+        assert g["mt"][0, 624] == d["mtidx"][e, 0]
+
+
+# ------------------------------------------------------------ vs oracle ---
+CONFIGS = {
+    "c1_8x8_n4": dict(n_drones=4, grid_size=8),
+    "c2_16x16_n8": dict(n_drones=8, grid_size=16),
+    "c4_32x32_n16": dict(n_drones=16, grid_size=32),
+    "c5_64x64_n32": dict(n_drones=32, grid_size=64),
+    "n1_5x5": dict(n_drones=1, grid_size=5),
+    "n3_8x8": dict(n_drones=3, grid_size=8),
+    "n6_11x11": dict(n_drones=6, grid_size=11),
+    "n33_26x26": dict(n_drones=33, grid_size=26),
+    "n64_36x36": dict(n_drones=64, grid_size=36),
+    "pool_5x5_n2": dict(n_drones=2, grid_size=5, packets_factor=2, dropzones_factor=1, stations_factor=1),
+    "dense_10x10_n8": dict(n_drones=8, grid_size=10, pickup_reward=0.5, charge_reward=-0.25, discharge=15,
+                           charge=30),
+    "bigside_128_n4": dict(n_drones=4, grid_size=128),
+}
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_reset_matches_oracle(name):
+    p = EnvParams(**CONFIGS[name])
+    E = 300
+    env = Env(p, E)
+    env.reset(seed=1000)
+    o = OracleMulti(oparams(p), E)
+    o.reset(1000 + np.arange(E))
+    assert_state(gpu_state(env), o.state(), f"{name} reset")
+
+
+@pytest.mark.parametrize("name,E,steps,every", [
+    ("c1_8x8_n4", 1, 1000, 1),
+    ("c2_16x16_n8", 4096, 300, 25),
+    ("c4_32x32_n16", 1024, 150, 30),
+    ("c5_64x64_n32", 256, 100, 25),
+    ("n1_5x5", 333, 300, 20),
+    ("n3_8x8", 500, 300, 20),
+    ("n6_11x11", 257, 300, 20),
+    ("n33_26x26", 97, 120, 20),
+    ("n64_36x36", 65, 120, 20),
+    ("pool_5x5_n2", 200, 300, 20),
+    ("dense_10x10_n8", 600, 300, 20),
+    ("bigside_128_n4", 40, 100, 50),
+])
+def test_rollout_matches_oracle(name, E, steps, every):
+    p = EnvParams(**CONFIGS[name])
+    env = Env(p, E)
+    env.reset(seed=7)
+    o = OracleMulti(oparams(p), E)
+    o.reset(7 + np.arange(E))
+    for t in range(1, steps + 1):
+        a = env.synth_actions(seed=99, step=t)
+        check = (t % every == 0) or t == steps
+        out = env.step(a, obs_k=1 if check else 0)
+        ro, do = o.step(a.cpu().numpy())
+        assert_rewards(out[0].cpu().numpy(), ro, f"{name} step {t}")
+        np.testing.assert_array_equal(out[1].cpu().numpy().astype(bool), do, err_msg=f"{name} step {t} dones")
+        if check:
+            assert_state(gpu_state(env), o.state(), f"{name} step {t}")
+            np.testing.assert_array_equal(out[2].cpu().numpy(), o.obs(3, 1), err_msg=f"{name} step {t} obs")
+    env.check_errors()
+
+
+@pytest.mark.parametrize("E", [1, 2, 3, 7, 31, 33, 63, 65, 129, 1001])
+def test_ragged_num_envs(E):
+    p = EnvParams(n_drones=8, grid_size=16)
+    env = Env(p, E)
+    env.reset(seed=3)
+    o = OracleMulti(oparams(p), E)
+    o.reset(3 + np.arange(E))
+    for t in range(1, 41):
+        a = env.synth_actions(seed=5, step=t)
+        r, dn, ob = env.step(a, obs_k=8)
+        ro, do = o.step(a.cpu().numpy())
+        assert_rewards(r.cpu().numpy(), ro, f"E={E} step {t}")
+    assert_state(gpu_state(env), o.state(), f"E={E}")
+    np.testing.assert_array_equal(ob.cpu().numpy(), o.obs(3, 8))
+
+
+@pytest.mark.parametrize("radius", [1, 2, 3, 4, 5, 8])
+@pytest.mark.parametrize("k", [1, 3, 8])
+def test_obs_variants(radius, k):
+    p = EnvParams(n_drones=8, grid_size=16, window_radius=radius)
+    E = 130
+    env = Env(p, E)
+    env.reset(seed=11)
+    o = OracleMulti(oparams(p), E)
+    o.reset(11 + np.arange(E))
+    for t in range(1, 13):
+        a = env.synth_actions(seed=1, step=t)
+        _, _, ob = env.step(a, obs_k=k)
+        o.step(a.cpu().numpy())
+    want = o.obs(radius, k)
+    np.testing.assert_array_equal(ob.cpu().numpy(), want)
+    np.testing.assert_array_equal(env.get_obs(k).cpu().numpy(), want)
+
+
+def test_shard_invariance():
+    """Two shards with env_offset == one unsharded run (train_jax.py:196-212 semantics)."""
+    p = EnvParams(n_drones=8, grid_size=16)
+    full = Env(p, 1000)
+    halves = [Env(p, 500, env_offset=0), Env(p, 500, env_offset=500)]
+    for e in [full] + halves:
+        e.reset(seed=42)
+    for t in range(1, 61):
+        rf, df = full.step(full.synth_actions(seed=8, step=t))
+        rh = [h.step(h.synth_actions(seed=8, step=t)) for h in halves]
+        assert torch.equal(rf, torch.cat([x[0] for x in rh]))
+        assert torch.equal(df, torch.cat([x[1] for x in rh]))
+    for k in ["ground", "drones", "mt"]:
+        assert torch.equal(getattr(full.state, k), torch.cat([getattr(h.state, k) for h in halves]))
+
+
+def test_masked_reset_continues_stream():
+    p = EnvParams(n_drones=8, grid_size=16)
+    E = 200
+    env = Env(p, E)
+    env.reset(seed=5)
+    o = OracleMulti(oparams(p), E)
+    o.reset(5 + np.arange(E))
+    for t in range(1, 21):
+        a = env.synth_actions(seed=2, step=t)
+        env.step(a)
+        o.step(a.cpu().numpy())
+    mask = (torch.arange(E) % 3 == 0).to(torch.uint8)
+    env.reset(seed=None, env_mask=mask)
+    # oracle: reset (continuing the stream) only the masked envs
+    st = o.state()
+    o2 = OracleMulti(oparams(p), E)
+    o2.set_state(st["ground"], st["order"], st["y"], st["x"], st["charge"], st["packet"], st["mt"])
+    sel = np.nonzero(mask.numpy())[0]
+    o3 = OracleMulti(oparams(p), len(sel))
+    o3.set_state(st["ground"][sel], st["order"][sel], st["y"][sel], st["x"][sel], st["charge"][sel],
+                 st["packet"][sel], st["mt"][sel])
+    o3.reset(None)
+    s3 = o3.state()
+    want = {k: v.copy() for k, v in st.items()}
+    for k in want:
+        want[k][sel] = s3[k]
+    assert_state(gpu_state(env), want, "masked reset")
+
+
+def test_negative_and_bad_actions():
+    """Python list indexing: -1..-5 wrap (STAY..LEFT); others raise (flag)."""
+    p = EnvParams(n_drones=8, grid_size=16)
+    E = 64
+    env = Env(p, E)
+    env.reset(seed=1)
+    o = OracleMulti(oparams(p), E)
+    o.reset(1 + np.arange(E))
+    g = torch.Generator().manual_seed(0)
+    for t in range(30):
+        a = torch.randint(-5, 5, (E, 8), generator=g, dtype=torch.int32)
+        r, _ = env.step(a.cuda())
+        ro, _ = o.step(a.numpy())
+        assert_rewards(r.cpu().numpy(), ro, f"neg step {t}")
+    assert_state(gpu_state(env), o.state(), "negative actions")
+    env.check_errors()
+    bad = torch.full((E, 8), 4, dtype=torch.int32)
+    bad[3, 2] = 5
+    env.step(bad.cuda())
+    from dronerl_amd._native import DroneRLError
+    with pytest.raises(DroneRLError):
+        env.check_errors()
+
+
+def test_hand_built_states_kat():
+    """jax_tests/test_env.py RNG-free known answers (torch semantics) on the GPU."""
+    p = EnvParams(n_drones=3, grid_size=8)
+    env = Env(p, 1)
+    env.reset(seed=0)
+    g = np.zeros((8, 8), np.uint8)
+    g[3, 4] = 3
+    env.set_state(g, [0, 1, 2], [0, 3, 0], [3, 3, 0], [50, 50, 10], [0, 0, 0])
+    r, d = env.step(torch.tensor([[2, 2, 2]], dtype=torch.int32))
+    s = gpu_state(env)
+    assert s["charge"][0].tolist() == [40, 70, 100]
+    assert d[0].tolist() == [0, 0, 1]
+    assert r[0].tolist() == [0.0, np.float32(-0.1), -1.0]
+    # single movements
+    p1 = EnvParams(n_drones=1, grid_size=8)
+    for a, (x, y) in zip(range(5), [(2, 3), (3, 4), (4, 3), (3, 2), (3, 3)]):
+        e1 = Env(p1, 1)
+        e1.reset(seed=0)
+        e1.set_state(np.zeros((8, 8)), [0], [3], [3], [100], [0])
+        e1.step(torch.tensor([[a]], dtype=torch.int32))
+        s = gpu_state(e1)
+        assert (s["x"][0, 0], s["y"][0, 0]) == (x, y)
+    # packages: pickup then delivery, two objects respawned
+    e1 = Env(p1, 1)
+    e1.reset(seed=0)
+    g = np.zeros((8, 8), np.uint8)
+    g[3, 4], g[3, 5] = 5, 4
+    e1.set_state(g, [0], [3], [3], [100], [0])
+    r, _ = e1.step(torch.tensor([[2]], dtype=torch.int32))
+    s = gpu_state(e1)
+    assert s["packet"][0, 0] and s["ground"][0, 3, 4] == 0 and r.item() == 0
+    r, _ = e1.step(torch.tensor([[2]], dtype=torch.int32))
+    s = gpu_state(e1)
+    assert not s["packet"][0, 0] and r.item() == 1 and (s["ground"][0] > 0).sum() == 2
+
+
+# -------------------------------------------- full-size properties (C3-C5) ---
+@pytest.mark.parametrize("cfg,E,steps", [
+    (dict(n_drones=8, grid_size=16), 65536, 200),       # C3 on one GPU
+    (dict(n_drones=16, grid_size=32), 65536, 60),       # C4 per-GPU share (262144 / 4)
+    (dict(n_drones=32, grid_size=64), 131072, 30),      # C5 per-GPU share (2**20 / 8)
+])
+def test_full_size_sampled_parity_and_invariants(cfg, E, steps):
+    p = EnvParams(**cfg)
+    N, G = p.n_drones, p.side
+    env = Env(p, E)
+    env.reset(seed=123)
+    rng = np.random.default_rng(0)
+    sample = np.unique(np.concatenate([[0, 1, E - 1, E // 2], rng.choice(E, 200, replace=False)]))
+    o = OracleMulti(oparams(p), len(sample))
+    o.reset(123 + sample)
+    sidx = torch.as_tensor(sample, device=env.device)
+    rsum = torch.zeros(E, dtype=torch.float64, device=env.device)
+    for t in range(1, steps + 1):
+        a = env.synth_actions(seed=77, step=t)
+        r, dn = env.step(a)
+        rsum += r.double().sum(1)
+        ro, do = o.step(a.index_select(0, sidx).cpu().numpy())
+        assert_rewards(r.index_select(0, sidx).cpu().numpy(), ro, f"step {t}")
+        np.testing.assert_array_equal(dn.index_select(0, sidx).cpu().numpy().astype(bool), do)
+    env.check_errors()
+    assert_state(gpu_state(env, sample), o.state(), "sampled envs")
+    # size-independent invariants over every env
+    d = env.decode()
+    gr = d["ground"]
+    cnt = lambda v: (gr == v).sum(dim=(1, 2))
+    assert torch.all(cnt(2) == 3 * N) and torch.all(cnt(3) == 2 * N) and torch.all(cnt(4) == 2 * N)
+    assert torch.all(cnt(5) + d["carrying"].sum(1) == 3 * N)
+    cells = d["y"].long() * G + d["x"].long()
+    assert torch.all(cells.sort(1).values.diff(dim=1) > 0)  # distinct cells
+    onsky = torch.gather(gr.view(E, -1), 1, cells) == 2
+    assert not onsky.any()
+    assert torch.all((d["charge"] >= 1) & (d["charge"] <= 100))
+    assert torch.all(d["order"].sort(1).values == torch.arange(N, device=env.device))
+    assert torch.all(d["mt_index"] <= 624)
+
+
+# -------------------------------------------------- torch_impl drop-in API ---
+def test_compat_reference_golden_scripts():
+    """The reference's golden scripts, driven through dronerl_amd.compat exactly
+    as they drive torch_impl (set_seed -> reset -> step dicts)."""
+    from dronerl_amd.compat import DeliveryDrones, WindowedGridView, set_seed
+    g = load_ref_tests()
+    base = {'drone_density': 0.05, 'pickup_reward': 0, 'delivery_reward': 1, 'crash_reward': -1,
+            'charge_reward': -0.1, 'discharge': 10, 'charge': 20, 'packets_factor': 3, 'dropzones_factor': 2,
+            'stations_factor': 2, 'skyscrapers_factor': 3, 'rgb_render_rescale': 1.0}
+    # test_windowedgridview.py
+    env = WindowedGridView(DeliveryDrones(dict(base, n_drones=2, charge_reward=0.0)), radius=3)
+    set_seed(env, 0)
+    env.reset()
+    for t, a in enumerate(g["wgv_actions"]):
+        st, _, _, _, _ = env.step({0: int(a[0]), 1: int(a[1])})
+        np.testing.assert_array_equal(st[0].astype(np.float32), g["wgv_windows"][t])
+        assert st[0].dtype == np.float64 and st[0].shape == (7, 7, 6)
+    # test_env_single_drone.py
+    env = WindowedGridView(DeliveryDrones(dict(base, n_drones=1, charge_reward=0.0)), radius=3)
+    set_seed(env, 0)
+    env.reset()
+    for t, a in enumerate(g["single_actions"]):
+        _, r, _, _, _ = env.step({0: int(a)})
+        d0 = env.drones_list[0]
+        assert d0.charge == g["single_charge"][t] and d0.packet == g["single_carry"][t] and r[0] == g["single_reward"][t]
+    # test_env_multiple_drones.py (gym-sampled actions captured in the fixture)
+    env = WindowedGridView(DeliveryDrones(dict(base, n_drones=8)), radius=3)
+    set_seed(env, 0)
+    env.reset()
+    for t, a in enumerate(g["multi_actions"]):
+        _, r, d, _, _ = env.step({i: int(a[i]) for i in range(8)})
+        ch = [dr.charge for dr in sorted(env.drones_list, key=lambda z: z.index)]
+        assert ch == g["multi_charge"][t].tolist()
+        assert [r[i] for i in range(8)] == g["multi_reward"][t].tolist()
+    # the action space reproduces gym 0.25.2 sampling (RandomAgent, 8 draws per step)
+    from dronerl_amd.compat import Discrete
+    sp = Discrete(5)
+    sp.seed(0)
+    for t in range(len(g["multi_actions"])):
+        draws = [sp.sample() for _ in range(8)]
+        assert draws[1:] == g["multi_actions"][t][1:].tolist()
