@@ -3,6 +3,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -41,16 +42,28 @@ int bit_length(uint32_t n) {
     return k;
 }
 
-constexpr int kStepLdsTarget = 64 * 1024;   // aim for >= 2 blocks per CU
+constexpr int kStepLdsTarget = 64 * 1024;   // per block
 constexpr int kLdsMax = 160 * 1024;
 constexpr int kResetLdsTarget = 64 * 1024;
 
-// lanes per env in drl_step: pow2 >= n_drones (>= 4), widened when a 256-thread
-// block of narrower groups would not fit the LDS target.
+int env_np(int n_drones) { return (n_drones + 7) / 8 * 8; }
+
+// LDS bytes per env in drl_step: ground + air map + MT prefetch + posidx
+int step_env_lds(int gstride, int n_drones) { return 2 * gstride + 4 * drl::MT_PF + 2 * env_np(n_drones); }
+
+// waves per block of drl_step (DRL_WAVES_PER_BLOCK overrides; 1, 2 or 4)
+int step_wpb() {
+    const char* v = getenv("DRL_WAVES_PER_BLOCK");
+    const int w = v ? atoi(v) : 2;
+    return (w == 1 || w == 2 || w == 4) ? w : 2;
+}
+
+// lanes per env in drl_step: pow2 >= n_drones (>= 4), widened when one wave
+// of narrower groups would not fit a quarter of the LDS target.
 int step_group_lanes(int n_drones, int gstride) {
-    int P = next_pow2(n_drones < 4 ? 4 : n_drones);
-    auto block_lds = [&](int p) { return 4 * (drl::TW_BYTES + (64 / p) * (2 * gstride + 128)); };
-    while (P < 64 && block_lds(P) > kStepLdsTarget) P <<= 1;
+    int P = 1;
+    while (P < (n_drones < 4 ? 4 : n_drones)) P <<= 1;
+    while (P < 64 && (64 / P) * step_env_lds(gstride, n_drones) > kStepLdsTarget / 4) P <<= 1;
     return P;
 }
 
@@ -82,7 +95,7 @@ int validate(const drl_params* p, drl_layout* L) {
         L->obs_window = 2 * p->window_radius + 1;
         L->obs_floats = L->obs_window * L->obs_window * 6;
         L->step_group_lanes = step_group_lanes(N, L->ground_stride);
-        L->step_lds_bytes = 4 * (drl::TW_BYTES + (64 / L->step_group_lanes) * (2 * L->ground_stride + 128));
+        L->step_lds_bytes = step_wpb() * (64 / L->step_group_lanes) * step_env_lds(L->ground_stride, N);
         if (L->step_lds_bytes > kLdsMax) return fail("side %d needs %d B of LDS per block", p->side, L->step_lds_bytes);
     }
     return 0;
@@ -105,8 +118,8 @@ drl::ObsGeom obs_geom(const drl_params* p, const drl_layout& L, int k) {
     g.per = (uint32_t)L.obs_floats;
     g.env_floats = (uint32_t)(k > 0 ? k : 1) * g.per;
     g.gstride = (uint32_t)L.ground_stride;
-    g.div_env = drl::make_fastdiv(g.env_floats);
-    g.div_per = drl::make_fastdiv(g.per);
+    g.div_env = drl::make_fastdiv(g.env_floats / 6u);  // window cells per env
+    g.div_per = drl::make_fastdiv(g.W * g.W);          // cells per window
     g.div_6 = drl::make_fastdiv(6);
     g.div_w = drl::make_fastdiv(g.W);
     g.div_side = drl::make_fastdiv((uint32_t)p->side);
@@ -130,7 +143,9 @@ drl::StepArgs step_args(const drl_params* p, const drl_state* s, const drl_layou
     a.ground = s->ground;
     a.drones = s->drones;
     a.mt = s->mt;
-    a.wave_lds = L.step_lds_bytes / 4;
+    a.wpb = step_wpb();
+    a.np = env_np(p->n_drones);
+    a.wave_lds = (64 / L.step_group_lanes) * step_env_lds(L.ground_stride, p->n_drones);
     a.max_rounds = 1u << 20;
     a.div_side = drl::make_fastdiv((uint32_t)p->side);
     return a;
@@ -184,11 +199,11 @@ int drl_reset(const drl_params* p, const drl_state* s, int32_t reseed, uint64_t 
     a.pool_branch = n <= setsize ? 1 : 0;
     a.list_cap = (GG + 7) / 8 * 8;
     a.lane_lds = (2 * a.list_cap + 128 + (a.pool_branch ? 2 * a.list_cap : 0) + 15) / 16 * 16;
-    int lanes = (kResetLdsTarget - drl::TW_BYTES) / a.lane_lds;
-    if (lanes < 1) lanes = (kLdsMax - drl::TW_BYTES) / a.lane_lds;
+    int lanes = kResetLdsTarget / a.lane_lds;
+    if (lanes < 1) lanes = kLdsMax / a.lane_lds;
     if (lanes < 1) return fail("side %d: reset list does not fit LDS", p->side);
     a.lanes = lanes > 64 ? 64 : lanes;
-    a.block_lds = drl::TW_BYTES + a.lanes * a.lane_lds;
+    a.block_lds = a.lanes * a.lane_lds;
     a.div_side = drl::make_fastdiv((uint32_t)p->side);
     hipError_t e = drl::launch_reset(a, stream);
     return e == hipSuccess ? 0 : hip_fail(e, "drl_reset launch");

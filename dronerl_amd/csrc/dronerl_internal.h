@@ -10,7 +10,7 @@ namespace drl {
 constexpr int MT_N = 624;
 constexpr int MT_M = 397;
 constexpr int MT_WORDS = DRL_MT_WORDS;
-constexpr int TW_BYTES = 2560;  // 624-word twist buffer, padded to 16 B multiple
+constexpr int MT_PF = 32;       // MT words prefetched into LDS per env and step
 
 enum : int { OBJ_EMPTY = 0, OBJ_SKYSCRAPER = 2, OBJ_STATION = 3, OBJ_DROPZONE = 4, OBJ_PACKET = 5 };
 
@@ -46,7 +46,9 @@ struct StepArgs {
     uint8_t* dones;
     float* obs;
     int32_t* err;
-    int wave_lds;
+    int wave_lds;  // LDS bytes per wave
+    int wpb;       // waves per block
+    int np;        // posidx entries per env (n_drones rounded up to 8)
     uint32_t max_rounds;
     FastDiv div_side;
     ObsGeom og;

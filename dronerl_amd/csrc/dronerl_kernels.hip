@@ -57,102 +57,118 @@ __device__ __forceinline__ uint32_t pack_drone(int y, int x, int c, int carry, i
 }
 
 // In-place MT19937 twist of one env's state by all 64 lanes of the wave,
-// staged through a 624-word LDS buffer.  Processing i in ascending 64-wide
-// chunks, each chunk reading before writing, reproduces the sequential
-// generator exactly: mt[i+1] and mt[i+397] (i < 227) are still old, mt[i-227]
-// (i >= 227) and mt[0] (i = 623) are already new.
-__device__ __noinline__ void twist_wave(uint32_t* row, uint32_t* tw, int lane) {
-    for (int i = lane; i < MT_N; i += 64) tw[i] = load_l2(row + i);
-    wave_sync();
-    for (int base = 0; base < MT_N; base += 64) {
-        const int i = base + lane;
-        uint32_t v = 0;
-        if (i < MT_N) {
-            const uint32_t cur = tw[i];
-            const uint32_t nxt = tw[i + 1 < MT_N ? i + 1 : 0];
-            const uint32_t far = tw[i < MT_N - MT_M ? i + MT_M : i - (MT_N - MT_M)];
-            const uint32_t y = (cur & 0x80000000u) | (nxt & 0x7fffffffu);
-            v = far ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-        }
-        wave_sync();
-        if (i < MT_N) tw[i] = v;
-        wave_sync();
+// register-resident: lane l holds x[c] = mt[64c + l].  Chunks are processed in
+// ascending order, each computed from old/new values exactly as the sequential
+// generator sees them: mt[i+1] and mt[i+397] (i < 227) are still old (chunks
+// > c), mt[i-227] (i >= 227) and mt[0] (i = 623) are already new (chunks < c).
+// Lane offsets are constants (397 = 6*64 + 13, 227 = 4*64 - 29).
+__device__ __noinline__ void twist_wave(uint32_t* row, int lane) {
+    uint32_t x[10];
+#pragma unroll
+    for (int c = 0; c < 10; ++c) {
+        const int i = 64 * c + lane;
+        x[c] = (i < MT_N) ? load_l2(row + i) : 0u;
     }
-    for (int i = lane; i < MT_N; i += 64) row[i] = tw[i];
+#pragma unroll
+    for (int c = 0; c < 10; ++c) {
+        const int i = 64 * c + lane;
+        uint32_t nxt = __shfl(x[c], (lane + 1) & 63);
+        if (c < 9) {
+            const uint32_t n0 = __shfl(x[c + 1], 0);
+            if (lane == 63) nxt = n0;
+        } else {
+            const uint32_t m0 = __shfl(x[0], 0);  // new mt[0]
+            if (i == MT_N - 1) nxt = m0;
+        }
+        const int l13 = lane + 13, l29 = lane + 29;
+        const uint32_t fo_a = (c + 6 < 10) ? __shfl(x[(c + 6) % 10], l13 & 63) : 0u;
+        const uint32_t fo_b = (c + 7 < 10) ? __shfl(x[(c + 7) % 10], l13 & 63) : 0u;
+        const uint32_t fn_a = (c >= 4) ? __shfl(x[(c + 6) % 10], l29 & 63) : 0u;  // x[c-4]
+        const uint32_t fn_b = (c >= 3) ? __shfl(x[(c + 7) % 10], l29 & 63) : 0u;  // x[c-3]
+        const uint32_t far = (i < MT_N - MT_M) ? (l13 < 64 ? fo_a : fo_b) : (l29 < 64 ? fn_a : fn_b);
+        const uint32_t y = (x[c] & 0x80000000u) | (nxt & 0x7fffffffu);
+        x[c] = far ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+#pragma unroll
+    for (int c = 0; c < 10; ++c) {
+        const int i = 64 * c + lane;
+        if (i < MT_N) row[i] = x[c];
+    }
     // make the rewritten words visible to this workgroup's later sc1 loads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     wave_sync();
 }
 
 // ------------------------------------------------------- observation write ---
-// Writes the observation windows of the wave's envs: floats [F0, F0 + n) of
-// obs, where the wave owns envs wenv0.. and float f (wave-local) decomposes as
-// (env, k, wy, wx, ch).  Quads fully inside the range use 16-B stores.
-// wrappers.py:10-31: ch0 drone, ch1 packet OR carrying drone, ch2 dropzone,
-// ch3 station, ch4 charge/100 (true f32 division), ch5 skyscraper / wall.
-__device__ __forceinline__ float obs_value(uint32_t f, const ObsGeom& g, const uint8_t* gl_all,
-                                           const uint8_t* al_all, const uint16_t* posidx_all) {
-    const uint32_t e = fdiv(f, g.div_env);
-    uint32_t rem = f - e * g.env_floats;
-    const uint32_t k = fdiv(rem, g.div_per);
-    rem -= k * g.per;
-    const uint32_t cw = fdiv(rem, g.div_6);
-    const uint32_t ch = rem - cw * 6u;
-    const uint32_t wy = fdiv(cw, g.div_w);
-    const uint32_t wx = cw - wy * g.W;
-    const uint32_t pos = posidx_all[e * 64u + k];
-    const uint32_t py = fdiv(pos, g.div_side);
-    const uint32_t px = pos - py * g.side;
-    const int y = (int)(py + wy) - g.radius;
-    const int x = (int)(px + wx) - g.radius;
-    if (y < 0 || y >= g.side || x < 0 || x >= g.side) return ch == 5u ? 1.0f : 0.0f;
-    const uint32_t cell = (uint32_t)(y * g.side + x);
-    const uint32_t obj = gl_all[e * g.gstride + cell];
-    const uint32_t air = al_all[e * g.gstride + cell];
-    switch (ch) {
-        case 0: return air ? 1.0f : 0.0f;
-        case 1: return (obj == OBJ_PACKET || (air & 0x80u)) ? 1.0f : 0.0f;
-        case 2: return obj == OBJ_DROPZONE ? 1.0f : 0.0f;
-        case 3: return obj == OBJ_STATION ? 1.0f : 0.0f;
-        case 4: return air ? (float)((int)(air & 0x7fu) - 1) / 100.0f : 0.0f;
-        default: return obj == OBJ_SKYSCRAPER ? 1.0f : 0.0f;
-    }
+// Per-wave LDS image of its envs (every region a multiple of 16 B):
+//   gl  [GPW][gstride] ground codes      al [GPW][gstride] air: 0 or (charge+1)|carry<<7
+//   mtw [GPW][PF] u32  prefetched MT words   posidx [GPW][NP] u16 cell of drone index k
+struct WaveLds {
+    uint8_t* gl;
+    uint8_t* al;
+    uint32_t* mtw;
+    uint16_t* posidx;
+};
+
+__device__ __forceinline__ WaveLds carve(unsigned char* wbase, int gpw, int gstride, int np) {
+    WaveLds w;
+    w.gl = wbase;
+    w.al = w.gl + gpw * gstride;
+    w.mtw = reinterpret_cast<uint32_t*>(w.al + gpw * gstride);
+    w.posidx = reinterpret_cast<uint16_t*>(w.mtw + gpw * MT_PF);
+    (void)np;
+    return w;
 }
 
+// WindowedGridView windows (wrappers.py:10-31,55-73) of the wave's envs:
+// lane = one window cell; its 6 channels are computed branch-free and stored
+// as three 8-B pieces (consecutive lanes cover a contiguous span).  ch0 drone,
+// ch1 packet OR carrying drone, ch2 dropzone, ch3 station, ch4 charge/100
+// (true f32 division, == f32(double c/100)), ch5 skyscraper or wall.
 __device__ __forceinline__ void write_obs_wave(float* __restrict__ obs, int64_t wenv0, int nenv_w,
-                                               const ObsGeom& g, const uint8_t* gl_all, const uint8_t* al_all,
-                                               const uint16_t* posidx_all, int lane) {
-    const int64_t F0 = wenv0 * (int64_t)g.env_floats;
-    const uint32_t n = (uint32_t)nenv_w * g.env_floats;
-    const int64_t q0 = F0 >> 2, q1 = (F0 + n + 3) >> 2;
-    for (int64_t q = q0 + lane; q < q1; q += 64) {
-        const int64_t Fq = q << 2;
-        if (Fq >= F0 && Fq + 4 <= F0 + (int64_t)n) {
-            const uint32_t f = (uint32_t)(Fq - F0);
-            float4 v;
-            v.x = obs_value(f + 0, g, gl_all, al_all, posidx_all);
-            v.y = obs_value(f + 1, g, gl_all, al_all, posidx_all);
-            v.z = obs_value(f + 2, g, gl_all, al_all, posidx_all);
-            v.w = obs_value(f + 3, g, gl_all, al_all, posidx_all);
-            *reinterpret_cast<float4*>(obs + Fq) = v;
-        } else {
-            for (int t = 0; t < 4; ++t) {
-                const int64_t F = Fq + t;
-                if (F >= F0 && F < F0 + (int64_t)n)
-                    obs[F] = obs_value((uint32_t)(F - F0), g, gl_all, al_all, posidx_all);
-            }
-        }
+                                               const ObsGeom& g, const WaveLds& w, int np, int lane) {
+    const uint32_t win = g.W * g.W;
+    const uint32_t env_cells = g.env_floats / 6u;  // K * W*W
+    const uint32_t ncell = (uint32_t)nenv_w * env_cells;
+    float* base = obs + wenv0 * (int64_t)g.env_floats;
+    for (uint32_t q = lane; q < ncell; q += 64) {
+        const uint32_t e = fdiv(q, g.div_env);
+        uint32_t rem = q - e * env_cells;
+        const uint32_t k = fdiv(rem, g.div_per);
+        rem -= k * win;
+        const uint32_t wy = fdiv(rem, g.div_w);
+        const uint32_t wx = rem - wy * g.W;
+        const uint32_t pos = w.posidx[e * np + k];
+        const uint32_t py = fdiv(pos, g.div_side);
+        const uint32_t px = pos - py * (uint32_t)g.side;
+        const int y = (int)(py + wy) - g.radius;
+        const int x = (int)(px + wx) - g.radius;
+        const bool in = (unsigned)y < (unsigned)g.side && (unsigned)x < (unsigned)g.side;
+        const uint32_t cell = e * g.gstride + (uint32_t)(y * g.side + x);
+        const uint32_t obj = in ? w.gl[cell] : (uint32_t)OBJ_SKYSCRAPER;
+        const uint32_t air = in ? w.al[cell] : 0u;
+        float2 v01, v23, v45;
+        v01.x = air ? 1.0f : 0.0f;
+        v01.y = (obj == OBJ_PACKET || (air & 0x80u)) ? 1.0f : 0.0f;
+        v23.x = obj == OBJ_DROPZONE ? 1.0f : 0.0f;
+        v23.y = obj == OBJ_STATION ? 1.0f : 0.0f;
+        v45.x = air ? (float)((int)(air & 0x7fu) - 1) / 100.0f : 0.0f;
+        v45.y = obj == OBJ_SKYSCRAPER ? 1.0f : 0.0f;
+        float2* o = reinterpret_cast<float2*>(base + 6u * q);
+        o[0] = v01;
+        o[1] = v23;
+        o[2] = v45;
     }
 }
 
 // Stage a wave's grounds (contiguous, env-major) into LDS and clear the air map.
 __device__ __forceinline__ void stage_ground(const uint8_t* __restrict__ ground, int64_t wenv0, int nenv_w,
-                                             int gstride, uint8_t* gl_all, uint8_t* al_all, int lane) {
+                                             int gstride, const WaveLds& w, int lane) {
     const uint4* src = reinterpret_cast<const uint4*>(ground + wenv0 * gstride);
     const int nvec = nenv_w * gstride / 16;
     for (int v = lane; v < nvec; v += 64) {
-        reinterpret_cast<uint4*>(gl_all)[v] = src[v];
-        reinterpret_cast<uint4*>(al_all)[v] = make_uint4(0u, 0u, 0u, 0u);
+        reinterpret_cast<uint4*>(w.gl)[v] = src[v];
+        reinterpret_cast<uint4*>(w.al)[v] = make_uint4(0u, 0u, 0u, 0u);
     }
 }
 
@@ -165,34 +181,37 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
     const int wave = threadIdx.x >> 6;
     const int grp = lane / P;
     const int j = lane % P;
-    const int64_t wenv0 = ((int64_t)blockIdx.x * 4 + wave) * GPW;
+    const int64_t wenv0 = ((int64_t)blockIdx.x * a.wpb + wave) * GPW;
     const int nenv_w = (int)min((int64_t)GPW, a.E - wenv0);
     if (nenv_w <= 0) return;  // no block-level barriers anywhere: whole idle waves may leave
     const int64_t env = wenv0 + grp;
     const bool env_ok = grp < nenv_w;
-    const int G = a.side, N = a.n_drones, gstride = a.gstride;
+    const int G = a.side, N = a.n_drones, gstride = a.gstride, np = a.np;
+    const WaveLds W = carve(smem + wave * a.wave_lds, GPW, gstride, np);
+    uint8_t* gl = W.gl + grp * gstride;
+    uint8_t* al = W.al + grp * gstride;
+    uint32_t* mtw = W.mtw + grp * MT_PF;
+    uint16_t* posidx = W.posidx + grp * np;
 
-    unsigned char* wbase = smem + wave * a.wave_lds;
-    uint32_t* tw = reinterpret_cast<uint32_t*>(wbase);
-    uint8_t* gl_all = wbase + TW_BYTES;
-    uint8_t* al_all = gl_all + GPW * gstride;
-    uint16_t* posidx_all = reinterpret_cast<uint16_t*>(al_all + GPW * gstride);
-    uint8_t* gl = gl_all + grp * gstride;
-    uint8_t* al = al_all + grp * gstride;
-    uint16_t* posidx = posidx_all + grp * 64;
-
-    stage_ground(a.ground, wenv0, nenv_w, gstride, gl_all, al_all, lane);
-
-    // ---- drone record and action (env.py:124-127)
+    // ---- loads, all independent: drone record, this lane's action (by drone
+    // index j), the env's MT index, the ground (-> LDS)
     const bool active = env_ok && j < N;
     const uint32_t rec = active ? a.drones[env * N + j] : 0u;
+    const int my_action = active ? a.actions[env * N + j] : 4;
+    const uint32_t* mrow = a.mt + (env_ok ? env : 0) * MT_WORDS;
+    int midx = env_ok ? (int)mrow[MT_N] : MT_N;
+    stage_ground(a.ground, wenv0, nenv_w, gstride, W, lane);
+    // prefetch the next MT_PF words of the stream into LDS (dependent on midx only)
+    const int pf_base0 = midx;
+    int pfn = min(MT_PF, MT_N - midx);
+    for (int o = j; o < pfn; o += P) mtw[o] = mrow[midx + o];
+
     const int y = rec & 255u, x = (rec >> 8) & 255u;
     const int idx = ((int)(rec >> 25) < N) ? (int)(rec >> 25) : j;  // corrupt records never index out of bounds
     int c = (rec >> 16) & 255u;
     int carry = (rec >> 24) & 1u;
-    int act = 4;
+    int act = __shfl(my_action, idx, P);  // actions are by drone index (env.py:125)
     if (active) {
-        act = a.actions[env * N + idx];
         if (act < 0) act += 5;  // Python negative list index
         if ((unsigned)act > 4u) {
             if (a.err) atomicOr(a.err, DRL_ERR_BAD_ACTION);
@@ -255,16 +274,19 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
     const bool crashB = claimer && (collided || dead);
     const bool survivor = claimer && !crashB;
     const bool crashed = crashA || crashB;
-    const uint64_t gm = (P == 64) ? ~0ull : (((1ull << P) - 1ull) << (grp * P));
+    const int gshift = grp * P;
+    const uint64_t gm = (P == 64) ? ~0ull : (((1ull << P) - 1ull) << gshift);
     const uint64_t lower = (1ull << lane) - 1ull;
     const uint64_t bS = __ballot(survivor) & gm;
     const uint64_t bA = __ballot(crashA) & gm;
     const uint64_t bB = __ballot(crashB) & gm;
     const int nS = __popcll(bS), nA = __popcll(bA), nR = nA + __popcll(bB);
-    const int bkey = crashB ? (collided ? later_min : P + j) : 4 * P;
     int rankB = 0;
+    if (bB) {
+        const int bkey = crashB ? (collided ? later_min : P + j) : 4 * P;
 #pragma unroll
-    for (int s = 0; s < P; ++s) rankB += (__shfl(bkey, s, P) < bkey);
+        for (int s = 0; s < P; ++s) rankB += (__shfl(bkey, s, P) < bkey);
+    }
     const int newslot = survivor ? __popcll(bS & lower)
                                  : (crashA ? nS + __popcll(bA & lower) : (crashB ? nS + nA + rankB : j));
     const int n_deliver = __popcll(__ballot(deliver) & gm);
@@ -286,8 +308,7 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
     // draws P consecutive MT outputs, keeps those < side (randint(0, side-1)
     // == _randbelow(side)), pairs accepted draws as (y, x) and takes the
     // first pair whose cell is free.
-    const uint32_t* mrow = a.mt + (env_ok ? env : 0) * MT_WORDS;
-    int midx = env_ok ? (int)a.mt[env * MT_WORDS + MT_N] : MT_N;
+    int pf_base = pf_base0;
     int w = 0, have_y = 0, yv = 0;
     const int shift = 32 - a.kbits;
     uint32_t rounds = 0;
@@ -298,15 +319,22 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
         while (need) {
             const int tl = __ffsll((unsigned long long)need) - 1;
             need &= need - 1ull;
-            twist_wave(a.mt + (wenv0 + tl / P) * MT_WORDS, tw, lane);
-            if (grp == tl / P) midx = 0;
+            twist_wave(a.mt + (wenv0 + tl / P) * MT_WORDS, lane);
+            if (grp == tl / P) {
+                midx = 0;
+                pf_base = 0;
+                pfn = 0;  // prefetched words are stale now
+            }
         }
         if (work) {
             const int avail = MT_N - midx;
             const bool valid = j < avail;
-            const int r = valid ? (int)(temper(load_l2(mrow + midx + j)) >> shift) : G;
+            const int off = midx - pf_base + j;
+            uint32_t word = 0u;
+            if (valid) word = (off < pfn) ? mtw[off] : load_l2(mrow + midx + j);
+            const int r = valid ? (int)(temper(word) >> shift) : G;
             const bool acc = valid && r < G;
-            const uint64_t accb = (__ballot(acc) & gm) >> (grp * P);
+            const uint64_t accb = (__ballot(acc) & gm) >> gshift;
             const uint64_t lowrel = (1ull << j) - 1ull;
             const int apos = have_y + __popcll(accb & lowrel);
             const uint64_t prevm = accb & lowrel;
@@ -320,7 +348,7 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
                 const int obj = gl[ccell];
                 free_cell = (w < nR) ? (al[ccell] == 0 && obj != OBJ_SKYSCRAPER) : (obj == OBJ_EMPTY);
             }
-            const uint64_t okb = (__ballot(cand && free_cell) & gm) >> (grp * P);
+            const uint64_t okb = (__ballot(cand && free_cell) & gm) >> gshift;
             if (okb) {
                 const int js = __ffsll((unsigned long long)okb) - 1;
                 const int cell = __shfl(ccell, js, P);
@@ -375,7 +403,7 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
         const uint4* src = reinterpret_cast<const uint4*>(gl);
         for (int v = j; v < gstride / 16; v += P) dst[v] = src[v];
     }
-    if (a.obs) write_obs_wave(a.obs, wenv0, nenv_w, a.og, gl_all, al_all, posidx_all, lane);
+    if (a.obs) write_obs_wave(a.obs, wenv0, nenv_w, a.og, W, np, lane);
 }
 
 // ------------------------------------------------------------ observation ---
@@ -387,28 +415,25 @@ __global__ void __launch_bounds__(256) drl_obs_kernel(StepArgs a) {
     const int wave = threadIdx.x >> 6;
     const int grp = lane / P;
     const int j = lane % P;
-    const int64_t wenv0 = ((int64_t)blockIdx.x * 4 + wave) * GPW;
+    const int64_t wenv0 = ((int64_t)blockIdx.x * a.wpb + wave) * GPW;
     const int nenv_w = (int)min((int64_t)GPW, a.E - wenv0);
     if (nenv_w <= 0) return;
     const int64_t env = wenv0 + grp;
     const bool env_ok = grp < nenv_w;
-    const int N = a.n_drones, gstride = a.gstride;
-    unsigned char* wbase = smem + wave * a.wave_lds;
-    uint8_t* gl_all = wbase + TW_BYTES;
-    uint8_t* al_all = gl_all + GPW * gstride;
-    uint16_t* posidx_all = reinterpret_cast<uint16_t*>(al_all + GPW * gstride);
-    stage_ground(a.ground, wenv0, nenv_w, gstride, gl_all, al_all, lane);
+    const int N = a.n_drones, gstride = a.gstride, np = a.np;
+    const WaveLds W = carve(smem + wave * a.wave_lds, GPW, gstride, np);
+    stage_ground(a.ground, wenv0, nenv_w, gstride, W, lane);
     wave_sync();
     if (env_ok && j < N) {
         const uint32_t rec = a.drones[env * N + j];
         const int pos = (int)(rec & 255u) * a.side + (int)((rec >> 8) & 255u);
         const int c = (rec >> 16) & 255u, carry = (rec >> 24) & 1u;
         const int idx = ((int)(rec >> 25) < N) ? (int)(rec >> 25) : j;
-        posidx_all[grp * 64 + idx] = (uint16_t)pos;
-        al_all[grp * gstride + pos] = (uint8_t)((c + 1) | (carry << 7));
+        W.posidx[grp * np + idx] = (uint16_t)pos;
+        W.al[grp * gstride + pos] = (uint8_t)((c + 1) | (carry << 7));
     }
     wave_sync();
-    write_obs_wave(a.obs, wenv0, nenv_w, a.og, gl_all, al_all, posidx_all, lane);
+    write_obs_wave(a.obs, wenv0, nenv_w, a.og, W, np, lane);
 }
 
 // ------------------------------------------------------------------ reset ---
@@ -474,8 +499,7 @@ __global__ void __launch_bounds__(64) drl_reset_kernel(ResetArgs a) {
     const int lane = threadIdx.x;
     const int64_t env = (int64_t)blockIdx.x * a.lanes + lane;
     const bool own = lane < a.lanes && env < a.E && (a.mask == nullptr || a.mask[env] != 0);
-    uint32_t* tw = reinterpret_cast<uint32_t*>(smem);
-    uint16_t* list = reinterpret_cast<uint16_t*>(smem + TW_BYTES + (size_t)lane * a.lane_lds);
+    uint16_t* list = reinterpret_cast<uint16_t*>(smem + (size_t)lane * a.lane_lds);
     uint16_t* sel = list + a.list_cap;
     uint16_t* pool = sel + 64;
     const int GG = a.cells, N = a.n_drones;
@@ -501,7 +525,7 @@ __global__ void __launch_bounds__(64) drl_reset_kernel(ResetArgs a) {
         while (need_) {                                                                   \
             const int tl_ = __ffsll((unsigned long long)need_) - 1;                       \
             need_ &= need_ - 1ull;                                                        \
-            twist_wave(a.mt + ((int64_t)blockIdx.x * a.lanes + tl_) * MT_WORDS, tw, lane); \
+            twist_wave(a.mt + ((int64_t)blockIdx.x * a.lanes + tl_) * MT_WORDS, lane);     \
             if (lane == tl_) midx = 0;                                                    \
         }                                                                                 \
         if (act_) {                                                                       \
@@ -641,12 +665,13 @@ __global__ void drl_synth_actions_kernel(uint64_t seed, uint64_t step, int64_t e
 // ---------------------------------------------------------------- launch ---
 template <int P>
 static hipError_t launch_step_t(const StepArgs& a, hipStream_t s, bool obs_only) {
-    const int envs_per_block = 4 * (64 / P);
+    const int envs_per_block = a.wpb * (64 / P);
     const int64_t blocks = (a.E + envs_per_block - 1) / envs_per_block;
+    const dim3 grid((unsigned)blocks), block(64 * a.wpb);
     if (obs_only)
-        hipLaunchKernelGGL(drl_obs_kernel<P>, dim3((unsigned)blocks), dim3(256), 4 * a.wave_lds, s, a);
+        hipLaunchKernelGGL(drl_obs_kernel<P>, grid, block, a.wpb * a.wave_lds, s, a);
     else
-        hipLaunchKernelGGL(drl_step_kernel<P>, dim3((unsigned)blocks), dim3(256), 4 * a.wave_lds, s, a);
+        hipLaunchKernelGGL(drl_step_kernel<P>, grid, block, a.wpb * a.wave_lds, s, a);
     return hipGetLastError();
 }
 

@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Interleaved in-process A/B timing of drl_step variants (methodology rule 24).
+
+python tools/ab.py --config c3 --rounds 5 --steps 100
+Variants: waves-per-block 1/2/4 (env DRL_WAVES_PER_BLOCK, read per call) and
+obs K=1 vs no obs.  Prints median/min µs per launch per variant.
+"""
+import argparse
+import ctypes
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+from bench import CONFIGS  # noqa: E402
+from dronerl_amd import BatchedDeliveryDrones, EnvParams  # noqa: E402
+from dronerl_amd._native import lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--variants", default="wpb1,wpb2,wpb4,wpb2_noobs")
+    args = ap.parse_args()
+    G, N, E, K = CONFIGS[args.config]
+    env = BatchedDeliveryDrones(EnvParams(n_drones=N, grid_size=G), E)
+    env.reset(seed=0)
+    T = args.steps
+    acts = torch.empty((T, E, N), dtype=torch.int32, device="cuda")
+    for t in range(T):
+        env.synth_actions(seed=5, step=t, out=acts[t])
+    W = env.layout.obs_window
+    rew = torch.empty((E, N), device="cuda")
+    dn = torch.empty((E, N), dtype=torch.uint8, device="cuda")
+    obs = torch.empty((E, K, W, W, 6), device="cuda")
+    L = lib()
+    cp, st = ctypes.byref(env._cp), env.state.c()
+    sp = ctypes.byref(st)
+    ap_ = [ctypes.c_void_p(acts[t].data_ptr()) for t in range(T)]
+    rp, dp, op = (ctypes.c_void_p(x.data_ptr()) for x in (rew, dn, obs))
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    variants = args.variants.split(",")
+    res = {v: [] for v in variants}
+    for v in variants + variants:  # warm every variant
+        pass
+    for r in range(args.rounds + 1):
+        for v in variants:
+            wpb = v.split("_")[0][3:]
+            os.environ["DRL_WAVES_PER_BLOCK"] = wpb
+            k = 0 if v.endswith("noobs") else K
+            o = op if k else None
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for t in range(T):
+                L.drl_step(cp, sp, ap_[t], rp, dp, o, k, None, s)
+            e1.record()
+            torch.cuda.synchronize()
+            if r:
+                res[v].append(e0.elapsed_time(e1) * 1e3 / T)
+    for v in variants:
+        x = res[v]
+        print(f"{args.config} {v:12s} median {statistics.median(x):8.2f} us  min {min(x):8.2f} us  "
+              f"-> {E / statistics.median(x) * 1e6:.3e} env-steps/s")
+
+
+if __name__ == "__main__":
+    main()
