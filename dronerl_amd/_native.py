@@ -53,6 +53,7 @@ class DrlState(ctypes.Structure):
         ("ground", ctypes.c_void_p),
         ("drones", ctypes.c_void_p),
         ("mt", ctypes.c_void_p),
+        ("mt_index", ctypes.c_void_p),
         ("num_envs", ctypes.c_int64),
     ]
 
@@ -90,7 +91,7 @@ def lib():
     for f in ["drl_layout_query", "drl_reset", "drl_step", "drl_obs", "drl_decode", "drl_encode",
               "drl_synth_actions"]:
         getattr(L, f).restype = ctypes.c_int
-    if L.drl_abi_version() != 1:
+    if L.drl_abi_version() != 2:
         raise DroneRLError("libdronerl.so ABI version mismatch; rebuild it")
     _lib = L
     return L

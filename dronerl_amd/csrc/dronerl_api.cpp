@@ -47,23 +47,45 @@ constexpr int kLdsMax = 160 * 1024;
 constexpr int kResetLdsTarget = 64 * 1024;
 
 int env_np(int n_drones) { return (n_drones + 7) / 8 * 8; }
+int r16(int v) { return (v + 15) / 16 * 16; }
 
-// LDS bytes per env in drl_step: ground + air map + MT prefetch + posidx
-int step_env_lds(int gstride, int n_drones) { return 2 * gstride + 4 * drl::MT_PF + 2 * env_np(n_drones); }
+// Per-env LDS regions of drl_step (see WaveLds in dronerl_kernels.hip)
+struct EnvLds {
+    int bm, paint, chg, nchg, fixed, scratch;
+};
+EnvLds env_lds(int gstride, int cells, int n_drones, int obs_k, int window) {
+    EnvLds e;
+    e.bm = r16((cells + 31) / 32 * 4);
+    e.paint = obs_k > 0 ? r16(obs_k * window * window) : 0;
+    e.nchg = 6 * n_drones + 2;
+    e.chg = r16(2 * e.nchg);
+    e.fixed = gstride + e.paint + 2 * env_np(n_drones);
+    e.scratch = e.bm + 4 * drl::MT_PF + e.chg + 16;
+    return e;
+}
+
+// LDS bytes per wave of drl_step: per-env regions + the scratch area, which
+// must also hold the observation transpose stage.
+int wave_lds_bytes(int gpw, const EnvLds& e, bool obs) {
+    int scratch = gpw * e.scratch;
+    if (obs && scratch < drl::OBS_U * 1536) scratch = drl::OBS_U * 1536;
+    return gpw * e.fixed + scratch;
+}
 
 // waves per block of drl_step (DRL_WAVES_PER_BLOCK overrides; 1, 2 or 4)
 int step_wpb() {
     const char* v = getenv("DRL_WAVES_PER_BLOCK");
-    const int w = v ? atoi(v) : 2;
-    return (w == 1 || w == 2 || w == 4) ? w : 2;
+    const int w = v ? atoi(v) : 1;
+    return (w == 1 || w == 2 || w == 4) ? w : 1;
 }
 
 // lanes per env in drl_step: pow2 >= n_drones (>= 4), widened when one wave
 // of narrower groups would not fit a quarter of the LDS target.
-int step_group_lanes(int n_drones, int gstride) {
+int step_group_lanes(int n_drones, int gstride, int cells, int window) {
     int P = 1;
     while (P < (n_drones < 4 ? 4 : n_drones)) P <<= 1;
-    while (P < 64 && (64 / P) * step_env_lds(gstride, n_drones) > kStepLdsTarget / 4) P <<= 1;
+    while (P < 64 && wave_lds_bytes(64 / P, env_lds(gstride, cells, n_drones, 1, window), true) > kStepLdsTarget / 4)
+        P <<= 1;
     return P;
 }
 
@@ -94,8 +116,9 @@ int validate(const drl_params* p, drl_layout* L) {
         L->mt_stride = DRL_MT_WORDS;
         L->obs_window = 2 * p->window_radius + 1;
         L->obs_floats = L->obs_window * L->obs_window * 6;
-        L->step_group_lanes = step_group_lanes(N, L->ground_stride);
-        L->step_lds_bytes = step_wpb() * (64 / L->step_group_lanes) * step_env_lds(L->ground_stride, N);
+        L->step_group_lanes = step_group_lanes(N, L->ground_stride, GG, L->obs_window);
+        L->step_lds_bytes =
+            wave_lds_bytes(64 / L->step_group_lanes, env_lds(L->ground_stride, GG, N, 1, L->obs_window), true);
         if (L->step_lds_bytes > kLdsMax) return fail("side %d needs %d B of LDS per block", p->side, L->step_lds_bytes);
     }
     return 0;
@@ -104,7 +127,7 @@ int validate(const drl_params* p, drl_layout* L) {
 int check_state(const drl_state* s, const drl_layout& L) {
     if (!s) return fail("state is NULL");
     if (s->num_envs < 0) return fail("num_envs < 0");
-    if (s->num_envs > 0 && (!s->ground || !s->drones || !s->mt)) return fail("state has NULL buffers");
+    if (s->num_envs > 0 && (!s->ground || !s->drones || !s->mt || !s->mt_index)) return fail("state has NULL buffers");
     if ((uintptr_t)s->ground % 16) return fail("ground must be 16-byte aligned");
     (void)L;
     return 0;
@@ -126,7 +149,7 @@ drl::ObsGeom obs_geom(const drl_params* p, const drl_layout& L, int k) {
     return g;
 }
 
-drl::StepArgs step_args(const drl_params* p, const drl_state* s, const drl_layout& L) {
+drl::StepArgs step_args(const drl_params* p, const drl_state* s, const drl_layout& L, int obs_k) {
     drl::StepArgs a;
     memset(&a, 0, sizeof a);
     a.side = p->side;
@@ -143,9 +166,21 @@ drl::StepArgs step_args(const drl_params* p, const drl_state* s, const drl_layou
     a.ground = s->ground;
     a.drones = s->drones;
     a.mt = s->mt;
-    a.wpb = step_wpb();
+    a.mt_index = s->mt_index;
+    const EnvLds e = env_lds(L.ground_stride, L.cells, p->n_drones, obs_k, L.obs_window);
     a.np = env_np(p->n_drones);
-    a.wave_lds = (64 / L.step_group_lanes) * step_env_lds(L.ground_stride, p->n_drones);
+    a.lds_bm = e.bm;
+    a.lds_paint = e.paint;
+    a.lds_chg = e.chg;
+    a.nchg = e.nchg;
+    a.obs_k = obs_k;
+    a.wave_lds = wave_lds_bytes(64 / L.step_group_lanes, e, obs_k > 0);
+    a.wpb = step_wpb();
+    {
+        const char* v = getenv("DRL_OBS_WIDE");
+        a.obs_wide = v ? atoi(v) : 1;
+    }
+    while (a.wpb > 1 && a.wpb * a.wave_lds > kLdsMax) a.wpb >>= 1;
     a.max_rounds = 1u << 20;
     a.div_side = drl::make_fastdiv((uint32_t)p->side);
     return a;
@@ -189,6 +224,7 @@ int drl_reset(const drl_params* p, const drl_state* s, int32_t reseed, uint64_t 
     a.ground = s->ground;
     a.drones = s->drones;
     a.mt = s->mt;
+    a.mt_index = s->mt_index;
     a.reseed = reseed ? 1 : 0;
     a.seed_base = seed_base;
     a.mask = d_env_mask;
@@ -217,7 +253,8 @@ int drl_step(const drl_params* p, const drl_state* s, const int32_t* d_actions, 
     if (!d_actions || !d_rewards || !d_dones) return fail("actions/rewards/dones must be non-NULL");
     if (d_obs && (obs_k < 1 || obs_k > p->n_drones)) return fail("obs_k %d outside [1, n_drones]", obs_k);
     if (d_obs && ((uintptr_t)d_obs % 16)) return fail("obs must be 16-byte aligned");
-    drl::StepArgs a = step_args(p, s, L);
+    drl::StepArgs a = step_args(p, s, L, d_obs ? obs_k : 0);
+    if (a.wave_lds > kLdsMax) return fail("obs_k %d needs %d B of LDS per wave", obs_k, a.wave_lds);
     a.actions = d_actions;
     a.rewards = d_rewards;
     a.dones = d_dones;
@@ -235,7 +272,8 @@ int drl_obs(const drl_params* p, const drl_state* s, int32_t k, float* d_obs, hi
     if (!d_obs) return fail("obs is NULL");
     if (k < 1 || k > p->n_drones) return fail("k %d outside [1, n_drones]", k);
     if ((uintptr_t)d_obs % 16) return fail("obs must be 16-byte aligned");
-    drl::StepArgs a = step_args(p, s, L);
+    drl::StepArgs a = step_args(p, s, L, k);
+    if (a.wave_lds > kLdsMax) return fail("k %d needs %d B of LDS per wave", k, a.wave_lds);
     a.obs = d_obs;
     a.og = obs_geom(p, L, k);
     hipError_t e = drl::launch_step(a, L.step_group_lanes, stream, true);

@@ -10,7 +10,8 @@ namespace drl {
 constexpr int MT_N = 624;
 constexpr int MT_M = 397;
 constexpr int MT_WORDS = DRL_MT_WORDS;
-constexpr int MT_PF = 32;       // MT words prefetched into LDS per env and step
+constexpr int MT_PF = 16;       // MT words prefetched into LDS per env and step
+constexpr int OBS_U = 2;        // observation cells per lane per pass (stage: OBS_U*1536 B per wave)
 
 enum : int { OBJ_EMPTY = 0, OBJ_SKYSCRAPER = 2, OBJ_STATION = 3, OBJ_DROPZONE = 4, OBJ_PACKET = 5 };
 
@@ -41,14 +42,21 @@ struct StepArgs {
     uint8_t* ground;
     uint32_t* drones;
     uint32_t* mt;
+    uint32_t* mt_index;
     const int32_t* actions;
     float* rewards;
     uint8_t* dones;
     float* obs;
     int32_t* err;
-    int wave_lds;  // LDS bytes per wave
-    int wpb;       // waves per block
-    int np;        // posidx entries per env (n_drones rounded up to 8)
+    int wave_lds;   // LDS bytes per wave
+    int wpb;        // waves per block
+    int np;         // posidx entries per env (n_drones rounded up to 8)
+    int lds_bm;     // bytes per env of the occupancy bitmap (16-B multiple)
+    int lds_paint;  // bytes per env of the observation paint buffer (16-B multiple)
+    int lds_chg;    // bytes per env of the changed-cell list (16-B multiple)
+    int nchg;       // changed-cell list capacity (entries)
+    int obs_k;      // observed drones (0: no observation)
+    int obs_wide;   // observation stores: 1 = 16-B via LDS transpose, 0 = 3 x 8-B per cell
     uint32_t max_rounds;
     FastDiv div_side;
     ObsGeom og;
@@ -61,6 +69,7 @@ struct ResetArgs {
     uint8_t* ground;
     uint32_t* drones;
     uint32_t* mt;
+    uint32_t* mt_index;
     int reseed;
     uint64_t seed_base;
     const uint8_t* mask;

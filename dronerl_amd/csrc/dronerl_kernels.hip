@@ -23,6 +23,24 @@
 
 namespace drl {
 
+// Diagnostic build only (-DDRL_STAMPS, tools/stamps.py): per-wave phase
+// timestamps (s_memtime) into a debug buffer.  Never compiled into the product.
+#ifdef DRL_STAMPS
+__device__ unsigned long long* g_stamps;
+#define DRL_STAMP(i)                                                                     \
+    do {                                                                                 \
+        __builtin_amdgcn_sched_barrier(0);                                               \
+        unsigned long long t_;                                                           \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
+        if (lane == 0) g_stamps[((int64_t)blockIdx.x * a.wpb + wave) * 8 + (i)] = t_;   \
+        __builtin_amdgcn_sched_barrier(0);                                               \
+    } while (0)
+#else
+#define DRL_STAMP(i) \
+    do {             \
+    } while (0)
+#endif
+
 // ---------------------------------------------------------------- helpers ---
 __device__ __forceinline__ void wave_sync() {
     // LDS traffic inside one wavefront is processed in order; this keeps the
@@ -99,86 +117,201 @@ __device__ __noinline__ void twist_wave(uint32_t* row, int lane) {
     wave_sync();
 }
 
-// ------------------------------------------------------- observation write ---
-// Per-wave LDS image of its envs (every region a multiple of 16 B):
-//   gl  [GPW][gstride] ground codes      al [GPW][gstride] air: 0 or (charge+1)|carry<<7
-//   mtw [GPW][PF] u32  prefetched MT words   posidx [GPW][NP] u16 cell of drone index k
+// ------------------------------------------------------------ LDS image ---
+// Per-wave LDS image of its GPW envs; every region is [GPW][stride] with
+// 16-byte strides (StepArgs::lds_*):
+//   gl     u8  [gstride]  ground codes (staged by LDS-DMA, env-major = HBM order)
+//   paint  u8  [K*W*W]    air byte (charge+1)|carry<<7 of drones inside each observed window
+//   posidx u16 [np]       cell of drone index k
+//   -- scratch, dead once the step is written back; the observation's
+//      transpose stage (OBS_U*1536 B per wave) aliases it --
+//   bm     u32 [bm]       drone-occupancy bitmap of the cells (respawn mask)
+//   mtw    u32 [MT_PF]    next MT words of the env's stream (prefetched)
+//   chg    u16 [nchg]     ground cells changed this step (written back as bytes)
+//   cnt    u32 [4]        chg count
 struct WaveLds {
     uint8_t* gl;
-    uint8_t* al;
-    uint32_t* mtw;
+    uint8_t* paint;
     uint16_t* posidx;
+    uint32_t* bm;
+    uint32_t* mtw;
+    uint16_t* chg;
+    uint32_t* cnt;
+    unsigned char* stage;
 };
 
-__device__ __forceinline__ WaveLds carve(unsigned char* wbase, int gpw, int gstride, int np) {
+__device__ __forceinline__ WaveLds carve(unsigned char* wb, int gpw, const StepArgs& a) {
     WaveLds w;
-    w.gl = wbase;
-    w.al = w.gl + gpw * gstride;
-    w.mtw = reinterpret_cast<uint32_t*>(w.al + gpw * gstride);
-    w.posidx = reinterpret_cast<uint16_t*>(w.mtw + gpw * MT_PF);
-    (void)np;
+    w.gl = wb;
+    wb += gpw * a.gstride;
+    w.paint = wb;
+    wb += gpw * a.lds_paint;
+    w.posidx = reinterpret_cast<uint16_t*>(wb);
+    wb += gpw * a.np * 2;
+    w.stage = wb;
+    w.bm = reinterpret_cast<uint32_t*>(wb);
+    wb += gpw * a.lds_bm;
+    w.mtw = reinterpret_cast<uint32_t*>(wb);
+    wb += gpw * MT_PF * 4;
+    w.chg = reinterpret_cast<uint16_t*>(wb);
+    wb += gpw * a.lds_chg;
+    w.cnt = reinterpret_cast<uint32_t*>(wb);
     return w;
 }
 
+// Async copy of the wave's grounds (contiguous in HBM, env-major) into LDS:
+// global_load_lds_dwordx4, 1 KiB per wave-instruction, no VGPR round trip.
+__device__ __forceinline__ void stage_ground_dma(const uint8_t* __restrict__ ground, int64_t wenv0, int nenv_w,
+                                                 int gstride, uint8_t* gl, int lane) {
+    const uint8_t* src = ground + wenv0 * gstride;
+    const int nvec = nenv_w * gstride / 16;
+    for (int v0 = 0; v0 < nvec; v0 += 64) {
+        if (v0 + lane < nvec)
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(src + (size_t)(v0 + lane) * 16),
+                (__attribute__((address_space(3))) void*)(gl + v0 * 16), 16, 0, 0);
+    }
+}
+
+// Zero [nbytes) of LDS (16-B multiple) cooperatively.
+__device__ __forceinline__ void lds_zero(void* p, int nbytes, int lane) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+    for (int v = lane; v < nbytes / 16; v += 64) q[v] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// ------------------------------------------------------- observation write ---
 // WindowedGridView windows (wrappers.py:10-31,55-73) of the wave's envs:
 // lane = one window cell; its 6 channels are computed branch-free and stored
 // as three 8-B pieces (consecutive lanes cover a contiguous span).  ch0 drone,
 // ch1 packet OR carrying drone, ch2 dropzone, ch3 station, ch4 charge/100
 // (true f32 division, == f32(double c/100)), ch5 skyscraper or wall.
 __device__ __forceinline__ void write_obs_wave(float* __restrict__ obs, int64_t wenv0, int nenv_w,
-                                               const ObsGeom& g, const WaveLds& w, int np, int lane) {
+                                               const ObsGeom& g, const WaveLds& w, const StepArgs& a, int lane) {
     const uint32_t win = g.W * g.W;
     const uint32_t env_cells = g.env_floats / 6u;  // K * W*W
     const uint32_t ncell = (uint32_t)nenv_w * env_cells;
     float* base = obs + wenv0 * (int64_t)g.env_floats;
-    for (uint32_t q = lane; q < ncell; q += 64) {
-        const uint32_t e = fdiv(q, g.div_env);
-        uint32_t rem = q - e * env_cells;
-        const uint32_t k = fdiv(rem, g.div_per);
-        rem -= k * win;
-        const uint32_t wy = fdiv(rem, g.div_w);
-        const uint32_t wx = rem - wy * g.W;
-        const uint32_t pos = w.posidx[e * np + k];
-        const uint32_t py = fdiv(pos, g.div_side);
-        const uint32_t px = pos - py * (uint32_t)g.side;
-        const int y = (int)(py + wy) - g.radius;
-        const int x = (int)(px + wx) - g.radius;
-        const bool in = (unsigned)y < (unsigned)g.side && (unsigned)x < (unsigned)g.side;
-        const uint32_t cell = e * g.gstride + (uint32_t)(y * g.side + x);
-        const uint32_t obj = in ? w.gl[cell] : (uint32_t)OBJ_SKYSCRAPER;
-        const uint32_t air = in ? w.al[cell] : 0u;
-        float2 v01, v23, v45;
-        v01.x = air ? 1.0f : 0.0f;
-        v01.y = (obj == OBJ_PACKET || (air & 0x80u)) ? 1.0f : 0.0f;
-        v23.x = obj == OBJ_DROPZONE ? 1.0f : 0.0f;
-        v23.y = obj == OBJ_STATION ? 1.0f : 0.0f;
-        v45.x = air ? (float)((int)(air & 0x7fu) - 1) / 100.0f : 0.0f;
-        v45.y = obj == OBJ_SKYSCRAPER ? 1.0f : 0.0f;
-        float2* o = reinterpret_cast<float2*>(base + 6u * q);
-        o[0] = v01;
-        o[1] = v23;
-        o[2] = v45;
+    // 16-B stores need a 16-B aligned wave base (always, unless one env per wave
+    // with an odd K*W*W); otherwise each lane stores its cell as 3 x 8 B.
+    const bool wide = a.obs_wide && ((uintptr_t)base & 15u) == 0;
+    for (uint32_t q0 = 0; q0 < ncell; q0 += 64 * OBS_U) {
+        uint32_t e[OBS_U], rem[OBS_U], wy[OBS_U], wx[OBS_U], pos[OBS_U];
+#pragma unroll
+        for (int u = 0; u < OBS_U; ++u) {
+            const uint32_t q = min(q0 + (uint32_t)(lane + 64 * u), ncell - 1u);
+            e[u] = fdiv(q, g.div_env);
+            rem[u] = q - e[u] * env_cells;
+            const uint32_t k = fdiv(rem[u], g.div_per);
+            const uint32_t c = rem[u] - k * win;
+            wy[u] = fdiv(c, g.div_w);
+            wx[u] = c - wy[u] * g.W;
+            pos[u] = w.posidx[e[u] * a.np + k];
+        }
+        float2 v[OBS_U][3];
+#pragma unroll
+        for (int u = 0; u < OBS_U; ++u) {
+            const uint32_t py = fdiv(pos[u], g.div_side);
+            const uint32_t px = pos[u] - py * (uint32_t)g.side;
+            const int y = (int)(py + wy[u]) - g.radius;
+            const int x = (int)(px + wx[u]) - g.radius;
+            const bool in = (unsigned)y < (unsigned)g.side && (unsigned)x < (unsigned)g.side;
+            const uint32_t o = w.gl[e[u] * g.gstride + (uint32_t)(in ? y * g.side + x : 0)];
+            const uint32_t obj = in ? o : (uint32_t)OBJ_SKYSCRAPER;
+            const uint32_t air = w.paint[e[u] * a.lds_paint + rem[u]];
+            v[u][0].x = air ? 1.0f : 0.0f;
+            v[u][0].y = (obj == OBJ_PACKET || (air & 0x80u)) ? 1.0f : 0.0f;
+            v[u][1].x = obj == OBJ_DROPZONE ? 1.0f : 0.0f;
+            v[u][1].y = obj == OBJ_STATION ? 1.0f : 0.0f;
+            v[u][2].x = air ? (float)((int)(air & 0x7fu) - 1) / 100.0f : 0.0f;
+            v[u][2].y = obj == OBJ_SKYSCRAPER ? 1.0f : 0.0f;
+        }
+        if (wide) {
+            // transpose through LDS: lane u*64+l's 24 B at stage[(u*64+l)*24], then 16-B stores
+            float2* st = reinterpret_cast<float2*>(w.stage);
+#pragma unroll
+            for (int u = 0; u < OBS_U; ++u) {
+                const int slot = (u * 64 + lane) * 3;
+                st[slot] = v[u][0];
+                st[slot + 1] = v[u][1];
+                st[slot + 2] = v[u][2];
+            }
+            wave_sync();
+            const uint32_t nbytes = min(ncell - q0, 64u * OBS_U) * 24u;
+            const uint4* sv = reinterpret_cast<const uint4*>(w.stage);
+            uint4* dst = reinterpret_cast<uint4*>(base + 6u * q0);
+            for (uint32_t t = lane; t * 16u < nbytes; t += 64) {
+                if (t * 16u + 16u <= nbytes) {
+                    dst[t] = sv[t];
+                } else {  // 8-byte tail
+                    reinterpret_cast<uint2*>(dst + t)[0] = reinterpret_cast<const uint2*>(sv + t)[0];
+                }
+            }
+            wave_sync();
+        } else {
+#pragma unroll
+            for (int u = 0; u < OBS_U; ++u) {
+                const uint32_t q = q0 + (uint32_t)(lane + 64 * u);
+                if (q < ncell) {
+                    float2* o = reinterpret_cast<float2*>(base + 6u * q);
+                    o[0] = v[u][0];
+                    o[1] = v[u][1];
+                    o[2] = v[u][2];
+                }
+            }
+        }
     }
 }
 
-// Stage a wave's grounds (contiguous, env-major) into LDS and clear the air map.
-__device__ __forceinline__ void stage_ground(const uint8_t* __restrict__ ground, int64_t wenv0, int nenv_w,
-                                             int gstride, const WaveLds& w, int lane) {
-    const uint4* src = reinterpret_cast<const uint4*>(ground + wenv0 * gstride);
-    const int nvec = nenv_w * gstride / 16;
-    for (int v = lane; v < nvec; v += 64) {
-        reinterpret_cast<uint4*>(w.gl)[v] = src[v];
-        reinterpret_cast<uint4*>(w.al)[v] = make_uint4(0u, 0u, 0u, 0u);
+// Each drone paints its air byte into every observed window (drone indices
+// 0..K-1) that contains it.  posidx must be final.
+__device__ __forceinline__ void paint_windows(uint8_t* paint, const uint16_t* posidx, int K, int y, int x,
+                                              uint8_t airbyte, const ObsGeom& g) {
+    const int W = (int)g.W;
+    for (int k = 0; k < K; ++k) {
+        const uint32_t pk = posidx[k];
+        const int pky = (int)fdiv(pk, g.div_side);
+        const int pkx = (int)pk - pky * g.side;
+        const int dy = y - pky + g.radius, dx = x - pkx + g.radius;
+        if ((unsigned)dy < (unsigned)W && (unsigned)dx < (unsigned)W) paint[k * W * W + dy * W + dx] = airbyte;
     }
 }
+
+__device__ __forceinline__ void chg_push(const WaveLds& w, int grp, int nchg_cap, int cell) {
+    const uint32_t q = atomicAdd(&w.cnt[grp * 4], 1u);
+    if (q < (uint32_t)nchg_cap) w.chg[grp * nchg_cap + q] = (uint16_t)cell;
+}
+
+__device__ __forceinline__ bool bm_test(const uint32_t* bm, int cell) { return (bm[cell >> 5] >> (cell & 31)) & 1u; }
+__device__ __forceinline__ void bm_set(uint32_t* bm, int cell) { atomicOr(&bm[cell >> 5], 1u << (cell & 31)); }
+
+// Group-relative lane masks: 32-bit when a group fits a 32-lane half.
+template <int P> struct GMaskT { using type = uint32_t; };
+template <> struct GMaskT<64> { using type = uint64_t; };
+
+template <int P>
+__device__ __forceinline__ typename GMaskT<P>::type gballot(bool pred, int gshift) {
+    using M = typename GMaskT<P>::type;
+    const uint64_t b = __ballot(pred);
+    if constexpr (P == 64) return b;
+    else return (M)(b >> gshift) & (M)((1ull << P) - 1ull);
+}
+__device__ __forceinline__ int popc(uint32_t m) { return __popc(m); }
+__device__ __forceinline__ int popc(uint64_t m) { return __popcll(m); }
+__device__ __forceinline__ int lobit(uint32_t m) { return __ffs(m) - 1; }
+__device__ __forceinline__ int lobit(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
+__device__ __forceinline__ int hibit(uint32_t m) { return 31 - __clz(m); }
+__device__ __forceinline__ int hibit(uint64_t m) { return 63 - __clzll((long long)m); }
 
 // ------------------------------------------------------------------ step ---
 template <int P>
 __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
+    using GMask = typename GMaskT<P>::type;
     constexpr int GPW = 64 / P;
+    constexpr int PFR = (MT_PF + P - 1) / P;   // prefetched MT words per lane
+    constexpr int CH = P < 16 ? P : 16;        // shuffle batch
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int grp = lane / P;
     const int j = lane % P;
     const int64_t wenv0 = ((int64_t)blockIdx.x * a.wpb + wave) * GPW;
@@ -186,26 +319,45 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
     if (nenv_w <= 0) return;  // no block-level barriers anywhere: whole idle waves may leave
     const int64_t env = wenv0 + grp;
     const bool env_ok = grp < nenv_w;
-    const int G = a.side, N = a.n_drones, gstride = a.gstride, np = a.np;
-    const WaveLds W = carve(smem + wave * a.wave_lds, GPW, gstride, np);
+    const int G = a.side, N = a.n_drones, gstride = a.gstride;
+    const WaveLds W = carve(smem + wave * a.wave_lds, GPW, a);
     uint8_t* gl = W.gl + grp * gstride;
-    uint8_t* al = W.al + grp * gstride;
+    uint32_t* bm = W.bm + grp * (a.lds_bm / 4);
     uint32_t* mtw = W.mtw + grp * MT_PF;
-    uint16_t* posidx = W.posidx + grp * np;
+    uint16_t* posidx = W.posidx + grp * a.np;
 
-    // ---- loads, all independent: drone record, this lane's action (by drone
-    // index j), the env's MT index, the ground (-> LDS)
+    DRL_STAMP(0);
+    // ---- loads.  The wave's MT indices are contiguous: scalar loads (lgkmcnt),
+    // so the MT-word prefetch that depends on them starts early.  Then the drone
+    // record and the action of drone index j, the MT words, and the ground by
+    // LDS-DMA; consumers of the MT words come last (respawn loop).
+    uint32_t mi[GPW];
+    if (nenv_w == GPW) {
+#pragma unroll
+        for (int g = 0; g < GPW; ++g) mi[g] = a.mt_index[wenv0 + g];
+    } else {
+#pragma unroll
+        for (int g = 0; g < GPW; ++g) mi[g] = a.mt_index[min(wenv0 + g, a.E - 1)];
+    }
+    int midx = MT_N;
+#pragma unroll
+    for (int g = 0; g < GPW; ++g) midx = (g == grp) ? (int)mi[g] : midx;
+    if (!env_ok) midx = MT_N;
     const bool active = env_ok && j < N;
     const uint32_t rec = active ? a.drones[env * N + j] : 0u;
     const int my_action = active ? a.actions[env * N + j] : 4;
     const uint32_t* mrow = a.mt + (env_ok ? env : 0) * MT_WORDS;
-    int midx = env_ok ? (int)mrow[MT_N] : MT_N;
-    stage_ground(a.ground, wenv0, nenv_w, gstride, W, lane);
-    // prefetch the next MT_PF words of the stream into LDS (dependent on midx only)
     const int pf_base0 = midx;
     int pfn = min(MT_PF, MT_N - midx);
-    for (int o = j; o < pfn; o += P) mtw[o] = mrow[midx + o];
+    uint32_t pfw[PFR];  // next MT words of the stream (addresses clamped: no per-word branch)
+#pragma unroll
+    for (int r = 0; r < PFR; ++r) pfw[r] = mrow[min(midx + j + P * r, MT_N - 1)];
+    stage_ground_dma(a.ground, wenv0, nenv_w, gstride, W.gl, lane);
+    lds_zero(W.bm, GPW * a.lds_bm, lane);
+    if (a.obs) lds_zero(W.paint, GPW * a.lds_paint, lane);
+    if (lane < GPW) W.cnt[lane * 4] = 0u;
 
+    DRL_STAMP(1);
     const int y = rec & 255u, x = (rec >> 8) & 255u;
     const int idx = ((int)(rec >> 25) < N) ? (int)(rec >> 25) : j;  // corrupt records never index out of bounds
     int c = (rec >> 16) & 255u;
@@ -222,27 +374,34 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
     const int ty = y + (act == 1) - (act == 3);
     const int tx = x + (act == 2) - (act == 0);
     const bool inb = active && ty >= 0 && ty < G && tx >= 0 && tx < G;
-    const int tcell = inb ? ty * G + tx : -1;
+    const int tcell = inb ? ty * G + tx : -1 - j;  // unique negatives never match
 
     // ---- phase 1 claims (env.py:124-140): first in O order claims a cell;
     // later ones crash (list A) and record the cell; OOB crashes (list A).
     bool earlier = false;
     int later_min = P;
 #pragma unroll
-    for (int s = 0; s < P; ++s) {
-        const int ts = __shfl(tcell, s, P);
-        if (inb && ts == tcell) {
-            if (s < j) earlier = true;
-            else if (s > j && s < later_min) later_min = s;
+    for (int s0 = 0; s0 < P; s0 += CH) {
+        int ts[CH];
+#pragma unroll
+        for (int t = 0; t < CH; ++t) ts[t] = __shfl(tcell, s0 + t, P);
+#pragma unroll
+        for (int t = 0; t < CH; ++t) {
+            const int s = s0 + t;
+            const bool same = ts[t] == tcell;
+            earlier |= same && s < j;
+            later_min = (same && s > j && s < later_min) ? s : later_min;
         }
     }
     const bool claimer = inb && !earlier;
     const bool crashA = active && !claimer;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ground DMA landed
     wave_sync();
 
+    DRL_STAMP(2);
     // ---- phase 2 effects on claimers (env.py:143-172), own cell only
     float reward = 0.0f;
-    bool dead = false, deliver = false, dirty = false;
+    bool dead = false, deliver = false;
     if (claimer) {
         const int obj = gl[tcell];
         if (obj == OBJ_STATION) {
@@ -256,13 +415,13 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
             reward = a.r_pickup;
             carry = 1;
             gl[tcell] = OBJ_EMPTY;
-            dirty = true;
+            chg_push(W, grp, a.nchg, tcell);
         } else if (obj == OBJ_DROPZONE && carry) {
             reward = a.r_delivery;
             carry = 0;
             gl[tcell] = OBJ_EMPTY;
             deliver = true;
-            dirty = true;
+            chg_push(W, grp, a.nchg, tcell);
         }
         if (obj == OBJ_SKYSCRAPER) dead = true;
     }
@@ -275,17 +434,23 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
     const bool survivor = claimer && !crashB;
     const bool crashed = crashA || crashB;
     const int gshift = grp * P;
-    const uint64_t gm = (P == 64) ? ~0ull : (((1ull << P) - 1ull) << gshift);
+    const uint64_t gm = (P == 64) ? ~0ull : (((1ull << (P & 63)) - 1ull) << gshift);
     const uint64_t lower = (1ull << lane) - 1ull;
     const uint64_t bS = __ballot(survivor) & gm;
     const uint64_t bA = __ballot(crashA) & gm;
     const uint64_t bB = __ballot(crashB) & gm;
     const int nS = __popcll(bS), nA = __popcll(bA), nR = nA + __popcll(bB);
     int rankB = 0;
-    if (bB) {
+    if (__ballot(crashB)) {
         const int bkey = crashB ? (collided ? later_min : P + j) : 4 * P;
 #pragma unroll
-        for (int s = 0; s < P; ++s) rankB += (__shfl(bkey, s, P) < bkey);
+        for (int s0 = 0; s0 < P; s0 += CH) {
+            int ks[CH];
+#pragma unroll
+            for (int t = 0; t < CH; ++t) ks[t] = __shfl(bkey, s0 + t, P);
+#pragma unroll
+            for (int t = 0; t < CH; ++t) rankB += (ks[t] < bkey);
+        }
     }
     const int newslot = survivor ? __popcll(bS & lower)
                                  : (crashA ? nS + __popcll(bA & lower) : (crashB ? nS + nA + rankB : j));
@@ -298,23 +463,32 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
         reward = a.r_crash;
     }
     int pos = survivor ? tcell : -1;
-    if (survivor) al[tcell] = 1;
-    bool gdirty = (__ballot(dirty) & gm) != 0ull;
+    if (survivor) bm_set(bm, tcell);
     wave_sync();
 
+    DRL_STAMP(3);
     // ---- respawns (env.py:186-210, _find_respawn_position :226-233):
     // items w < nR: crashed drones (mask: drones | skyscrapers); then n_pack
     // packets, then n_deliver dropzones (mask: any ground object).  Each round
     // draws P consecutive MT outputs, keeps those < side (randint(0, side-1)
-    // == _randbelow(side)), pairs accepted draws as (y, x) and takes the
-    // first pair whose cell is free.
+    // == _randbelow(side)) and pairs accepted draws as (y, x).  A placement
+    // always ends on the second draw of a pair, so the pairing is the same for
+    // every item: the round's candidate cells are read from LDS once and
+    // several items are placed per round, later items seeing the cells placed
+    // earlier in the round through register compares.
+#pragma unroll
+    for (int r = 0; r < PFR; ++r)
+        if (j + P * r < pfn) mtw[j + P * r] = pfw[r];
     int pf_base = pf_base0;
     int w = 0, have_y = 0, yv = 0;
     const int shift = 32 - a.kbits;
+    const int my_item = crashed ? newslot - nS : -1;  // this drone's respawn item
     uint32_t rounds = 0;
+    [[maybe_unused]] uint32_t rounds_w = 0;  // wave-level loop trips (diagnostics)
     for (;;) {
         const bool work = env_ok && w < total;
         if (!__ballot(work)) break;
+        ++rounds_w;
         uint64_t need = __ballot(work && j == 0 && midx >= MT_N);
         while (need) {
             const int tl = __ffsll((unsigned long long)need) - 1;
@@ -326,45 +500,72 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
                 pfn = 0;  // prefetched words are stale now
             }
         }
-        if (work) {
-            const int avail = MT_N - midx;
-            const bool valid = j < avail;
-            const int off = midx - pf_base + j;
-            uint32_t word = 0u;
-            if (valid) word = (off < pfn) ? mtw[off] : load_l2(mrow + midx + j);
-            const int r = valid ? (int)(temper(word) >> shift) : G;
-            const bool acc = valid && r < G;
-            const uint64_t accb = (__ballot(acc) & gm) >> gshift;
-            const uint64_t lowrel = (1ull << j) - 1ull;
-            const int apos = have_y + __popcll(accb & lowrel);
-            const uint64_t prevm = accb & lowrel;
-            const int prevlane = prevm ? 63 - __clzll((long long)prevm) : 0;
-            const int rprev = __shfl(r, prevlane, P);
-            const int ycand = prevm ? rprev : yv;
-            const bool cand = acc && (apos & 1);
-            const int ccell = ycand * G + r;
-            bool free_cell = false;
-            if (cand) {
-                const int obj = gl[ccell];
-                free_cell = (w < nR) ? (al[ccell] == 0 && obj != OBJ_SKYSCRAPER) : (obj == OBJ_EMPTY);
-            }
-            const uint64_t okb = (__ballot(cand && free_cell) & gm) >> gshift;
-            if (okb) {
-                const int js = __ffsll((unsigned long long)okb) - 1;
-                const int cell = __shfl(ccell, js, P);
-                if (w < nR) {
-                    if (crashed && newslot == nS + w) pos = cell;
-                    if (j == 0) al[cell] = 1;
+        // ---- one round: P consecutive draws of this env's stream (branch-free;
+        // groups without work compute and discard)
+        const int avail = MT_N - midx;
+        const bool valid = work && j < avail;
+        const int off = midx - pf_base + j;
+        const bool inpf = off < pfn;
+        uint32_t word = mtw[min(max(off, 0), MT_PF - 1)];
+        if (__ballot(valid && !inpf)) {  // beyond the prefetched words (rare)
+            const uint32_t g = (valid && !inpf) ? load_l2(mrow + midx + j) : 0u;
+            word = inpf ? word : g;
+        }
+        const int r = valid ? (int)(temper(word) >> shift) : G;
+        const bool acc = r < G;
+        const GMask accb = gballot<P>(acc, gshift);
+        const GMask lowrel = (GMask(1) << j) - GMask(1);
+        const GMask prevm = accb & lowrel;
+        const int apos = have_y + popc(prevm);
+        const int rprev = __shfl(r, prevm ? hibit(prevm) : 0, P);
+        const int ycand = prevm ? rprev : yv;
+        const bool cand = acc && (apos & 1);
+        const int cc = cand ? ycand * G + r : 0;
+        const int gobj = gl[cc];
+        const bool occ = bm_test(bm, cc);
+        GMask okd = gballot<P>(cand && !occ && gobj != OBJ_SKYSCRAPER, gshift);  // drone items
+        GMask okg = gballot<P>(cand && gobj == OBJ_EMPTY, gshift);              // packet / dropzone items
+        // ---- place as many items as this round's candidates allow: a placement
+        // ends on a pair's second draw, so the pairing holds for the next item;
+        // cells placed this round are removed from the masks by compare-ballots.
+        int last = -1;
+        bool more = work;
+        while (__ballot(more)) {
+            if (more) {
+                const bool isd = w < nR;
+                const GMask after = (last < 0) ? ~GMask(0) : ~((GMask(2) << last) - GMask(1));
+                const GMask m = (isd ? okd : okg) & after;
+                if (!m) {
+                    more = false;
                 } else {
-                    if (j == 0) gl[cell] = (w < nR + n_pack) ? OBJ_PACKET : OBJ_DROPZONE;
-                    gdirty = true;
+                    const int js = lobit(m);
+                    const int cell = __shfl(cc, js, P);
+                    const GMask same = gballot<P>(cand && cc == cell, gshift);
+                    if (isd) {
+                        pos = (my_item == w) ? cell : pos;
+                        if (j == 0) bm_set(bm, cell);
+                        okd &= ~same;
+                    } else {
+                        if (j == 0) {
+                            gl[cell] = (w < nR + n_pack) ? OBJ_PACKET : OBJ_DROPZONE;
+                            chg_push(W, grp, a.nchg, cell);
+                        }
+                        okg &= ~same;
+                    }
+                    last = js;
+                    ++w;
+                    more = w < total;
                 }
-                midx += js + 1;
-                ++w;
+            }
+        }
+        if (work) {
+            if (w >= total) {
+                midx += last + 1;  // draws after the last placement stay unconsumed
                 have_y = 0;
             } else {
-                const int cnt = have_y + __popcll(accb);
-                if (accb && (cnt & 1)) yv = __shfl(r, 63 - __clzll((long long)accb), P);
+                const int cnt = have_y + popc(accb);
+                const int yl = __shfl(r, accb ? hibit(accb) : 0, P);
+                if (accb && (cnt & 1)) yv = yl;
                 have_y = cnt & 1;
                 midx += min(P, avail);
             }
@@ -377,33 +578,49 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
         wave_sync();
     }
 
+    DRL_STAMP(4);
+#ifdef DRL_STAMPS
+    if (lane == 0) g_stamps[((int64_t)blockIdx.x * a.wpb + wave) * 8 + 7] = __builtin_amdgcn_readfirstlane(rounds_w);
+#endif
     // ---- _pick_packets_after_respawn (env.py:217-224): distinct cells, parallel
     if (active && pos < 0) pos = 0;  // unreachable for valid params (respawn always finds a cell)
     if (active && !carry && gl[pos] == OBJ_PACKET) {
         carry = 1;
         gl[pos] = OBJ_EMPTY;
-        dirty = true;
+        chg_push(W, grp, a.nchg, pos);
     }
-    gdirty |= (__ballot(dirty) & gm) != 0ull;
 
-    // ---- write back: records permuted to O', rewards/dones by drone index
+    // ---- write back: records permuted to O', rewards/dones by drone index,
+    // changed ground cells as bytes
+    const uint32_t py = fdiv((uint32_t)(pos > 0 ? pos : 0), a.div_side);
+    const uint32_t px = (uint32_t)(pos > 0 ? pos : 0) - py * (uint32_t)G;
     if (active) {
-        const uint32_t py = fdiv((uint32_t)pos, a.div_side);
-        const uint32_t px = (uint32_t)pos - py * (uint32_t)G;
         a.drones[env * N + newslot] = pack_drone((int)py, (int)px, c, carry, idx);
         a.rewards[env * N + idx] = reward;
         a.dones[env * N + idx] = crashed ? 1 : 0;
         posidx[idx] = (uint16_t)pos;
-        al[pos] = (uint8_t)((c + 1) | (carry << 7));
     }
-    if (env_ok && j == 0) a.mt[env * MT_WORDS + MT_N] = (uint32_t)midx;
+    if (env_ok && j == 0) a.mt_index[env] = (uint32_t)midx;
     wave_sync();
-    if (env_ok && gdirty) {
-        uint4* dst = reinterpret_cast<uint4*>(a.ground + env * gstride);
-        const uint4* src = reinterpret_cast<const uint4*>(gl);
-        for (int v = j; v < gstride / 16; v += P) dst[v] = src[v];
+    if (env_ok) {
+        const uint32_t nc = W.cnt[grp * 4];
+        const uint16_t* ch = W.chg + grp * a.nchg;
+        uint8_t* gdst = a.ground + env * gstride;
+        if (nc <= (uint32_t)a.nchg) {
+            for (uint32_t q = j; q < nc; q += P) gdst[ch[q]] = gl[ch[q]];
+        } else {  // cannot happen (<= 6N changes per step); whole-row fallback
+            for (int v = j; v < gstride / 16; v += P)
+                reinterpret_cast<uint4*>(gdst)[v] = reinterpret_cast<const uint4*>(gl)[v];
+        }
     }
-    if (a.obs) write_obs_wave(a.obs, wenv0, nenv_w, a.og, W, np, lane);
+    DRL_STAMP(5);
+    if (a.obs) {
+        if (active) paint_windows(W.paint + grp * a.lds_paint, posidx, a.obs_k, (int)py, (int)px,
+                                  (uint8_t)((c + 1) | (carry << 7)), a.og);
+        wave_sync();
+        write_obs_wave(a.obs, wenv0, nenv_w, a.og, W, a, lane);
+    }
+    DRL_STAMP(6);
 }
 
 // ------------------------------------------------------------ observation ---
@@ -420,20 +637,23 @@ __global__ void __launch_bounds__(256) drl_obs_kernel(StepArgs a) {
     if (nenv_w <= 0) return;
     const int64_t env = wenv0 + grp;
     const bool env_ok = grp < nenv_w;
-    const int N = a.n_drones, gstride = a.gstride, np = a.np;
-    const WaveLds W = carve(smem + wave * a.wave_lds, GPW, gstride, np);
-    stage_ground(a.ground, wenv0, nenv_w, gstride, W, lane);
+    const int N = a.n_drones;
+    const WaveLds W = carve(smem + wave * a.wave_lds, GPW, a);
+    stage_ground_dma(a.ground, wenv0, nenv_w, a.gstride, W.gl, lane);
+    lds_zero(W.paint, GPW * a.lds_paint, lane);
+    const bool active = env_ok && j < N;
+    const uint32_t rec = active ? a.drones[env * N + j] : 0u;
+    const int y = rec & 255u, x = (rec >> 8) & 255u;
+    const int c = (rec >> 16) & 255u, carry = (rec >> 24) & 1u;
+    const int idx = ((int)(rec >> 25) < N) ? (int)(rec >> 25) : j;
+    uint16_t* posidx = W.posidx + grp * a.np;
+    if (active) posidx[idx] = (uint16_t)(y * a.side + x);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
-    if (env_ok && j < N) {
-        const uint32_t rec = a.drones[env * N + j];
-        const int pos = (int)(rec & 255u) * a.side + (int)((rec >> 8) & 255u);
-        const int c = (rec >> 16) & 255u, carry = (rec >> 24) & 1u;
-        const int idx = ((int)(rec >> 25) < N) ? (int)(rec >> 25) : j;
-        W.posidx[grp * np + idx] = (uint16_t)pos;
-        W.al[grp * gstride + pos] = (uint8_t)((c + 1) | (carry << 7));
-    }
+    if (active) paint_windows(W.paint + grp * a.lds_paint, posidx, a.obs_k, y, x, (uint8_t)((c + 1) | (carry << 7)),
+                              a.og);
     wave_sync();
-    write_obs_wave(a.obs, wenv0, nenv_w, a.og, W, np, lane);
+    write_obs_wave(a.obs, wenv0, nenv_w, a.og, W, a, lane);
 }
 
 // ------------------------------------------------------------------ reset ---
@@ -512,7 +732,7 @@ __global__ void __launch_bounds__(64) drl_reset_kernel(ResetArgs a) {
         for (int i = 0; i < GG; ++i) list[i] = (uint16_t)i;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    int midx = own ? (a.reseed ? MT_N : (int)mrow[MT_N]) : MT_N;
+    int midx = own ? (a.reseed ? MT_N : (int)a.mt_index[env]) : MT_N;
     int n = GG;
 
     // Draw one tempered output for every participating lane; twists are
@@ -613,7 +833,7 @@ __global__ void __launch_bounds__(64) drl_reset_kernel(ResetArgs a) {
             const uint32_t py = fdiv((uint32_t)cell, a.div_side);
             a.drones[env * N + d] = pack_drone((int)py, cell - (int)py * a.side, 100, carry, d);
         }
-        mrow[MT_N] = (uint32_t)midx;
+        a.mt_index[env] = (uint32_t)midx;
     }
 }
 
@@ -685,6 +905,12 @@ hipError_t launch_step(const StepArgs& a, int P, hipStream_t s, bool obs_only) {
         default: return hipErrorInvalidValue;
     }
 }
+
+#ifdef DRL_STAMPS
+extern "C" int drl_debug_set_stamps(void* p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t launch_reset(const ResetArgs& a, hipStream_t s) {
     const int64_t blocks = (a.E + a.lanes - 1) / a.lanes;

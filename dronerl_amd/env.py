@@ -35,26 +35,29 @@ class DroneEnvState:
 
     ground : uint8 [E, ground_stride]  object code per cell, row-major (first side*side bytes)
     drones : int32 [E, n_drones]       packed u32 records in dict order O
-    mt     : int32 [E, 640]            CPython MT19937 words 0..623, [624] = index
+    mt     : int32 [E, 640]            CPython MT19937 state words 0..623
+    mt_index: int32 [E]                CPython's MT index (next word; 624 = twist first)
     """
     ground: torch.Tensor
     drones: torch.Tensor
     mt: torch.Tensor
+    mt_index: torch.Tensor
 
     @property
     def num_envs(self) -> int:
         return self.ground.shape[0]
 
     def c(self) -> DrlState:
-        return DrlState(self.ground.data_ptr(), self.drones.data_ptr(), self.mt.data_ptr(), self.num_envs)
+        return DrlState(self.ground.data_ptr(), self.drones.data_ptr(), self.mt.data_ptr(), self.mt_index.data_ptr(),
+                        self.num_envs)
 
     def clone(self) -> "DroneEnvState":
-        return DroneEnvState(self.ground.clone(), self.drones.clone(), self.mt.clone())
+        return DroneEnvState(self.ground.clone(), self.drones.clone(), self.mt.clone(), self.mt_index.clone())
 
     def narrow(self, start: int, length: int) -> "DroneEnvState":
         """A view of envs [start, start+length) (used for sharding and subsets)."""
         return DroneEnvState(self.ground.narrow(0, start, length), self.drones.narrow(0, start, length),
-                             self.mt.narrow(0, start, length))
+                             self.mt.narrow(0, start, length), self.mt_index.narrow(0, start, length))
 
 
 class BatchedDeliveryDrones:
@@ -85,6 +88,7 @@ class BatchedDeliveryDrones:
             ground=torch.zeros((E, L.ground_stride), dtype=torch.uint8, device=dev),
             drones=torch.zeros((E, L.drone_stride), dtype=torch.int32, device=dev),
             mt=torch.zeros((E, DRL_MT_WORDS), dtype=torch.int32, device=dev),
+            mt_index=torch.full((E,), 624, dtype=torch.int32, device=dev),
         )
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
 
@@ -159,7 +163,7 @@ class BatchedDeliveryDrones:
                                _ptr(out["x"]), _ptr(out["charge"]), _ptr(out["carrying"]), _stream(self.device)),
               "drl_decode")
         out["ground"] = self.state.ground[:, :G * G].view(E, G, G)
-        out["mt_index"] = self.state.mt[:, 624]
+        out["mt_index"] = self.state.mt_index
         return out
 
     def set_state(self, ground, order, y, x, charge, carrying, mt_words=None):
@@ -192,12 +196,14 @@ class BatchedDeliveryDrones:
         w = torch.where(w >= 2**31, w - 2**32, w).to(torch.int32)
         if w.shape[0] == 1:
             w = w.expand(self.num_envs, 625)
-        self.state.mt[:, :625].copy_(w.to(self.device))
+        w = w.to(self.device)
+        self.state.mt[:, :624].copy_(w[:, :624])
+        self.state.mt_index.copy_(w[:, 624])
 
     def mt_words(self):
-        """CPython-ordered MT words (uint32 values as Python ints) for every env."""
-        w = self.state.mt[:, :625].cpu().to(torch.int64) & 0xFFFFFFFF
-        return w
+        """CPython getstate() words (624 state words + index) per env, as int64 on the host."""
+        w = torch.cat([self.state.mt[:, :624], self.state.mt_index[:, None]], 1)
+        return w.cpu().to(torch.int64) & 0xFFFFFFFF
 
     def check_errors(self):
         """Synchronise and raise if a kernel flagged an error since the last check."""

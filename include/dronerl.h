@@ -41,8 +41,8 @@ extern "C" {
 
 typedef struct ihipStream_t* hipStream_t;
 
-#define DRL_ABI_VERSION 1
-#define DRL_MT_WORDS 640     /* per-env MT19937 record: words 0..623 state, [624] = index */
+#define DRL_ABI_VERSION 2
+#define DRL_MT_WORDS 640     /* per-env MT19937 row: words 0..623 state (row padded to 2560 B) */
 #define DRL_MAX_DRONES 64
 #define DRL_MAX_SIDE 128
 #define DRL_MAX_RADIUS 8
@@ -95,11 +95,14 @@ typedef struct drl_layout {
  *  ground : u8  [E][ground_stride]  object code per cell (row-major y*side+x)
  *  drones : u32 [E][n_drones]       one record per drone in dict order:
  *           bits 0-7 y, 8-15 x, 16-23 charge, 24 carrying, 25-31 drone index
- *  mt     : u32 [E][DRL_MT_WORDS]   CPython MT19937 state; word 624 = index */
+ *  mt     : u32 [E][DRL_MT_WORDS]   CPython MT19937 state words 0..623
+ *  mt_index: u32 [E]                CPython's MT index (next word; 624 = twist first),
+ *                                   kept apart so a wave's envs share one cache line */
 typedef struct drl_state {
     uint8_t* ground;
     uint32_t* drones;
     uint32_t* mt;
+    uint32_t* mt_index;
     int64_t num_envs;
 } drl_state;
 

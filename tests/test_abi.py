@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol():
     exported = set(re.findall(r"\s(drl_\w+)$", out, re.M))
     missing = [f for f in fns if f not in exported]
     assert not missing, missing
-    assert lib().drl_abi_version() == 1
+    assert lib().drl_abi_version() == 2
 
 
 def test_library_is_gfx950_code_object():
@@ -74,9 +74,9 @@ def test_layout_and_validation():
 def test_null_and_empty_calls_fail_cleanly():
     from dronerl_amd._native import DrlState
     p = EnvParams(n_drones=8, grid_size=16).to_c()
-    s = DrlState(None, None, None, 0)
+    s = DrlState(None, None, None, None, 0)
     assert lib().drl_step(ctypes.byref(p), ctypes.byref(s), None, None, None, None, 0, None, None) == 0
-    s = DrlState(None, None, None, 10)
+    s = DrlState(None, None, None, None, 10)
     assert lib().drl_step(ctypes.byref(p), ctypes.byref(s), None, None, None, None, 0, None, None) != 0
     assert b"NULL" in lib().drl_last_error()
 

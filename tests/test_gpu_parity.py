@@ -45,7 +45,7 @@ def oparams(p) -> OParams:
 def gpu_state(env, envs=None):
     d = env.decode()
     out = {k: d[k] for k in ["ground", "order", "y", "x", "charge", "carrying"]}
-    out["mt"] = env.state.mt[:, :625]
+    out["mt"] = torch.cat([env.state.mt[:, :624], env.state.mt_index[:, None]], 1)
     if envs is not None:
         idx = torch.as_tensor(envs, device=env.device)
         out = {k: v.index_select(0, idx) for k, v in out.items()}
@@ -238,7 +238,7 @@ def test_shard_invariance():
         rh = [h.step(h.synth_actions(seed=8, step=t)) for h in halves]
         assert torch.equal(rf, torch.cat([x[0] for x in rh]))
         assert torch.equal(df, torch.cat([x[1] for x in rh]))
-    for k in ["ground", "drones", "mt"]:
+    for k in ["ground", "drones", "mt", "mt_index"]:
         assert torch.equal(getattr(full.state, k), torch.cat([getattr(h.state, k) for h in halves]))
 
 

@@ -26,7 +26,8 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--variants", default="wpb1,wpb2,wpb4,wpb2_noobs")
+    ap.add_argument("--variants", default="wpb1,wpb2,wpb4,wpb2_noobs",
+                    help="comma list; each: wpbN[_noobs][_wide0|_wide1]")
     args = ap.parse_args()
     G, N, E, K = CONFIGS[args.config]
     env = BatchedDeliveryDrones(EnvParams(n_drones=N, grid_size=G), E)
@@ -51,9 +52,10 @@ def main():
         pass
     for r in range(args.rounds + 1):
         for v in variants:
-            wpb = v.split("_")[0][3:]
-            os.environ["DRL_WAVES_PER_BLOCK"] = wpb
-            k = 0 if v.endswith("noobs") else K
+            parts = v.split("_")
+            os.environ["DRL_WAVES_PER_BLOCK"] = parts[0][3:]
+            os.environ["DRL_OBS_WIDE"] = "0" if "wide0" in parts else "1"
+            k = 0 if "noobs" in parts else K
             o = op if k else None
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()

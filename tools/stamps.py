@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-phase wave timing of drl_step from s_memtime stamps.
+
+Builds a separate libdronerl_stamps.so (-DDRL_STAMPS; never the product
+library), runs the bench workload and prints mean/median phase durations
+(shader clocks) over waves:
+  0->1 loads + MT prefetch   1->2 claims/collision scan + DMA wait
+  2->3 effects + ordering    3->4 respawn rounds   4->5 write-back
+  5->6 observation
+"""
+import argparse
+import ctypes
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def build_stamps_lib():
+    from dronerl_amd import build as b
+    out = os.path.join(REPO, "dronerl_amd", "libdronerl_stamps.so")
+    cmd = [b.hipcc(), f"--offload-arch={b.ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DDRL_STAMPS",
+           "-I", os.path.join(REPO, "include"), "-o", out] + b.SOURCES
+    subprocess.run(cmd, check=True)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--envs", type=int, default=0)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--obs", type=int, default=1)
+    args = ap.parse_args()
+    path = build_stamps_lib()
+    import dronerl_amd._native as nat
+    nat.LIB_PATH = path
+    L = nat.lib()
+    L.drl_debug_set_stamps.argtypes = [ctypes.c_void_p]
+    from bench import CONFIGS
+    from dronerl_amd import BatchedDeliveryDrones, EnvParams
+    G, N, E, K = CONFIGS[args.config]
+    E = args.envs or E
+    K = args.obs
+    env = BatchedDeliveryDrones(EnvParams(n_drones=N, grid_size=G), E)
+    env.reset(seed=0)
+    P = env.layout.step_group_lanes
+    nwaves = (E + 64 // P - 1) // (64 // P)
+    stamps = torch.zeros((nwaves + 64, 8), dtype=torch.int64, device="cuda")
+    assert L.drl_debug_set_stamps(ctypes.c_void_p(stamps.data_ptr())) == 0
+    acc = []
+    rounds = []
+    for t in range(args.steps):
+        a = env.synth_actions(seed=1, step=t)
+        env.step(a, obs_k=K)
+        torch.cuda.synchronize()
+        st = stamps[:nwaves].cpu().numpy().astype(np.int64)
+        if t >= 2:
+            acc.append(np.diff(st[:, :7], axis=1))
+            rounds.append(st[:, 7].copy())
+        stamps.zero_()
+    d = np.concatenate(acc)
+    names = ["loads+MT prefetch", "claims+DMA wait", "effects+ordering", "respawn rounds", "write-back",
+             "observation"]
+    tot = d.sum(1)
+    print(f"{args.config} E={E} K={K}: wave lifetime (clk) mean {tot.mean():.0f} median {np.median(tot):.0f} "
+          f"p90 {np.percentile(tot, 90):.0f}")
+    rr = np.concatenate(rounds)
+    print(f"  respawn loop trips per wave: mean {rr.mean():.2f}  median {np.median(rr):.0f}  p90 "
+          f"{np.percentile(rr, 90):.0f}  max {rr.max()}  hist {np.bincount(rr, minlength=8)[:10].tolist()}")
+    for i, n in enumerate(names):
+        print(f"  {n:20s} mean {d[:, i].mean():8.0f}  median {np.median(d[:, i]):8.0f}  p90 "
+              f"{np.percentile(d[:, i], 90):8.0f}  share {d[:, i].mean() / tot.mean() * 100:5.1f}%")
+
+
+if __name__ == "__main__":
+    main()
