@@ -413,3 +413,13 @@ def test_compat_reference_golden_scripts():
     for t in range(len(g["multi_actions"])):
         draws = [sp.sample() for _ in range(8)]
         assert draws[1:] == g["multi_actions"][t][1:].tolist()
+
+
+def test_gpu_eval_runner_matches_oracle():
+    """eval_jax-style sharded evaluation on the GPU env == oracle episodes."""
+    from dronerl_amd.distributed import evaluate_sharded, gpu_episode_runner
+    from tests.test_distributed import oracle_runner
+    p = EnvParams(n_drones=3, grid_size=8)
+    g_agent, g_rnd, g_table = evaluate_sharded(gpu_episode_runner(p, 50, 100), num_evals=7)
+    o_agent, o_rnd, o_table = evaluate_sharded(oracle_runner(3, 8, 50, 100), num_evals=7)
+    np.testing.assert_allclose(g_table.cpu().numpy(), o_table.numpy(), rtol=0, atol=1e-6)
