@@ -53,14 +53,14 @@ int r16(int v) { return (v + 15) / 16 * 16; }
 struct EnvLds {
     int bm, paint, chg, nchg, fixed, scratch;
 };
-EnvLds env_lds(int gstride, int cells, int n_drones, int obs_k, int window) {
+EnvLds env_lds(int gstride, int cells, int n_drones, int obs_k, int window, int P) {
     EnvLds e;
     e.bm = r16((cells + 31) / 32 * 4);
     e.paint = obs_k > 0 ? r16(obs_k * window * window) : 0;
     e.nchg = 6 * n_drones + 2;
     e.chg = r16(2 * e.nchg);
     e.fixed = gstride + e.paint + 2 * env_np(n_drones);
-    e.scratch = e.bm + 4 * drl::MT_PF + e.chg + 16;
+    e.scratch = e.bm + 4 * drl::step_pf(P) + e.chg + 16;
     return e;
 }
 
@@ -72,19 +72,16 @@ int wave_lds_bytes(int gpw, const EnvLds& e, bool obs) {
     return gpw * e.fixed + scratch;
 }
 
-// waves per block of drl_step (DRL_WAVES_PER_BLOCK overrides; 1, 2 or 4)
-int step_wpb() {
-    const char* v = getenv("DRL_WAVES_PER_BLOCK");
-    const int w = v ? atoi(v) : 1;
-    return (w == 1 || w == 2 || w == 4) ? w : 1;
-}
+// waves per block of drl_step: one (kernels are __launch_bounds__(64); the
+// A/B of 1/2/4 waves per block measured 1 fastest)
+int step_wpb() { return 1; }
 
 // lanes per env in drl_step: pow2 >= n_drones (>= 4), widened when one wave
 // of narrower groups would not fit a quarter of the LDS target.
 int step_group_lanes(int n_drones, int gstride, int cells, int window) {
     int P = 1;
     while (P < (n_drones < 4 ? 4 : n_drones)) P <<= 1;
-    while (P < 64 && wave_lds_bytes(64 / P, env_lds(gstride, cells, n_drones, 1, window), true) > kStepLdsTarget / 4)
+    while (P < 64 && wave_lds_bytes(64 / P, env_lds(gstride, cells, n_drones, 1, window, P), true) > kStepLdsTarget / 4)
         P <<= 1;
     return P;
 }
@@ -118,7 +115,8 @@ int validate(const drl_params* p, drl_layout* L) {
         L->obs_floats = L->obs_window * L->obs_window * 6;
         L->step_group_lanes = step_group_lanes(N, L->ground_stride, GG, L->obs_window);
         L->step_lds_bytes =
-            wave_lds_bytes(64 / L->step_group_lanes, env_lds(L->ground_stride, GG, N, 1, L->obs_window), true);
+            wave_lds_bytes(64 / L->step_group_lanes,
+                           env_lds(L->ground_stride, GG, N, 1, L->obs_window, L->step_group_lanes), true);
         if (L->step_lds_bytes > kLdsMax) return fail("side %d needs %d B of LDS per block", p->side, L->step_lds_bytes);
     }
     return 0;
@@ -167,7 +165,7 @@ drl::StepArgs step_args(const drl_params* p, const drl_state* s, const drl_layou
     a.drones = s->drones;
     a.mt = s->mt;
     a.mt_index = s->mt_index;
-    const EnvLds e = env_lds(L.ground_stride, L.cells, p->n_drones, obs_k, L.obs_window);
+    const EnvLds e = env_lds(L.ground_stride, L.cells, p->n_drones, obs_k, L.obs_window, L.step_group_lanes);
     a.np = env_np(p->n_drones);
     a.lds_bm = e.bm;
     a.lds_paint = e.paint;
@@ -179,6 +177,8 @@ drl::StepArgs step_args(const drl_params* p, const drl_state* s, const drl_layou
     {
         const char* v = getenv("DRL_OBS_WIDE");
         a.obs_wide = v ? atoi(v) : 1;
+        const char* st = getenv("DRL_STAGGER");
+        a.stagger = st ? atoi(st) : 0;
     }
     while (a.wpb > 1 && a.wpb * a.wave_lds > kLdsMax) a.wpb >>= 1;
     a.max_rounds = 1u << 20;

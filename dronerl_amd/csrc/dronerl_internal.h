@@ -10,8 +10,11 @@ namespace drl {
 constexpr int MT_N = 624;
 constexpr int MT_M = 397;
 constexpr int MT_WORDS = DRL_MT_WORDS;
-constexpr int MT_PF = 16;       // MT words prefetched into LDS per env and step
-constexpr int OBS_U = 2;        // observation cells per lane per pass (stage: OBS_U*1536 B per wave)
+// respawn rounds: D draws per lane (D*P MT outputs per round); the first
+// round's words (>= 16) are prefetched into LDS with the step's other loads
+constexpr int step_draws(int P) { return P <= 16 ? 2 : 1; }
+constexpr int step_pf(int P) { return step_draws(P) * P < 16 ? 16 : step_draws(P) * P; }
+constexpr int OBS_U = 1;        // observation cells per lane per pass (stage: OBS_U*1536 B per wave)
 
 enum : int { OBJ_EMPTY = 0, OBJ_SKYSCRAPER = 2, OBJ_STATION = 3, OBJ_DROPZONE = 4, OBJ_PACKET = 5 };
 
@@ -57,6 +60,7 @@ struct StepArgs {
     int nchg;       // changed-cell list capacity (entries)
     int obs_k;      // observed drones (0: no observation)
     int obs_wide;   // observation stores: 1 = 16-B via LDS transpose, 0 = 3 x 8-B per cell
+    int stagger;    // diagnostic: s_sleep(127) x (block & 3) x stagger before starting (0 = off)
     uint32_t max_rounds;
     FastDiv div_side;
     ObsGeom og;

@@ -32,7 +32,10 @@ __device__ unsigned long long* g_stamps;
         __builtin_amdgcn_sched_barrier(0);                                               \
         unsigned long long t_;                                                           \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
-        if (lane == 0) g_stamps[((int64_t)blockIdx.x * a.wpb + wave) * 8 + (i)] = t_;   \
+        if (lane == 0) g_stamps[((int64_t)blockIdx.x * a.wpb + wave) * 16 + (i)] = t_;  \
+        if (lane == 0 && ((i) == 0 || (i) == 6))                                         \
+            g_stamps[((int64_t)blockIdx.x * a.wpb + wave) * 16 + 8 + (i) / 6] =          \
+                __builtin_amdgcn_s_memrealtime();                                        \
         __builtin_amdgcn_sched_barrier(0);                                               \
     } while (0)
 #else
@@ -126,7 +129,7 @@ __device__ __noinline__ void twist_wave(uint32_t* row, int lane) {
 //   -- scratch, dead once the step is written back; the observation's
 //      transpose stage (OBS_U*1536 B per wave) aliases it --
 //   bm     u32 [bm]       drone-occupancy bitmap of the cells (respawn mask)
-//   mtw    u32 [MT_PF]    next MT words of the env's stream (prefetched)
+//   mtw    u32 [pf]       next MT words of the env's stream (prefetched, step_pf(P))
 //   chg    u16 [nchg]     ground cells changed this step (written back as bytes)
 //   cnt    u32 [4]        chg count
 struct WaveLds {
@@ -140,7 +143,7 @@ struct WaveLds {
     unsigned char* stage;
 };
 
-__device__ __forceinline__ WaveLds carve(unsigned char* wb, int gpw, const StepArgs& a) {
+__device__ __forceinline__ WaveLds carve(unsigned char* wb, int gpw, int pf, const StepArgs& a) {
     WaveLds w;
     w.gl = wb;
     wb += gpw * a.gstride;
@@ -152,7 +155,7 @@ __device__ __forceinline__ WaveLds carve(unsigned char* wb, int gpw, const StepA
     w.bm = reinterpret_cast<uint32_t*>(wb);
     wb += gpw * a.lds_bm;
     w.mtw = reinterpret_cast<uint32_t*>(wb);
-    wb += gpw * MT_PF * 4;
+    wb += gpw * pf * 4;
     w.chg = reinterpret_cast<uint16_t*>(wb);
     wb += gpw * a.lds_chg;
     w.cnt = reinterpret_cast<uint32_t*>(wb);
@@ -285,7 +288,7 @@ __device__ __forceinline__ bool bm_test(const uint32_t* bm, int cell) { return (
 __device__ __forceinline__ void bm_set(uint32_t* bm, int cell) { atomicOr(&bm[cell >> 5], 1u << (cell & 31)); }
 
 // Group-relative lane masks: 32-bit when a group fits a 32-lane half.
-template <int P> struct GMaskT { using type = uint32_t; };
+template <int P> struct GMaskT { using type = uint32_t; };  // P <= 32
 template <> struct GMaskT<64> { using type = uint64_t; };
 
 template <int P>
@@ -303,11 +306,19 @@ __device__ __forceinline__ int hibit(uint32_t m) { return 31 - __clz(m); }
 __device__ __forceinline__ int hibit(uint64_t m) { return 63 - __clzll((long long)m); }
 
 // ------------------------------------------------------------------ step ---
+// One wave per block.  P <= 8 (small grids, LDS <= 5 KB/wave): cap registers
+// at 64 so 8 waves fit a SIMD and every wave of a 65536-env C3 launch is
+// resident at once (at 6 waves/SIMD a second, tail-heavy generation formed).
+// Wider groups are LDS-limited below 8 waves/SIMD: no cap (it only spilled).
 template <int P>
-__global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : 1, 8)))
+drl_step_kernel(StepArgs a) {
     using GMask = typename GMaskT<P>::type;
     constexpr int GPW = 64 / P;
-    constexpr int PFR = (MT_PF + P - 1) / P;   // prefetched MT words per lane
+    constexpr int D = step_draws(P);             // draws per lane per respawn round
+    constexpr int PF = step_pf(P);               // prefetched MT words per env
+    constexpr int PFR = (PF + P - 1) / P;        // prefetched MT words per lane
+    using CM = typename GMaskT<(P * D <= 32 ? 32 : 64)>::type;  // round-position masks
     constexpr int CH = P < 16 ? P : 16;        // shuffle batch
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
@@ -320,12 +331,16 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
     const int64_t env = wenv0 + grp;
     const bool env_ok = grp < nenv_w;
     const int G = a.side, N = a.n_drones, gstride = a.gstride;
-    const WaveLds W = carve(smem + wave * a.wave_lds, GPW, a);
+    const WaveLds W = carve(smem + wave * a.wave_lds, GPW, PF, a);
     uint8_t* gl = W.gl + grp * gstride;
     uint32_t* bm = W.bm + grp * (a.lds_bm / 4);
-    uint32_t* mtw = W.mtw + grp * MT_PF;
+    uint32_t* mtw = W.mtw + grp * PF;
     uint16_t* posidx = W.posidx + grp * a.np;
 
+    if (a.stagger) {  // diagnostic knob (DRL_STAGGER): desynchronise waves' phases
+        const int n = (int)(blockIdx.x & 3u) * a.stagger;
+        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+    }
     DRL_STAMP(0);
     // ---- loads.  The wave's MT indices are contiguous: scalar loads (lgkmcnt),
     // so the MT-word prefetch that depends on them starts early.  Then the drone
@@ -348,7 +363,7 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
     const int my_action = active ? a.actions[env * N + j] : 4;
     const uint32_t* mrow = a.mt + (env_ok ? env : 0) * MT_WORDS;
     const int pf_base0 = midx;
-    int pfn = min(MT_PF, MT_N - midx);
+    int pfn = min(PF, MT_N - midx);
     uint32_t pfw[PFR];  // next MT words of the stream (addresses clamped: no per-word branch)
 #pragma unroll
     for (int r = 0; r < PFR; ++r) pfw[r] = mrow[min(midx + j + P * r, MT_N - 1)];
@@ -500,31 +515,58 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
                 pfn = 0;  // prefetched words are stale now
             }
         }
-        // ---- one round: P consecutive draws of this env's stream (branch-free;
-        // groups without work compute and discard)
+        // ---- one round: D*P consecutive draws of this env's stream; position
+        // d = q*P + j is lane j's q-th draw (branch-free; groups without work
+        // compute and discard)
         const int avail = MT_N - midx;
-        const bool valid = work && j < avail;
-        const int off = midx - pf_base + j;
-        const bool inpf = off < pfn;
-        uint32_t word = mtw[min(max(off, 0), MT_PF - 1)];
-        if (__ballot(valid && !inpf)) {  // beyond the prefetched words (rare)
-            const uint32_t g = (valid && !inpf) ? load_l2(mrow + midx + j) : 0u;
-            word = inpf ? word : g;
+        int rq[D], ccq[D];
+        bool candq[D], accq[D];
+        GMask mq[D];
+        CM accall = 0;
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+            const int d = q * P + j;
+            const bool valid = work && d < avail;
+            const int off = midx - pf_base + d;
+            const bool inpf = off < pfn;
+            uint32_t word = mtw[min(max(off, 0), PF - 1)];
+            if (__ballot(valid && !inpf)) {  // beyond the prefetched words (rare)
+                const uint32_t g = (valid && !inpf) ? load_l2(mrow + midx + d) : 0u;
+                word = inpf ? word : g;
+            }
+            rq[q] = valid ? (int)(temper(word) >> shift) : G;
+            accq[q] = rq[q] < G;
+            mq[q] = gballot<P>(accq[q], gshift);
+            accall |= CM(mq[q]) << (q * P);
         }
-        const int r = valid ? (int)(temper(word) >> shift) : G;
-        const bool acc = r < G;
-        const GMask accb = gballot<P>(acc, gshift);
-        const GMask lowrel = (GMask(1) << j) - GMask(1);
-        const GMask prevm = accb & lowrel;
-        const int apos = have_y + popc(prevm);
-        const int rprev = __shfl(r, prevm ? hibit(prevm) : 0, P);
-        const int ycand = prevm ? rprev : yv;
-        const bool cand = acc && (apos & 1);
-        const int cc = cand ? ycand * G + r : 0;
-        const int gobj = gl[cc];
-        const bool occ = bm_test(bm, cc);
-        GMask okd = gballot<P>(cand && !occ && gobj != OBJ_SKYSCRAPER, gshift);  // drone items
-        GMask okg = gballot<P>(cand && gobj == OBJ_EMPTY, gshift);              // packet / dropzone items
+        // value r at a round position (group-uniform b)
+        auto r_at = [&](int b) {
+            int v = __shfl(rq[0], b % P, P);
+#pragma unroll
+            for (int q = 1; q < D; ++q) {
+                const int vq = __shfl(rq[q], b % P, P);
+                v = (b / P == q) ? vq : v;
+            }
+            return v;
+        };
+        GMask okd = 0, okg = 0;
+        CM okdc = 0, okgc = 0;
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+            const CM prevm = accall & ((CM(1) << (q * P + j)) - CM(1));
+            const int apos = have_y + popc(prevm);
+            const int pl = prevm ? hibit(prevm) : 0;
+            const int rp = r_at(pl);
+            const int ycand = prevm ? rp : yv;
+            candq[q] = accq[q] && (apos & 1);
+            ccq[q] = candq[q] ? ycand * G + rq[q] : 0;
+            const int gobj = gl[ccq[q]];
+            const bool occ = bm_test(bm, ccq[q]);
+            okd = gballot<P>(candq[q] && !occ && gobj != OBJ_SKYSCRAPER, gshift);  // drone items
+            okg = gballot<P>(candq[q] && gobj == OBJ_EMPTY, gshift);              // packet / dropzone items
+            okdc |= CM(okd) << (q * P);
+            okgc |= CM(okg) << (q * P);
+        }
         // ---- place as many items as this round's candidates allow: a placement
         // ends on a pair's second draw, so the pairing holds for the next item;
         // cells placed this round are removed from the masks by compare-ballots.
@@ -533,26 +575,33 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
         while (__ballot(more)) {
             if (more) {
                 const bool isd = w < nR;
-                const GMask after = (last < 0) ? ~GMask(0) : ~((GMask(2) << last) - GMask(1));
-                const GMask m = (isd ? okd : okg) & after;
+                const CM after = (last < 0) ? ~CM(0) : ~((CM(2) << last) - CM(1));
+                const CM m = (isd ? okdc : okgc) & after;
                 if (!m) {
                     more = false;
                 } else {
-                    const int js = lobit(m);
-                    const int cell = __shfl(cc, js, P);
-                    const GMask same = gballot<P>(cand && cc == cell, gshift);
+                    const int b = lobit(m);
+                    int cell = __shfl(ccq[0], b % P, P);
+#pragma unroll
+                    for (int q = 1; q < D; ++q) {
+                        const int cq = __shfl(ccq[q], b % P, P);
+                        cell = (b / P == q) ? cq : cell;
+                    }
+                    CM same = 0;
+#pragma unroll
+                    for (int q = 0; q < D; ++q) same |= CM(gballot<P>(candq[q] && ccq[q] == cell, gshift)) << (q * P);
                     if (isd) {
                         pos = (my_item == w) ? cell : pos;
                         if (j == 0) bm_set(bm, cell);
-                        okd &= ~same;
+                        okdc &= ~same;
                     } else {
                         if (j == 0) {
                             gl[cell] = (w < nR + n_pack) ? OBJ_PACKET : OBJ_DROPZONE;
                             chg_push(W, grp, a.nchg, cell);
                         }
-                        okg &= ~same;
+                        okgc &= ~same;
                     }
-                    last = js;
+                    last = b;
                     ++w;
                     more = w < total;
                 }
@@ -563,11 +612,11 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
                 midx += last + 1;  // draws after the last placement stay unconsumed
                 have_y = 0;
             } else {
-                const int cnt = have_y + popc(accb);
-                const int yl = __shfl(r, accb ? hibit(accb) : 0, P);
-                if (accb && (cnt & 1)) yv = yl;
+                const int cnt = have_y + popc(accall);
+                const int yl = r_at(accall ? hibit(accall) : 0);
+                if (accall && (cnt & 1)) yv = yl;
                 have_y = cnt & 1;
-                midx += min(P, avail);
+                midx += min(D * P, avail);
             }
             if (++rounds > a.max_rounds) {  // full grid: the reference spins forever
                 if (j == 0 && a.err) atomicOr(a.err, DRL_ERR_NO_FREE_CELL);
@@ -580,7 +629,7 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
 
     DRL_STAMP(4);
 #ifdef DRL_STAMPS
-    if (lane == 0) g_stamps[((int64_t)blockIdx.x * a.wpb + wave) * 8 + 7] = __builtin_amdgcn_readfirstlane(rounds_w);
+    if (lane == 0) g_stamps[((int64_t)blockIdx.x * a.wpb + wave) * 16 + 7] = __builtin_amdgcn_readfirstlane(rounds_w);
 #endif
     // ---- _pick_packets_after_respawn (env.py:217-224): distinct cells, parallel
     if (active && pos < 0) pos = 0;  // unreachable for valid params (respawn always finds a cell)
@@ -625,7 +674,7 @@ __global__ void __launch_bounds__(256) drl_step_kernel(StepArgs a) {
 
 // ------------------------------------------------------------ observation ---
 template <int P>
-__global__ void __launch_bounds__(256) drl_obs_kernel(StepArgs a) {
+__global__ void __launch_bounds__(64) drl_obs_kernel(StepArgs a) {
     constexpr int GPW = 64 / P;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
@@ -638,7 +687,7 @@ __global__ void __launch_bounds__(256) drl_obs_kernel(StepArgs a) {
     const int64_t env = wenv0 + grp;
     const bool env_ok = grp < nenv_w;
     const int N = a.n_drones;
-    const WaveLds W = carve(smem + wave * a.wave_lds, GPW, a);
+    const WaveLds W = carve(smem + wave * a.wave_lds, GPW, step_pf(P), a);
     stage_ground_dma(a.ground, wenv0, nenv_w, a.gstride, W.gl, lane);
     lds_zero(W.paint, GPW * a.lds_paint, lane);
     const bool active = env_ok && j < N;

@@ -55,6 +55,7 @@ def main():
             parts = v.split("_")
             os.environ["DRL_WAVES_PER_BLOCK"] = parts[0][3:]
             os.environ["DRL_OBS_WIDE"] = "0" if "wide0" in parts else "1"
+            os.environ["DRL_STAGGER"] = next((x[2:] for x in parts if x.startswith("st")), "0")
             k = 0 if "noobs" in parts else K
             o = op if k else None
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -51,7 +51,7 @@ def main():
     env.reset(seed=0)
     P = env.layout.step_group_lanes
     nwaves = (E + 64 // P - 1) // (64 // P)
-    stamps = torch.zeros((nwaves + 64, 8), dtype=torch.int64, device="cuda")
+    stamps = torch.zeros((nwaves + 64, 16), dtype=torch.int64, device="cuda")
     assert L.drl_debug_set_stamps(ctypes.c_void_p(stamps.data_ptr())) == 0
     acc = []
     rounds = []
@@ -63,7 +63,19 @@ def main():
         if t >= 2:
             acc.append(np.diff(st[:, :7], axis=1))
             rounds.append(st[:, 7].copy())
-        stamps.zero_()
+        if t == args.steps - 1:
+            # s_memrealtime (100 MHz, chip-wide) at wave start / end
+            rs, re_ = st[:, 8], st[:, 9]
+            t0 = rs.min()
+            starts, ends = (rs - t0) / 100.0, (re_ - t0) / 100.0  # us
+            span = ends.max()
+            life = ends - starts
+            print(f"launch span {span:.1f} us; wave start p10/50/90/max {np.percentile(starts, 10):.1f}/"
+                  f"{np.percentile(starts, 50):.1f}/{np.percentile(starts, 90):.1f}/{starts.max():.1f} us; "
+                  f"wave lifetime p10/50/90 {np.percentile(life, 10):.1f}/{np.percentile(life, 50):.1f}/"
+                  f"{np.percentile(life, 90):.1f} us")
+            conc = [int(((starts <= x) & (ends > x)).sum()) for x in np.linspace(0, span, 12)]
+            print(f"  resident waves over the span (12 samples): {conc}")
     d = np.concatenate(acc)
     names = ["loads+MT prefetch", "claims+DMA wait", "effects+ordering", "respawn rounds", "write-back",
              "observation"]
