@@ -46,8 +46,8 @@ constexpr int kStepLdsTarget = 64 * 1024;   // per block
 constexpr int kLdsMax = 160 * 1024;
 constexpr int kResetLdsTarget = 64 * 1024;
 
-int env_np(int n_drones) { return (n_drones + 7) / 8 * 8; }
-int r16(int v) { return (v + 15) / 16 * 16; }
+using drl::lay::r16;
+int env_np(int n_drones) { return drl::lay::np(n_drones); }
 
 // Per-env LDS regions of drl_step (see WaveLds in dronerl_kernels.hip)
 struct EnvLds {
@@ -55,10 +55,10 @@ struct EnvLds {
 };
 EnvLds env_lds(int gstride, int cells, int n_drones, int obs_k, int window, int P) {
     EnvLds e;
-    e.bm = r16((cells + 31) / 32 * 4);
-    e.paint = obs_k > 0 ? r16(obs_k * window * window) : 0;
-    e.nchg = 6 * n_drones + 2;
-    e.chg = r16(2 * e.nchg);
+    e.bm = drl::lay::bm_bytes(cells);
+    e.paint = drl::lay::paint_bytes(obs_k, window);
+    e.nchg = drl::lay::nchg(n_drones);
+    e.chg = drl::lay::chg_bytes(n_drones);
     e.fixed = gstride + e.paint + 2 * env_np(n_drones);
     e.scratch = e.bm + 4 * drl::step_pf(P) + e.chg + 16;
     return e;
@@ -71,10 +71,6 @@ int wave_lds_bytes(int gpw, const EnvLds& e, bool obs) {
     if (obs && scratch < drl::OBS_U * 1536) scratch = drl::OBS_U * 1536;
     return gpw * e.fixed + scratch;
 }
-
-// waves per block of drl_step: one (kernels are __launch_bounds__(64); the
-// A/B of 1/2/4 waves per block measured 1 fastest)
-int step_wpb() { return 1; }
 
 // lanes per env in drl_step: pow2 >= n_drones (>= 4), widened when one wave
 // of narrower groups would not fit a quarter of the LDS target.
@@ -108,7 +104,7 @@ int validate(const drl_params* p, drl_layout* L) {
         L->side = p->side;
         L->n_drones = N;
         L->cells = GG;
-        L->ground_stride = (GG + 15) / 16 * 16;
+        L->ground_stride = drl::lay::gstride(p->side);
         L->drone_stride = N;
         L->mt_stride = DRL_MT_WORDS;
         L->obs_window = 2 * p->window_radius + 1;
@@ -173,14 +169,14 @@ drl::StepArgs step_args(const drl_params* p, const drl_state* s, const drl_layou
     a.nchg = e.nchg;
     a.obs_k = obs_k;
     a.wave_lds = wave_lds_bytes(64 / L.step_group_lanes, e, obs_k > 0);
-    a.wpb = step_wpb();
     {
         const char* v = getenv("DRL_OBS_WIDE");
         a.obs_wide = v ? atoi(v) : 1;
         const char* st = getenv("DRL_STAGGER");
         a.stagger = st ? atoi(st) : 0;
+        const char* sp = getenv("DRL_SPECIALIZE");
+        a.specialize = sp ? atoi(sp) : 1;
     }
-    while (a.wpb > 1 && a.wpb * a.wave_lds > kLdsMax) a.wpb >>= 1;
     a.max_rounds = 1u << 20;
     a.div_side = drl::make_fastdiv((uint32_t)p->side);
     return a;

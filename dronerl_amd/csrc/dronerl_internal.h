@@ -16,6 +16,19 @@ constexpr int step_draws(int P) { return P <= 16 ? 2 : 1; }
 constexpr int step_pf(int P) { return step_draws(P) * P < 16 ? 16 : step_draws(P) * P; }
 constexpr int OBS_U = 1;        // observation cells per lane per pass (stage: OBS_U*1536 B per wave)
 
+// Per-env LDS layout of drl_step (WaveLds in dronerl_kernels.hip).  Shared by
+// the host (launch sizes) and by the compile-time-geometry kernel instances.
+namespace lay {
+constexpr int r16(int v) { return (v + 15) / 16 * 16; }
+constexpr int np(int n_drones) { return (n_drones + 7) / 8 * 8; }             // posidx entries
+constexpr int gstride(int side) { return r16(side * side); }                   // ground bytes
+constexpr int bm_bytes(int cells) { return r16((cells + 31) / 32 * 4); }       // occupancy bitmap
+constexpr int paint_bytes(int k, int w) { return k > 0 ? r16(k * w * w) : 0; }  // observation paint
+constexpr int nchg(int n_drones) { return 6 * n_drones + 2; }                  // changed-cell capacity
+constexpr int chg_bytes(int n_drones) { return r16(2 * nchg(n_drones)); }
+constexpr int bit_length(int v) { return v ? 1 + bit_length(v >> 1) : 0; }
+}  // namespace lay
+
 enum : int { OBJ_EMPTY = 0, OBJ_SKYSCRAPER = 2, OBJ_STATION = 3, OBJ_DROPZONE = 4, OBJ_PACKET = 5 };
 
 // n / d == umulhi(n, ceil(2^32 / d)) exactly for n * d < 2^32 (all our uses).
@@ -51,8 +64,7 @@ struct StepArgs {
     uint8_t* dones;
     float* obs;
     int32_t* err;
-    int wave_lds;   // LDS bytes per wave
-    int wpb;        // waves per block
+    int wave_lds;   // LDS bytes per wave (= per block: one wave per block)
     int np;         // posidx entries per env (n_drones rounded up to 8)
     int lds_bm;     // bytes per env of the occupancy bitmap (16-B multiple)
     int lds_paint;  // bytes per env of the observation paint buffer (16-B multiple)
@@ -60,6 +72,7 @@ struct StepArgs {
     int nchg;       // changed-cell list capacity (entries)
     int obs_k;      // observed drones (0: no observation)
     int obs_wide;   // observation stores: 1 = 16-B via LDS transpose, 0 = 3 x 8-B per cell
+    int specialize; // 1: use a compile-time-geometry instance when one matches (DRL_SPECIALIZE=0 disables)
     int stagger;    // diagnostic: s_sleep(127) x (block & 3) x stagger before starting (0 = off)
     uint32_t max_rounds;
     FastDiv div_side;

@@ -32,9 +32,9 @@ __device__ unsigned long long* g_stamps;
         __builtin_amdgcn_sched_barrier(0);                                               \
         unsigned long long t_;                                                           \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
-        if (lane == 0) g_stamps[((int64_t)blockIdx.x * a.wpb + wave) * 16 + (i)] = t_;  \
+        if (lane == 0) g_stamps[(int64_t)blockIdx.x * 16 + (i)] = t_;                    \
         if (lane == 0 && ((i) == 0 || (i) == 6))                                         \
-            g_stamps[((int64_t)blockIdx.x * a.wpb + wave) * 16 + 8 + (i) / 6] =          \
+            g_stamps[(int64_t)blockIdx.x * 16 + 8 + (i) / 6] =                           \
                 __builtin_amdgcn_s_memrealtime();                                        \
         __builtin_amdgcn_sched_barrier(0);                                               \
     } while (0)
@@ -120,9 +120,41 @@ __device__ __noinline__ void twist_wave(uint32_t* row, int lane) {
     wave_sync();
 }
 
+// ------------------------------------------------------------- geometry ---
+// Geometry of a step/obs launch.  The benchmark shapes get instances with the
+// side (GC), drone count (NC), window radius (RC) and observed-drone count (KC,
+// 0 = no observation) as compile-time constants, so LDS offsets, divisions by
+// side / window and loop bounds fold; every other shape runs the GC = NC = RC
+// = 0, KC = -1 instance, which reads them from StepArgs.  Both derive the LDS
+// layout from the same lay:: formulas as the host.
+template <int GC, int NC, int RC, int KC>
+struct Geo {
+    const StepArgs& a;
+    __device__ int side() const { return GC > 0 ? GC : a.side; }
+    __device__ uint32_t div_side(uint32_t n) const { return GC > 0 ? n / (uint32_t)GC : fdiv(n, a.div_side); }
+    __device__ int kbits() const { return GC > 0 ? lay::bit_length(GC) : a.kbits; }
+    __device__ int gstride() const { return GC > 0 ? lay::gstride(GC) : a.gstride; }
+    __device__ int lds_bm() const { return GC > 0 ? lay::bm_bytes(GC * GC) : a.lds_bm; }
+    __device__ int n() const { return NC > 0 ? NC : a.n_drones; }
+    __device__ int np() const { return NC > 0 ? lay::np(NC) : a.np; }
+    __device__ int nchg() const { return NC > 0 ? lay::nchg(NC) : a.nchg; }
+    __device__ int lds_chg() const { return NC > 0 ? lay::chg_bytes(NC) : a.lds_chg; }
+    __device__ int K() const { return KC >= 0 ? KC : a.obs_k; }
+    __device__ int radius() const { return RC > 0 ? RC : a.og.radius; }
+    __device__ uint32_t W() const { return RC > 0 ? (uint32_t)(2 * RC + 1) : a.og.W; }
+    __device__ int lds_paint() const { return (RC > 0 && KC >= 0) ? lay::paint_bytes(KC, 2 * RC + 1) : a.lds_paint; }
+    // observation: window cells per env (K windows) and divisions by it / a window / its width
+    __device__ uint32_t env_cells() const { return (RC > 0 && KC > 0) ? (uint32_t)KC * W() * W() : a.og.env_floats / 6u; }
+    __device__ uint32_t div_env(uint32_t n) const { return (RC > 0 && KC > 0) ? n / env_cells() : fdiv(n, a.og.div_env); }
+    __device__ uint32_t div_win(uint32_t n) const { return KC == 1 ? 0u : RC > 0 ? n / (W() * W()) : fdiv(n, a.og.div_per); }
+    __device__ uint32_t div_w(uint32_t n) const { return RC > 0 ? n / W() : fdiv(n, a.og.div_w); }
+    static constexpr bool kObs = KC != 0;  // KC == 0: instance for steps without observation
+};
+using GeoRT = Geo<0, 0, 0, -1>;
+
 // ------------------------------------------------------------ LDS image ---
 // Per-wave LDS image of its GPW envs; every region is [GPW][stride] with
-// 16-byte strides (StepArgs::lds_*):
+// 16-byte strides (lay:: / Geo):
 //   gl     u8  [gstride]  ground codes (staged by LDS-DMA, env-major = HBM order)
 //   paint  u8  [K*W*W]    air byte (charge+1)|carry<<7 of drones inside each observed window
 //   posidx u16 [np]       cell of drone index k
@@ -143,35 +175,34 @@ struct WaveLds {
     unsigned char* stage;
 };
 
-__device__ __forceinline__ WaveLds carve(unsigned char* wb, int gpw, int pf, const StepArgs& a) {
+template <class GEO>
+__device__ __forceinline__ WaveLds carve(unsigned char* wb, int gpw, int pf, const GEO& g) {
     WaveLds w;
     w.gl = wb;
-    wb += gpw * a.gstride;
+    wb += gpw * g.gstride();
     w.paint = wb;
-    wb += gpw * a.lds_paint;
+    wb += gpw * g.lds_paint();
     w.posidx = reinterpret_cast<uint16_t*>(wb);
-    wb += gpw * a.np * 2;
+    wb += gpw * g.np() * 2;
     w.stage = wb;
     w.bm = reinterpret_cast<uint32_t*>(wb);
-    wb += gpw * a.lds_bm;
+    wb += gpw * g.lds_bm();
     w.mtw = reinterpret_cast<uint32_t*>(wb);
     wb += gpw * pf * 4;
     w.chg = reinterpret_cast<uint16_t*>(wb);
-    wb += gpw * a.lds_chg;
+    wb += gpw * g.lds_chg();
     w.cnt = reinterpret_cast<uint32_t*>(wb);
     return w;
 }
 
 // Async copy of the wave's grounds (contiguous in HBM, env-major) into LDS:
 // global_load_lds_dwordx4, 1 KiB per wave-instruction, no VGPR round trip.
-__device__ __forceinline__ void stage_ground_dma(const uint8_t* __restrict__ ground, int64_t wenv0, int nenv_w,
-                                                 int gstride, uint8_t* gl, int lane) {
-    const uint8_t* src = ground + wenv0 * gstride;
-    const int nvec = nenv_w * gstride / 16;
+__device__ __forceinline__ void stage_ground_dma(const uint8_t* __restrict__ src, int nbytes, uint8_t* gl, int lane) {
+    const int nvec = nbytes / 16;
     for (int v0 = 0; v0 < nvec; v0 += 64) {
         if (v0 + lane < nvec)
             __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void*)(src + (size_t)(v0 + lane) * 16),
+                (const __attribute__((address_space(1))) void*)(src + (uint32_t)(v0 + lane) * 16u),
                 (__attribute__((address_space(3))) void*)(gl + v0 * 16), 16, 0, 0);
     }
 }
@@ -188,39 +219,42 @@ __device__ __forceinline__ void lds_zero(void* p, int nbytes, int lane) {
 // as three 8-B pieces (consecutive lanes cover a contiguous span).  ch0 drone,
 // ch1 packet OR carrying drone, ch2 dropzone, ch3 station, ch4 charge/100
 // (true f32 division, == f32(double c/100)), ch5 skyscraper or wall.
-__device__ __forceinline__ void write_obs_wave(float* __restrict__ obs, int64_t wenv0, int nenv_w,
-                                               const ObsGeom& g, const WaveLds& w, const StepArgs& a, int lane) {
-    const uint32_t win = g.W * g.W;
-    const uint32_t env_cells = g.env_floats / 6u;  // K * W*W
+// `base` is the wave's first observation float (16-B aligned unless a wave
+// holds one env with an odd K*W*W).
+template <class GEO>
+__device__ __forceinline__ void write_obs_wave(float* __restrict__ base, int nenv_w, const GEO& g, const WaveLds& w,
+                                               bool obs_wide, int lane) {
+    const uint32_t W = g.W();
+    const uint32_t win = W * W;
+    const uint32_t env_cells = g.env_cells();  // K * W*W
     const uint32_t ncell = (uint32_t)nenv_w * env_cells;
-    float* base = obs + wenv0 * (int64_t)g.env_floats;
-    // 16-B stores need a 16-B aligned wave base (always, unless one env per wave
-    // with an odd K*W*W); otherwise each lane stores its cell as 3 x 8 B.
-    const bool wide = a.obs_wide && ((uintptr_t)base & 15u) == 0;
+    const int G = g.side(), R = g.radius();
+    const uint32_t gstride = (uint32_t)g.gstride(), np = (uint32_t)g.np(), lpaint = (uint32_t)g.lds_paint();
+    const bool wide = obs_wide && ((uintptr_t)base & 15u) == 0;
     for (uint32_t q0 = 0; q0 < ncell; q0 += 64 * OBS_U) {
         uint32_t e[OBS_U], rem[OBS_U], wy[OBS_U], wx[OBS_U], pos[OBS_U];
 #pragma unroll
         for (int u = 0; u < OBS_U; ++u) {
             const uint32_t q = min(q0 + (uint32_t)(lane + 64 * u), ncell - 1u);
-            e[u] = fdiv(q, g.div_env);
+            e[u] = g.div_env(q);
             rem[u] = q - e[u] * env_cells;
-            const uint32_t k = fdiv(rem[u], g.div_per);
+            const uint32_t k = g.div_win(rem[u]);
             const uint32_t c = rem[u] - k * win;
-            wy[u] = fdiv(c, g.div_w);
-            wx[u] = c - wy[u] * g.W;
-            pos[u] = w.posidx[e[u] * a.np + k];
+            wy[u] = g.div_w(c);
+            wx[u] = c - wy[u] * W;
+            pos[u] = w.posidx[e[u] * np + k];
         }
         float2 v[OBS_U][3];
 #pragma unroll
         for (int u = 0; u < OBS_U; ++u) {
-            const uint32_t py = fdiv(pos[u], g.div_side);
-            const uint32_t px = pos[u] - py * (uint32_t)g.side;
-            const int y = (int)(py + wy[u]) - g.radius;
-            const int x = (int)(px + wx[u]) - g.radius;
-            const bool in = (unsigned)y < (unsigned)g.side && (unsigned)x < (unsigned)g.side;
-            const uint32_t o = w.gl[e[u] * g.gstride + (uint32_t)(in ? y * g.side + x : 0)];
+            const uint32_t py = g.div_side(pos[u]);
+            const uint32_t px = pos[u] - py * (uint32_t)G;
+            const int y = (int)(py + wy[u]) - R;
+            const int x = (int)(px + wx[u]) - R;
+            const bool in = (unsigned)y < (unsigned)G && (unsigned)x < (unsigned)G;
+            const uint32_t o = w.gl[e[u] * gstride + (uint32_t)(in ? y * G + x : 0)];
             const uint32_t obj = in ? o : (uint32_t)OBJ_SKYSCRAPER;
-            const uint32_t air = w.paint[e[u] * a.lds_paint + rem[u]];
+            const uint32_t air = w.paint[e[u] * lpaint + rem[u]];
             v[u][0].x = air ? 1.0f : 0.0f;
             v[u][0].y = (obj == OBJ_PACKET || (air & 0x80u)) ? 1.0f : 0.0f;
             v[u][1].x = obj == OBJ_DROPZONE ? 1.0f : 0.0f;
@@ -267,14 +301,15 @@ __device__ __forceinline__ void write_obs_wave(float* __restrict__ obs, int64_t 
 
 // Each drone paints its air byte into every observed window (drone indices
 // 0..K-1) that contains it.  posidx must be final.
-__device__ __forceinline__ void paint_windows(uint8_t* paint, const uint16_t* posidx, int K, int y, int x,
-                                              uint8_t airbyte, const ObsGeom& g) {
-    const int W = (int)g.W;
+template <class GEO>
+__device__ __forceinline__ void paint_windows(uint8_t* paint, const uint16_t* posidx, int y, int x, uint8_t airbyte,
+                                              const GEO& g) {
+    const int W = (int)g.W(), K = g.K(), R = g.radius();
     for (int k = 0; k < K; ++k) {
         const uint32_t pk = posidx[k];
-        const int pky = (int)fdiv(pk, g.div_side);
-        const int pkx = (int)pk - pky * g.side;
-        const int dy = y - pky + g.radius, dx = x - pkx + g.radius;
+        const int pky = (int)g.div_side(pk);
+        const int pkx = (int)pk - pky * g.side();
+        const int dy = y - pky + R, dx = x - pkx + R;
         if ((unsigned)dy < (unsigned)W && (unsigned)dx < (unsigned)W) paint[k * W * W + dy * W + dx] = airbyte;
     }
 }
@@ -310,7 +345,8 @@ __device__ __forceinline__ int hibit(uint64_t m) { return 63 - __clzll((long lon
 // at 64 so 8 waves fit a SIMD and every wave of a 65536-env C3 launch is
 // resident at once (at 6 waves/SIMD a second, tail-heavy generation formed).
 // Wider groups are LDS-limited below 8 waves/SIMD: no cap (it only spilled).
-template <int P>
+// Global addressing: 64-bit wave bases (scalar) + 32-bit lane offsets.
+template <int P, class GEO>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : 1, 8)))
 drl_step_kernel(StepArgs a) {
     using GMask = typename GMaskT<P>::type;
@@ -321,21 +357,25 @@ drl_step_kernel(StepArgs a) {
     using CM = typename GMaskT<(P * D <= 32 ? 32 : 64)>::type;  // round-position masks
     constexpr int CH = P < 16 ? P : 16;        // shuffle batch
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const GEO g{a};
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int grp = lane / P;
     const int j = lane % P;
-    const int64_t wenv0 = ((int64_t)blockIdx.x * a.wpb + wave) * GPW;
+    const int64_t wenv0 = (int64_t)blockIdx.x * GPW;
     const int nenv_w = (int)min((int64_t)GPW, a.E - wenv0);
-    if (nenv_w <= 0) return;  // no block-level barriers anywhere: whole idle waves may leave
-    const int64_t env = wenv0 + grp;
+    if (nenv_w <= 0) return;
     const bool env_ok = grp < nenv_w;
-    const int G = a.side, N = a.n_drones, gstride = a.gstride;
-    const WaveLds W = carve(smem + wave * a.wave_lds, GPW, PF, a);
+    const int G = g.side(), N = g.n(), gstride = g.gstride(), nchg = g.nchg();
+    const WaveLds W = carve(smem, GPW, PF, g);
     uint8_t* gl = W.gl + grp * gstride;
-    uint32_t* bm = W.bm + grp * (a.lds_bm / 4);
+    uint32_t* bm = W.bm + grp * (g.lds_bm() / 4);
     uint32_t* mtw = W.mtw + grp * PF;
-    uint16_t* posidx = W.posidx + grp * a.np;
+    uint16_t* posidx = W.posidx + grp * g.np();
+    // the wave's slices of the state (scalar bases)
+    uint32_t* const drones_w = a.drones + wenv0 * N;
+    uint32_t* const mt_w = a.mt + wenv0 * MT_WORDS;
+    uint8_t* const ground_w = a.ground + wenv0 * gstride;
+    const uint32_t rl = (uint32_t)(grp * N);  // lane's env offset in [env][drone] arrays of the wave
 
     if (a.stagger) {  // diagnostic knob (DRL_STAGGER): desynchronise waves' phases
         const int n = (int)(blockIdx.x & 3u) * a.stagger;
@@ -349,27 +389,27 @@ drl_step_kernel(StepArgs a) {
     uint32_t mi[GPW];
     if (nenv_w == GPW) {
 #pragma unroll
-        for (int g = 0; g < GPW; ++g) mi[g] = a.mt_index[wenv0 + g];
+        for (int e = 0; e < GPW; ++e) mi[e] = a.mt_index[wenv0 + e];
     } else {
 #pragma unroll
-        for (int g = 0; g < GPW; ++g) mi[g] = a.mt_index[min(wenv0 + g, a.E - 1)];
+        for (int e = 0; e < GPW; ++e) mi[e] = a.mt_index[min(wenv0 + e, a.E - 1)];
     }
     int midx = MT_N;
 #pragma unroll
-    for (int g = 0; g < GPW; ++g) midx = (g == grp) ? (int)mi[g] : midx;
+    for (int e = 0; e < GPW; ++e) midx = (e == grp) ? (int)mi[e] : midx;
     if (!env_ok) midx = MT_N;
     const bool active = env_ok && j < N;
-    const uint32_t rec = active ? a.drones[env * N + j] : 0u;
-    const int my_action = active ? a.actions[env * N + j] : 4;
-    const uint32_t* mrow = a.mt + (env_ok ? env : 0) * MT_WORDS;
+    const uint32_t rec = active ? drones_w[rl + j] : 0u;
+    const int my_action = active ? a.actions[wenv0 * N + (rl + j)] : 4;
+    const uint32_t* mrow = mt_w + (uint32_t)(env_ok ? grp : 0) * MT_WORDS;
     const int pf_base0 = midx;
     int pfn = min(PF, MT_N - midx);
     uint32_t pfw[PFR];  // next MT words of the stream (addresses clamped: no per-word branch)
 #pragma unroll
     for (int r = 0; r < PFR; ++r) pfw[r] = mrow[min(midx + j + P * r, MT_N - 1)];
-    stage_ground_dma(a.ground, wenv0, nenv_w, gstride, W.gl, lane);
-    lds_zero(W.bm, GPW * a.lds_bm, lane);
-    if (a.obs) lds_zero(W.paint, GPW * a.lds_paint, lane);
+    stage_ground_dma(ground_w, nenv_w * gstride, W.gl, lane);
+    lds_zero(W.bm, GPW * g.lds_bm(), lane);
+    if (GEO::kObs && a.obs) lds_zero(W.paint, GPW * g.lds_paint(), lane);
     if (lane < GPW) W.cnt[lane * 4] = 0u;
 
     DRL_STAMP(1);
@@ -430,13 +470,13 @@ drl_step_kernel(StepArgs a) {
             reward = a.r_pickup;
             carry = 1;
             gl[tcell] = OBJ_EMPTY;
-            chg_push(W, grp, a.nchg, tcell);
+            chg_push(W, grp, nchg, tcell);
         } else if (obj == OBJ_DROPZONE && carry) {
             reward = a.r_delivery;
             carry = 0;
             gl[tcell] = OBJ_EMPTY;
             deliver = true;
-            chg_push(W, grp, a.nchg, tcell);
+            chg_push(W, grp, nchg, tcell);
         }
         if (obj == OBJ_SKYSCRAPER) dead = true;
     }
@@ -485,7 +525,7 @@ drl_step_kernel(StepArgs a) {
     // ---- respawns (env.py:186-210, _find_respawn_position :226-233):
     // items w < nR: crashed drones (mask: drones | skyscrapers); then n_pack
     // packets, then n_deliver dropzones (mask: any ground object).  Each round
-    // draws P consecutive MT outputs, keeps those < side (randint(0, side-1)
+    // draws D*P consecutive MT outputs, keeps those < side (randint(0, side-1)
     // == _randbelow(side)) and pairs accepted draws as (y, x).  A placement
     // always ends on the second draw of a pair, so the pairing is the same for
     // every item: the round's candidate cells are read from LDS once and
@@ -496,7 +536,7 @@ drl_step_kernel(StepArgs a) {
         if (j + P * r < pfn) mtw[j + P * r] = pfw[r];
     int pf_base = pf_base0;
     int w = 0, have_y = 0, yv = 0;
-    const int shift = 32 - a.kbits;
+    const int shift = 32 - g.kbits();
     const int my_item = crashed ? newslot - nS : -1;  // this drone's respawn item
     uint32_t rounds = 0;
     [[maybe_unused]] uint32_t rounds_w = 0;  // wave-level loop trips (diagnostics)
@@ -508,7 +548,7 @@ drl_step_kernel(StepArgs a) {
         while (need) {
             const int tl = __ffsll((unsigned long long)need) - 1;
             need &= need - 1ull;
-            twist_wave(a.mt + (wenv0 + tl / P) * MT_WORDS, lane);
+            twist_wave(mt_w + (uint32_t)(tl / P) * MT_WORDS, lane);
             if (grp == tl / P) {
                 midx = 0;
                 pf_base = 0;
@@ -531,8 +571,8 @@ drl_step_kernel(StepArgs a) {
             const bool inpf = off < pfn;
             uint32_t word = mtw[min(max(off, 0), PF - 1)];
             if (__ballot(valid && !inpf)) {  // beyond the prefetched words (rare)
-                const uint32_t g = (valid && !inpf) ? load_l2(mrow + midx + d) : 0u;
-                word = inpf ? word : g;
+                const uint32_t gw = (valid && !inpf) ? load_l2(mrow + midx + d) : 0u;
+                word = inpf ? word : gw;
             }
             rq[q] = valid ? (int)(temper(word) >> shift) : G;
             accq[q] = rq[q] < G;
@@ -597,7 +637,7 @@ drl_step_kernel(StepArgs a) {
                     } else {
                         if (j == 0) {
                             gl[cell] = (w < nR + n_pack) ? OBJ_PACKET : OBJ_DROPZONE;
-                            chg_push(W, grp, a.nchg, cell);
+                            chg_push(W, grp, nchg, cell);
                         }
                         okgc &= ~same;
                     }
@@ -629,33 +669,33 @@ drl_step_kernel(StepArgs a) {
 
     DRL_STAMP(4);
 #ifdef DRL_STAMPS
-    if (lane == 0) g_stamps[((int64_t)blockIdx.x * a.wpb + wave) * 16 + 7] = __builtin_amdgcn_readfirstlane(rounds_w);
+    if (lane == 0) g_stamps[(int64_t)blockIdx.x * 16 + 7] = __builtin_amdgcn_readfirstlane(rounds_w);
 #endif
     // ---- _pick_packets_after_respawn (env.py:217-224): distinct cells, parallel
     if (active && pos < 0) pos = 0;  // unreachable for valid params (respawn always finds a cell)
     if (active && !carry && gl[pos] == OBJ_PACKET) {
         carry = 1;
         gl[pos] = OBJ_EMPTY;
-        chg_push(W, grp, a.nchg, pos);
+        chg_push(W, grp, nchg, pos);
     }
 
     // ---- write back: records permuted to O', rewards/dones by drone index,
     // changed ground cells as bytes
-    const uint32_t py = fdiv((uint32_t)(pos > 0 ? pos : 0), a.div_side);
+    const uint32_t py = g.div_side((uint32_t)(pos > 0 ? pos : 0));
     const uint32_t px = (uint32_t)(pos > 0 ? pos : 0) - py * (uint32_t)G;
     if (active) {
-        a.drones[env * N + newslot] = pack_drone((int)py, (int)px, c, carry, idx);
-        a.rewards[env * N + idx] = reward;
-        a.dones[env * N + idx] = crashed ? 1 : 0;
+        drones_w[rl + newslot] = pack_drone((int)py, (int)px, c, carry, idx);
+        a.rewards[wenv0 * N + (rl + idx)] = reward;
+        a.dones[wenv0 * N + (rl + idx)] = crashed ? 1 : 0;
         posidx[idx] = (uint16_t)pos;
     }
-    if (env_ok && j == 0) a.mt_index[env] = (uint32_t)midx;
+    if (env_ok && j == 0) a.mt_index[wenv0 + grp] = (uint32_t)midx;
     wave_sync();
     if (env_ok) {
         const uint32_t nc = W.cnt[grp * 4];
-        const uint16_t* ch = W.chg + grp * a.nchg;
-        uint8_t* gdst = a.ground + env * gstride;
-        if (nc <= (uint32_t)a.nchg) {
+        const uint16_t* ch = W.chg + grp * nchg;
+        uint8_t* gdst = ground_w + (uint32_t)(grp * gstride);
+        if (nc <= (uint32_t)nchg) {
             for (uint32_t q = j; q < nc; q += P) gdst[ch[q]] = gl[ch[q]];
         } else {  // cannot happen (<= 6N changes per step); whole-row fallback
             for (int v = j; v < gstride / 16; v += P)
@@ -663,46 +703,44 @@ drl_step_kernel(StepArgs a) {
         }
     }
     DRL_STAMP(5);
-    if (a.obs) {
-        if (active) paint_windows(W.paint + grp * a.lds_paint, posidx, a.obs_k, (int)py, (int)px,
-                                  (uint8_t)((c + 1) | (carry << 7)), a.og);
+    if (GEO::kObs && a.obs) {
+        if (active) paint_windows(W.paint + grp * g.lds_paint(), posidx, (int)py, (int)px,
+                                  (uint8_t)((c + 1) | (carry << 7)), g);
         wave_sync();
-        write_obs_wave(a.obs, wenv0, nenv_w, a.og, W, a, lane);
+        write_obs_wave(a.obs + wenv0 * (int64_t)(6u * g.env_cells()), nenv_w, g, W, a.obs_wide, lane);
     }
     DRL_STAMP(6);
 }
 
 // ------------------------------------------------------------ observation ---
-template <int P>
+template <int P, class GEO>
 __global__ void __launch_bounds__(64) drl_obs_kernel(StepArgs a) {
     constexpr int GPW = 64 / P;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const GEO g{a};
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
     const int grp = lane / P;
     const int j = lane % P;
-    const int64_t wenv0 = ((int64_t)blockIdx.x * a.wpb + wave) * GPW;
+    const int64_t wenv0 = (int64_t)blockIdx.x * GPW;
     const int nenv_w = (int)min((int64_t)GPW, a.E - wenv0);
     if (nenv_w <= 0) return;
-    const int64_t env = wenv0 + grp;
     const bool env_ok = grp < nenv_w;
-    const int N = a.n_drones;
-    const WaveLds W = carve(smem + wave * a.wave_lds, GPW, step_pf(P), a);
-    stage_ground_dma(a.ground, wenv0, nenv_w, a.gstride, W.gl, lane);
-    lds_zero(W.paint, GPW * a.lds_paint, lane);
+    const int N = g.n(), gstride = g.gstride();
+    const WaveLds W = carve(smem, GPW, step_pf(P), g);
+    stage_ground_dma(a.ground + wenv0 * gstride, nenv_w * gstride, W.gl, lane);
+    lds_zero(W.paint, GPW * g.lds_paint(), lane);
     const bool active = env_ok && j < N;
-    const uint32_t rec = active ? a.drones[env * N + j] : 0u;
+    const uint32_t rec = active ? a.drones[wenv0 * N + (uint32_t)(grp * N + j)] : 0u;
     const int y = rec & 255u, x = (rec >> 8) & 255u;
     const int c = (rec >> 16) & 255u, carry = (rec >> 24) & 1u;
     const int idx = ((int)(rec >> 25) < N) ? (int)(rec >> 25) : j;
-    uint16_t* posidx = W.posidx + grp * a.np;
-    if (active) posidx[idx] = (uint16_t)(y * a.side + x);
+    uint16_t* posidx = W.posidx + grp * g.np();
+    if (active) posidx[idx] = (uint16_t)(y * g.side() + x);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
-    if (active) paint_windows(W.paint + grp * a.lds_paint, posidx, a.obs_k, y, x, (uint8_t)((c + 1) | (carry << 7)),
-                              a.og);
+    if (active) paint_windows(W.paint + grp * g.lds_paint(), posidx, y, x, (uint8_t)((c + 1) | (carry << 7)), g);
     wave_sync();
-    write_obs_wave(a.obs, wenv0, nenv_w, a.og, W, a, lane);
+    write_obs_wave(a.obs + wenv0 * (int64_t)(6u * g.env_cells()), nenv_w, g, W, a.obs_wide, lane);
 }
 
 // ------------------------------------------------------------------ reset ---
@@ -932,25 +970,47 @@ __global__ void drl_synth_actions_kernel(uint64_t seed, uint64_t step, int64_t e
 }
 
 // ---------------------------------------------------------------- launch ---
-template <int P>
+template <int P, class GEO>
 static hipError_t launch_step_t(const StepArgs& a, hipStream_t s, bool obs_only) {
-    const int envs_per_block = a.wpb * (64 / P);
-    const int64_t blocks = (a.E + envs_per_block - 1) / envs_per_block;
-    const dim3 grid((unsigned)blocks), block(64 * a.wpb);
-    if (obs_only)
-        hipLaunchKernelGGL(drl_obs_kernel<P>, grid, block, a.wpb * a.wave_lds, s, a);
-    else
-        hipLaunchKernelGGL(drl_step_kernel<P>, grid, block, a.wpb * a.wave_lds, s, a);
+    const int64_t blocks = (a.E + (64 / P) - 1) / (64 / P);
+    const dim3 grid((unsigned)blocks), block(64);
+    if (obs_only) {
+        if constexpr (GEO::kObs) hipLaunchKernelGGL((drl_obs_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
+        else return hipErrorInvalidValue;
+    } else {
+        hipLaunchKernelGGL((drl_step_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
+    }
     return hipGetLastError();
 }
 
+// Compile-time-geometry instances for the benchmark shapes (side, drones,
+// radius; observation of drone 0 or none), the runtime-geometry one otherwise.
+template <int P, int G, int N, int R>
+static bool launch_spec(const StepArgs& a, hipStream_t s, bool obs_only, hipError_t* e) {
+    if (a.side != G || a.n_drones != N || a.og.radius != R) return false;
+    if (a.obs_k == 0 && !obs_only) *e = launch_step_t<P, Geo<G, N, R, 0>>(a, s, obs_only);
+    else if (a.obs_k == 1) *e = launch_step_t<P, Geo<G, N, R, 1>>(a, s, obs_only);
+    else return false;
+    return true;
+}
+
 hipError_t launch_step(const StepArgs& a, int P, hipStream_t s, bool obs_only) {
+    hipError_t e = hipSuccess;
+    const bool spec = a.specialize;
     switch (P) {
-        case 4: return launch_step_t<4>(a, s, obs_only);
-        case 8: return launch_step_t<8>(a, s, obs_only);
-        case 16: return launch_step_t<16>(a, s, obs_only);
-        case 32: return launch_step_t<32>(a, s, obs_only);
-        case 64: return launch_step_t<64>(a, s, obs_only);
+        case 4:
+            if (spec && launch_spec<4, 8, 4, 3>(a, s, obs_only, &e)) return e;
+            return launch_step_t<4, GeoRT>(a, s, obs_only);
+        case 8:
+            if (spec && launch_spec<8, 16, 8, 3>(a, s, obs_only, &e)) return e;
+            return launch_step_t<8, GeoRT>(a, s, obs_only);
+        case 16:
+            if (spec && launch_spec<16, 32, 16, 3>(a, s, obs_only, &e)) return e;
+            return launch_step_t<16, GeoRT>(a, s, obs_only);
+        case 32:
+            if (spec && launch_spec<32, 64, 32, 3>(a, s, obs_only, &e)) return e;
+            return launch_step_t<32, GeoRT>(a, s, obs_only);
+        case 64: return launch_step_t<64, GeoRT>(a, s, obs_only);
         default: return hipErrorInvalidValue;
     }
 }

@@ -172,8 +172,18 @@ def test_reset_matches_oracle(name):
     ("pool_5x5_n2", 200, 300, 20),
     ("dense_10x10_n8", 600, 300, 20),
     ("bigside_128_n4", 40, 100, 50),
+    # the benchmark shapes again on the runtime-geometry kernel instance
+    ("c1_8x8_n4|rt", 64, 300, 50),
+    ("c2_16x16_n8|rt", 1024, 200, 25),
+    ("c4_32x32_n16|rt", 512, 120, 30),
+    ("c5_64x64_n32|rt", 128, 80, 40),
 ])
-def test_rollout_matches_oracle(name, E, steps, every):
+def test_rollout_matches_oracle(name, E, steps, every, monkeypatch):
+    """Benchmark shapes run compile-time-geometry instances; "|rt" forces the
+    runtime-geometry one (DRL_SPECIALIZE=0) on the same shape."""
+    name, _, rt = name.partition("|")
+    if rt:
+        monkeypatch.setenv("DRL_SPECIALIZE", "0")
     p = EnvParams(**CONFIGS[name])
     env = Env(p, E)
     env.reset(seed=7)
@@ -192,8 +202,9 @@ def test_rollout_matches_oracle(name, E, steps, every):
     env.check_errors()
 
 
+@pytest.mark.parametrize("k", [1, 8])
 @pytest.mark.parametrize("E", [1, 2, 3, 7, 31, 33, 63, 65, 129, 1001])
-def test_ragged_num_envs(E):
+def test_ragged_num_envs(E, k):
     p = EnvParams(n_drones=8, grid_size=16)
     env = Env(p, E)
     env.reset(seed=3)
@@ -201,11 +212,12 @@ def test_ragged_num_envs(E):
     o.reset(3 + np.arange(E))
     for t in range(1, 41):
         a = env.synth_actions(seed=5, step=t)
-        r, dn, ob = env.step(a, obs_k=8)
+        r, dn, ob = env.step(a, obs_k=k)
         ro, do = o.step(a.cpu().numpy())
         assert_rewards(r.cpu().numpy(), ro, f"E={E} step {t}")
     assert_state(gpu_state(env), o.state(), f"E={E}")
-    np.testing.assert_array_equal(ob.cpu().numpy(), o.obs(3, 8))
+    np.testing.assert_array_equal(ob.cpu().numpy(), o.obs(3, k))
+    np.testing.assert_array_equal(env.get_obs(k).cpu().numpy(), o.obs(3, k))
 
 
 @pytest.mark.parametrize("radius", [1, 2, 3, 4, 5, 8])

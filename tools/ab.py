@@ -2,8 +2,9 @@
 """Interleaved in-process A/B timing of drl_step variants (methodology rule 24).
 
 python tools/ab.py --config c3 --rounds 5 --steps 100
-Variants: waves-per-block 1/2/4 (env DRL_WAVES_PER_BLOCK, read per call) and
-obs K=1 vs no obs.  Prints median/min µs per launch per variant.
+Variants (env knobs read per call): specN = DRL_SPECIALIZE (compile-time
+geometry instance on/off), noobs = step without observation, wide0 = 8-B
+observation stores, stN = DRL_STAGGER.  Prints median/min µs per launch.
 """
 import argparse
 import ctypes
@@ -26,8 +27,8 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--variants", default="wpb1,wpb2,wpb4,wpb2_noobs",
-                    help="comma list; each: wpbN[_noobs][_wide0|_wide1]")
+    ap.add_argument("--variants", default="spec1,spec0,spec1_noobs,spec0_noobs",
+                    help="comma list; each: specN[_noobs][_wide0|_wide1][_stN]")
     args = ap.parse_args()
     G, N, E, K = CONFIGS[args.config]
     env = BatchedDeliveryDrones(EnvParams(n_drones=N, grid_size=G), E)
@@ -48,12 +49,10 @@ def main():
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     variants = args.variants.split(",")
     res = {v: [] for v in variants}
-    for v in variants + variants:  # warm every variant
-        pass
     for r in range(args.rounds + 1):
         for v in variants:
             parts = v.split("_")
-            os.environ["DRL_WAVES_PER_BLOCK"] = parts[0][3:]
+            os.environ["DRL_SPECIALIZE"] = parts[0][4:] if parts[0].startswith("spec") else "1"
             os.environ["DRL_OBS_WIDE"] = "0" if "wide0" in parts else "1"
             os.environ["DRL_STAGGER"] = next((x[2:] for x in parts if x.startswith("st")), "0")
             k = 0 if "noobs" in parts else K
