@@ -117,6 +117,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-reset-bench", action="store_true")
+    ap.add_argument("--obs-k", type=int, default=-1,
+                    help="diagnostic: observed drones per step (default: the config's; 0 = step without obs)")
     args = ap.parse_args()
 
     rank, world, local = dist_init()
@@ -129,6 +131,8 @@ def main():
     G, N, E, K = CONFIGS[args.config]
     if args.envs:
         E = args.envs
+    if args.obs_k >= 0:
+        K = args.obs_k
     p = EnvParams(n_drones=N, grid_size=G)
     dev = torch.device("cuda", local)
     env = BatchedDeliveryDrones(p, E, device=dev, env_offset=rank * E)
@@ -141,7 +145,7 @@ def main():
     W = env.layout.obs_window
     rewards = torch.empty((E, N), dtype=torch.float32, device=dev)
     dones = torch.empty((E, N), dtype=torch.uint8, device=dev)
-    obs = torch.empty((E, K, W, W, 6), dtype=torch.float32, device=dev)
+    obs = torch.empty((E, max(K, 1), W, W, 6), dtype=torch.float32, device=dev)
 
     # fast path: ctypes arguments built once; only the actions pointer moves
     L = lib()
@@ -150,6 +154,8 @@ def main():
     sp = ctypes.byref(st)
     a_ptrs = [ctypes.c_void_p(actions[t].data_ptr()) for t in range(T)]
     r_p, d_p, o_p = (ctypes.c_void_p(x.data_ptr()) for x in (rewards, dones, obs))
+    if K == 0:
+        o_p = None
     e_p = ctypes.c_void_p(env.err.data_ptr())
     stream = torch.cuda.current_stream(dev)
     s_p = ctypes.c_void_p(stream.cuda_stream)

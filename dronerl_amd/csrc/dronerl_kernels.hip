@@ -120,6 +120,41 @@ __device__ __noinline__ void twist_wave(uint32_t* row, int lane) {
     wave_sync();
 }
 
+// n / D for n <= NMAX (compile-time) as one multiply and a shift: the
+// smallest shift whose rounded-up reciprocal is exact over [0, NMAX].
+struct SmallDiv {
+    uint32_t m;
+    int s;
+};
+constexpr SmallDiv find_small_div(uint32_t d, uint32_t nmax) {
+    for (int s = 0; s < 32; ++s) {
+        const uint64_t m = ((1ull << s) + d - 1) / d;
+        if (m * nmax >= (1ull << 24)) break;  // keep v_mul_u32_u24
+        bool ok = true;
+        for (uint32_t n = 0; n <= nmax && ok; ++n) ok = ((n * m) >> s) == n / d;
+        if (ok) return SmallDiv{(uint32_t)m, s};
+    }
+    return SmallDiv{0, -1};  // none: callers fall back to n / d
+}
+template <uint32_t D, uint32_t NMAX>
+__device__ __forceinline__ uint32_t small_div(uint32_t n) {
+    constexpr SmallDiv sd = find_small_div(D, NMAX);
+    if constexpr (sd.s < 0) return n / D;
+    else if constexpr (sd.m == 1) return n >> sd.s;
+    else return __umul24(n, sd.m) >> sd.s;
+}
+
+// c / 100.0f, correctly rounded, for integer c in [0, 255]: one multiply and
+// two FMA corrections (checked exhaustively against the IEEE quotient with
+// exact rational arithmetic), instead of the full f32 division sequence.
+__device__ __forceinline__ float div100(int c) {
+    const float x = (float)c;
+    const float r = 0.01f;
+    const float q = x * r;
+    const float e = __fmaf_rn(-q, 100.0f, x);
+    return __fmaf_rn(e, r, q);
+}
+
 // ------------------------------------------------------------- geometry ---
 // Geometry of a step/obs launch.  The benchmark shapes get instances with the
 // side (GC), drone count (NC), window radius (RC) and observed-drone count (KC,
@@ -144,10 +179,22 @@ struct Geo {
     __device__ uint32_t W() const { return RC > 0 ? (uint32_t)(2 * RC + 1) : a.og.W; }
     __device__ int lds_paint() const { return (RC > 0 && KC >= 0) ? lay::paint_bytes(KC, 2 * RC + 1) : a.lds_paint; }
     // observation: window cells per env (K windows) and divisions by it / a window / its width
-    __device__ uint32_t env_cells() const { return (RC > 0 && KC > 0) ? (uint32_t)KC * W() * W() : a.og.env_floats / 6u; }
-    __device__ uint32_t div_env(uint32_t n) const { return (RC > 0 && KC > 0) ? n / env_cells() : fdiv(n, a.og.div_env); }
-    __device__ uint32_t div_win(uint32_t n) const { return KC == 1 ? 0u : RC > 0 ? n / (W() * W()) : fdiv(n, a.og.div_per); }
-    __device__ uint32_t div_w(uint32_t n) const { return RC > 0 ? n / W() : fdiv(n, a.og.div_w); }
+    // (arguments: q < 16 envs x env_cells; a cell index within K windows; within one window)
+    static constexpr uint32_t kW = RC > 0 ? 2 * RC + 1 : 1, kCells = KC > 0 ? KC * kW * kW : 1;
+    __device__ uint32_t env_cells() const { return (RC > 0 && KC > 0) ? kCells : a.og.env_floats / 6u; }
+    __device__ uint32_t div_env(uint32_t n) const {
+        if constexpr (RC > 0 && KC > 0) return small_div<kCells, 16 * kCells>(n);
+        else return fdiv(n, a.og.div_env);
+    }
+    __device__ uint32_t div_win(uint32_t n) const {
+        if constexpr (KC == 1) return 0u;
+        else if constexpr (RC > 0 && KC > 0) return small_div<kW * kW, kCells>(n);
+        else return fdiv(n, a.og.div_per);
+    }
+    __device__ uint32_t div_w(uint32_t n) const {
+        if constexpr (RC > 0) return small_div<kW, kW * kW>(n);
+        else return fdiv(n, a.og.div_w);
+    }
     static constexpr bool kObs = KC != 0;  // KC == 0: instance for steps without observation
 };
 using GeoRT = Geo<0, 0, 0, -1>;
@@ -259,7 +306,7 @@ __device__ __forceinline__ void write_obs_wave(float* __restrict__ base, int nen
             v[u][0].y = (obj == OBJ_PACKET || (air & 0x80u)) ? 1.0f : 0.0f;
             v[u][1].x = obj == OBJ_DROPZONE ? 1.0f : 0.0f;
             v[u][1].y = obj == OBJ_STATION ? 1.0f : 0.0f;
-            v[u][2].x = air ? (float)((int)(air & 0x7fu) - 1) / 100.0f : 0.0f;
+            v[u][2].x = air ? div100((int)(air & 0x7fu) - 1) : 0.0f;
             v[u][2].y = obj == OBJ_SKYSCRAPER ? 1.0f : 0.0f;
         }
         if (wide) {
@@ -273,14 +320,20 @@ __device__ __forceinline__ void write_obs_wave(float* __restrict__ base, int nen
                 st[slot + 2] = v[u][2];
             }
             wave_sync();
-            const uint32_t nbytes = min(ncell - q0, 64u * OBS_U) * 24u;
             const uint4* sv = reinterpret_cast<const uint4*>(w.stage);
             uint4* dst = reinterpret_cast<uint4*>(base + 6u * q0);
-            for (uint32_t t = lane; t * 16u < nbytes; t += 64) {
-                if (t * 16u + 16u <= nbytes) {
-                    dst[t] = sv[t];
-                } else {  // 8-byte tail
-                    reinterpret_cast<uint2*>(dst + t)[0] = reinterpret_cast<const uint2*>(sv + t)[0];
+            if (q0 + 64u * OBS_U <= ncell) {  // full pass: 96*OBS_U 16-B pieces
+#pragma unroll
+                for (int t = 0; t < 96 * OBS_U; t += 64)
+                    if (96 * OBS_U - t >= 64 || lane < 96 * OBS_U - t) dst[t + lane] = sv[t + lane];
+            } else {
+                const uint32_t nbytes = (ncell - q0) * 24u;
+                for (uint32_t t = lane; t * 16u < nbytes; t += 64) {
+                    if (t * 16u + 16u <= nbytes) {
+                        dst[t] = sv[t];
+                    } else {  // 8-byte tail
+                        reinterpret_cast<uint2*>(dst + t)[0] = reinterpret_cast<const uint2*>(sv + t)[0];
+                    }
                 }
             }
             wave_sync();

@@ -1,8 +1,8 @@
 set -u
 cd /root/repo
 export TMPDIR=/tmp
-OUT=gpurun_out/pmcq; mkdir -p $OUT
-A="--config ${CFG:-c3} --steps 20 --warmup 2 --no-cpu-baseline --no-reset-bench"
+OUT=gpurun_out/pmcq${TAG:-}; mkdir -p $OUT
+A="--config ${CFG:-c3} --steps 20 --warmup 2 --no-cpu-baseline --no-reset-bench ${EXTRA:-}"
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_INSTS_SMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA"; do
   i=$((i+1))
@@ -10,10 +10,10 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD S
   rc=$?; if [ $rc -ne 0 ]; then echo "pass $i rc=$rc"; tail -3 $OUT/p$i.log; fi
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 done
-python3 - <<'PY'
-import csv, collections, glob
+OUT=$OUT python3 - <<'PY'
+import csv, collections, glob, os
 agg = collections.defaultdict(list)
-for f in glob.glob('gpurun_out/pmcq/p*/run_counter_collection.csv'):
+for f in glob.glob(os.environ['OUT'] + '/p*/run_counter_collection.csv'):
     for r in csv.DictReader(open(f)):
         agg[r['Counter_Name']].append(float(r['Counter_Value']))
 m = {k: sum(v)/len(v) for k, v in agg.items()}

@@ -76,6 +76,13 @@ def main():
                   f"{np.percentile(life, 90):.1f} us")
             conc = [int(((starts <= x) & (ends > x)).sum()) for x in np.linspace(0, span, 12)]
             print(f"  resident waves over the span (12 samples): {conc}")
+            print(f"  wave end p10/50/90/99/max {np.percentile(ends, 10):.1f}/{np.percentile(ends, 50):.1f}/"
+                  f"{np.percentile(ends, 90):.1f}/{np.percentile(ends, 99):.1f}/{ends.max():.1f} us; "
+                  f"lifetime max {life.max():.1f} us")
+            xcd = np.arange(len(starts)) % 8
+            print("  per-XCD (block % 8) mean start / mean end / max end us: " + ", ".join(
+                f"{starts[xcd == i].mean():.1f}/{ends[xcd == i].mean():.1f}/{ends[xcd == i].max():.1f}"
+                for i in range(8)))
     d = np.concatenate(acc)
     names = ["loads+MT prefetch", "claims+DMA wait", "effects+ordering", "respawn rounds", "write-back",
              "observation"]
