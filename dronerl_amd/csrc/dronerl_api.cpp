@@ -172,8 +172,6 @@ drl::StepArgs step_args(const drl_params* p, const drl_state* s, const drl_layou
     {
         const char* v = getenv("DRL_OBS_WIDE");
         a.obs_wide = v ? atoi(v) : 1;
-        const char* st = getenv("DRL_STAGGER");
-        a.stagger = st ? atoi(st) : 0;
         const char* sp = getenv("DRL_SPECIALIZE");
         a.specialize = sp ? atoi(sp) : 1;
     }

@@ -12,7 +12,7 @@ constexpr int MT_M = 397;
 constexpr int MT_WORDS = DRL_MT_WORDS;
 // respawn rounds: D draws per lane (D*P MT outputs per round); the first
 // round's words (>= 16) are prefetched into LDS with the step's other loads
-constexpr int step_draws(int P) { return P <= 16 ? 2 : 1; }
+constexpr int step_draws(int P) { return P == 16 ? 2 : 1; }
 constexpr int step_pf(int P) { return step_draws(P) * P < 16 ? 16 : step_draws(P) * P; }
 constexpr int OBS_U = 1;        // observation cells per lane per pass (stage: OBS_U*1536 B per wave)
 
@@ -73,7 +73,6 @@ struct StepArgs {
     int obs_k;      // observed drones (0: no observation)
     int obs_wide;   // observation stores: 1 = 16-B via LDS transpose, 0 = 3 x 8-B per cell
     int specialize; // 1: use a compile-time-geometry instance when one matches (DRL_SPECIALIZE=0 disables)
-    int stagger;    // diagnostic: s_sleep(127) x (block & 3) x stagger before starting (0 = off)
     uint32_t max_rounds;
     FastDiv div_side;
     ObsGeom og;

@@ -196,6 +196,7 @@ struct Geo {
         else return fdiv(n, a.og.div_w);
     }
     static constexpr bool kObs = KC != 0;  // KC == 0: instance for steps without observation
+    static constexpr int kGstride = GC > 0 ? lay::gstride(GC) : 0;
 };
 using GeoRT = Geo<0, 0, 0, -1>;
 
@@ -250,6 +251,22 @@ __device__ __forceinline__ void stage_ground_dma(const uint8_t* __restrict__ src
         if (v0 + lane < nvec)
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void*)(src + (uint32_t)(v0 + lane) * 16u),
+                (__attribute__((address_space(3))) void*)(gl + v0 * 16), 16, 0, 0);
+    }
+}
+
+// Compile-time variant: exactly NV vectors, unrolled, so the compiler can count
+// the outstanding loads (a runtime trip count forces a vmcnt(0) after the
+// loop).  Vectors past the wave's valid envs re-read the last valid vector
+// into LDS the wave does not use.
+template <int NV>
+__device__ __forceinline__ void stage_ground_dma_n(const uint8_t* __restrict__ src, int nbytes, uint8_t* gl, int lane) {
+    const uint32_t last = (uint32_t)(nbytes / 16 - 1);
+#pragma unroll
+    for (int v0 = 0; v0 < NV; v0 += 64) {
+        if (NV - v0 >= 64 || lane < NV - v0)
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(src + min((uint32_t)(v0 + lane), last) * 16u),
                 (__attribute__((address_space(3))) void*)(gl + v0 * 16), 16, 0, 0);
     }
 }
@@ -430,40 +447,36 @@ drl_step_kernel(StepArgs a) {
     uint8_t* const ground_w = a.ground + wenv0 * gstride;
     const uint32_t rl = (uint32_t)(grp * N);  // lane's env offset in [env][drone] arrays of the wave
 
-    if (a.stagger) {  // diagnostic knob (DRL_STAGGER): desynchronise waves' phases
-        const int n = (int)(blockIdx.x & 3u) * a.stagger;
-        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
-    }
     DRL_STAMP(0);
-    // ---- loads.  The wave's MT indices are contiguous: scalar loads (lgkmcnt),
-    // so the MT-word prefetch that depends on them starts early.  Then the drone
-    // record and the action of drone index j, the MT words, and the ground by
-    // LDS-DMA; consumers of the MT words come last (respawn loop).
-    uint32_t mi[GPW];
-    if (nenv_w == GPW) {
+    // ---- loads, in one round trip plus the MT-word prefetch: the env's MT
+    // index (one load per lane, all lanes of a group at one address), then the
+    // LDS zeroing (LDS writes must precede the LDS-DMA or they wait for it),
+    // the drone record and the action of drone index j, the ground by LDS-DMA,
+    // and last the MT words, which need the index.  Consumers of the ground
+    // and MT words come after the claims scan.
+    uint32_t mi[GPW];  // uniform addresses, nothing written before: scalar loads (lgkmcnt)
 #pragma unroll
-        for (int e = 0; e < GPW; ++e) mi[e] = a.mt_index[wenv0 + e];
-    } else {
-#pragma unroll
-        for (int e = 0; e < GPW; ++e) mi[e] = a.mt_index[min(wenv0 + e, a.E - 1)];
-    }
-    int midx = MT_N;
-#pragma unroll
-    for (int e = 0; e < GPW; ++e) midx = (e == grp) ? (int)mi[e] : midx;
-    if (!env_ok) midx = MT_N;
-    const bool active = env_ok && j < N;
-    const uint32_t rec = active ? drones_w[rl + j] : 0u;
-    const int my_action = active ? a.actions[wenv0 * N + (rl + j)] : 4;
-    const uint32_t* mrow = mt_w + (uint32_t)(env_ok ? grp : 0) * MT_WORDS;
-    const int pf_base0 = midx;
-    int pfn = min(PF, MT_N - midx);
-    uint32_t pfw[PFR];  // next MT words of the stream (addresses clamped: no per-word branch)
-#pragma unroll
-    for (int r = 0; r < PFR; ++r) pfw[r] = mrow[min(midx + j + P * r, MT_N - 1)];
-    stage_ground_dma(ground_w, nenv_w * gstride, W.gl, lane);
+    for (int e = 0; e < GPW; ++e) mi[e] = a.mt_index[wenv0 + min(e, nenv_w - 1)];
     lds_zero(W.bm, GPW * g.lds_bm(), lane);
     if (GEO::kObs && a.obs) lds_zero(W.paint, GPW * g.lds_paint(), lane);
     if (lane < GPW) W.cnt[lane * 4] = 0u;
+    wave_sync();
+    const bool active = env_ok && j < N;
+    // unconditional loads at clamped indices (no exec-mask branches around
+    // them, so the wait counts stay exact); inactive lanes discard the values
+    const uint32_t li = min(rl + (uint32_t)j, (uint32_t)(nenv_w * N - 1));
+    const uint32_t rec_ld = drones_w[li];
+    const int act_ld = a.actions[wenv0 * N + li];
+    if constexpr (GEO::kGstride > 0) stage_ground_dma_n<GPW * GEO::kGstride / 16>(ground_w, nenv_w * gstride, W.gl, lane);
+    else stage_ground_dma(ground_w, nenv_w * gstride, W.gl, lane);
+    __builtin_amdgcn_sched_barrier(0);  // issue every load above before waiting for the MT index
+    int midx = (int)mi[0];
+#pragma unroll
+    for (int e = 1; e < GPW; ++e) midx = (grp >= e) ? (int)mi[e] : midx;
+    const uint32_t rec = active ? rec_ld : 0u;
+    const int my_action = active ? act_ld : 4;
+    if (!env_ok) midx = MT_N;
+    const uint32_t* mrow = mt_w + (uint32_t)(env_ok ? grp : 0) * MT_WORDS;
 
     DRL_STAMP(1);
     const int y = rec & 255u, x = (rec >> 8) & 255u;
@@ -471,6 +484,16 @@ drl_step_kernel(StepArgs a) {
     int c = (rec >> 16) & 255u;
     int carry = (rec >> 24) & 1u;
     int act = __shfl(my_action, idx, P);  // actions are by drone index (env.py:125)
+    // MT-word prefetch: issued once the records have landed (LDS-DMA makes the
+    // compiler wait for every outstanding load before the first record use),
+    // so its latency overlaps the claim / effect / ordering phases
+    __builtin_amdgcn_sched_barrier(0);
+    const int pf_base0 = midx;
+    int pfn = min(PF, MT_N - midx);
+    uint32_t pfw[PFR];  // next MT words of the stream (addresses clamped: no per-word branch)
+#pragma unroll
+    for (int r = 0; r < PFR; ++r) pfw[r] = mrow[min(midx + j + P * r, MT_N - 1)];
+    __builtin_amdgcn_sched_barrier(0);
     if (active) {
         if (act < 0) act += 5;  // Python negative list index
         if ((unsigned)act > 4u) {
@@ -503,7 +526,8 @@ drl_step_kernel(StepArgs a) {
     }
     const bool claimer = inb && !earlier;
     const bool crashA = active && !claimer;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ground DMA landed
+    // the ground DMA has landed: the compiler waits for LDS-DMA before LDS
+    // reads (and already did, at the first record use); wave_sync orders lanes
     wave_sync();
 
     DRL_STAMP(2);
@@ -748,9 +772,13 @@ drl_step_kernel(StepArgs a) {
         const uint32_t nc = W.cnt[grp * 4];
         const uint16_t* ch = W.chg + grp * nchg;
         uint8_t* gdst = ground_w + (uint32_t)(grp * gstride);
+        // (usually one trip: keep these loops rolled, unrolled/vectorized
+        // copies of them cost registers the whole kernel pays for)
         if (nc <= (uint32_t)nchg) {
+#pragma clang loop unroll(disable) vectorize(disable)
             for (uint32_t q = j; q < nc; q += P) gdst[ch[q]] = gl[ch[q]];
         } else {  // cannot happen (<= 6N changes per step); whole-row fallback
+#pragma clang loop unroll(disable) vectorize(disable)
             for (int v = j; v < gstride / 16; v += P)
                 reinterpret_cast<uint4*>(gdst)[v] = reinterpret_cast<const uint4*>(gl)[v];
         }

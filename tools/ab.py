@@ -4,7 +4,7 @@
 python tools/ab.py --config c3 --rounds 5 --steps 100
 Variants (env knobs read per call): specN = DRL_SPECIALIZE (compile-time
 geometry instance on/off), noobs = step without observation, wide0 = 8-B
-observation stores, stN = DRL_STAGGER.  Prints median/min µs per launch.
+observation stores.  Prints median/min µs per launch.
 """
 import argparse
 import ctypes
@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--variants", default="spec1,spec0,spec1_noobs,spec0_noobs",
-                    help="comma list; each: specN[_noobs][_wide0|_wide1][_stN]")
+                    help="comma list; each: specN[_noobs][_wide0|_wide1]")
     args = ap.parse_args()
     G, N, E, K = CONFIGS[args.config]
     env = BatchedDeliveryDrones(EnvParams(n_drones=N, grid_size=G), E)
@@ -54,7 +54,6 @@ def main():
             parts = v.split("_")
             os.environ["DRL_SPECIALIZE"] = parts[0][4:] if parts[0].startswith("spec") else "1"
             os.environ["DRL_OBS_WIDE"] = "0" if "wide0" in parts else "1"
-            os.environ["DRL_STAGGER"] = next((x[2:] for x in parts if x.startswith("st")), "0")
             k = 0 if "noobs" in parts else K
             o = op if k else None
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
