@@ -88,29 +88,59 @@ def load_traffic(cfg_name: str):
         return None
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(G, N, K, seconds: float):
     """The oracle (C restatement of torch_impl step + WindowedGridView) on host
-    cores, bounded sample; 'port' baseline."""
+    cores, bounded sample; 'port' baseline (the same workload
+    with a static env partition over the host threads, plus a 1-thread figure)."""
     from oracle.oracle import Params, rollout
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
     p = Params(side=G, n_drones=N)
     E = 4096
-    t0 = time.perf_counter()
-    rollout(p, E, 10, nthreads=threads, want_state=False, obs_k=K)
-    dt = time.perf_counter() - t0
-    steps = max(10, int(10 * seconds / max(dt, 1e-3)))
-    t0 = time.perf_counter()
-    rollout(p, E, steps, nthreads=threads, want_state=False, obs_k=K, action_seed=1)
-    dt = time.perf_counter() - t0
+
+    def timed(envs, steps, nthreads):
+        t0 = time.perf_counter()
+        rollout(p, envs, steps, nthreads=nthreads, want_state=False, obs_k=K, action_seed=1)
+        return time.perf_counter() - t0
+
+    # per-step cost from two probe lengths (the reset and thread start-up cancel)
+    t_a, t_b = timed(E, 20, threads), timed(E, 220, threads)
+    per_step = max((t_b - t_a) / 200, 1e-6)
+    steps = max(10, int((seconds - max(t_a - 20 * per_step, 0.0)) / per_step))
+    dt = timed(E, steps, threads)
+    if dt < 0.6 * seconds:  # early-episode steps cost more than steady state: one corrective run
+        steps = int(steps * seconds / dt)
+        dt = timed(E, steps, threads)
+    # single thread, a quarter of the envs, ~1/4 of the time budget
+    e1 = E // 4
+    t1a, t1b = timed(e1, 4, 1), timed(e1, 24, 1)
+    s1 = max(2, int(seconds / 4 / max((t1b - t1a) / 20, 1e-6)))
+    d1 = timed(e1, s1, 1)
+    if d1 < 0.15 * seconds:
+        s1 = int(s1 * seconds / 4 / d1)
+        d1 = timed(e1, s1, 1)
     return {"value": E * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{E} envs x {steps} steps of step()+obs(K={K}) at {G}x{G}/{N} drones, "
-                      f"{threads} host threads, {dt:.1f}s wall"}
+            "sample": f"{E} envs x {steps} steps of reset + step()+obs(K={K}) at {G}x{G}/{N} drones, "
+                      f"{threads} host threads (static env partition), {dt:.1f}s wall",
+            "single_thread_value": e1 * s1 / d1,
+            "single_thread_sample": f"{e1} envs x {s1} steps, 1 thread, {d1:.1f}s wall",
+            "cpu_model": cpu_model()}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--envs", type=int, default=0, help="override envs per GPU")

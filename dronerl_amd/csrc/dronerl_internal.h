@@ -12,7 +12,19 @@ constexpr int MT_M = 397;
 constexpr int MT_WORDS = DRL_MT_WORDS;
 // respawn rounds: D draws per lane (D*P MT outputs per round); the first
 // round's words (>= 16) are prefetched into LDS with the step's other loads
-constexpr int step_draws(int P) { return P == 16 ? 2 : 1; }
+// (tuning knobs for tools/ab.py builds: DRL_DRAWS_P<P> overrides one width)
+#ifndef DRL_DRAWS_P8
+#define DRL_DRAWS_P8 1
+#endif
+#ifndef DRL_DRAWS_P16
+#define DRL_DRAWS_P16 2
+#endif
+#ifndef DRL_DRAWS_P32
+#define DRL_DRAWS_P32 1
+#endif
+constexpr int step_draws(int P) {
+    return P == 8 ? DRL_DRAWS_P8 : P == 16 ? DRL_DRAWS_P16 : P == 32 ? DRL_DRAWS_P32 : 1;
+}
 constexpr int step_pf(int P) { return step_draws(P) * P < 16 ? 16 : step_draws(P) * P; }
 constexpr int OBS_U = 1;        // observation cells per lane per pass (stage: OBS_U*1536 B per wave)
 

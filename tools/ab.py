@@ -27,9 +27,13 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--lib", default="", help="alternative library (tools/variants.py build)")
     ap.add_argument("--variants", default="spec1,spec0,spec1_noobs,spec0_noobs",
                     help="comma list; each: specN[_noobs][_wide0|_wide1]")
     args = ap.parse_args()
+    if args.lib:
+        import dronerl_amd._native as nat
+        nat.LIB_PATH = os.path.abspath(args.lib)
     G, N, E, K = CONFIGS[args.config]
     env = BatchedDeliveryDrones(EnvParams(n_drones=N, grid_size=G), E)
     env.reset(seed=0)
@@ -67,7 +71,7 @@ def main():
                 res[v].append(e0.elapsed_time(e1) * 1e3 / T)
     for v in variants:
         x = res[v]
-        print(f"{args.config} {v:12s} median {statistics.median(x):8.2f} us  min {min(x):8.2f} us  "
+        print(f"{os.path.basename(args.lib) or 'libdronerl.so'} {args.config} {v:12s} median {statistics.median(x):8.2f} us  min {min(x):8.2f} us  "
               f"-> {E / statistics.median(x) * 1e6:.3e} env-steps/s")
 
 
