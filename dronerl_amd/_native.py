@@ -21,7 +21,11 @@ DRL_ERR_NO_FREE_CELL = 2
 
 # Every symbol include/dronerl.h declares (tests check the .so exports them all).
 EXPORTS = ["drl_abi_version", "drl_last_error", "drl_side_from_density", "drl_layout_query", "drl_reset",
-           "drl_step", "drl_obs", "drl_decode", "drl_encode", "drl_synth_actions"]
+           "drl_step", "drl_obs", "drl_decode", "drl_encode", "drl_synth_actions",
+           # library-owned env handles
+           "drl_env_create", "drl_env_destroy", "drl_env_seed", "drl_env_reset", "drl_env_step",
+           "drl_env_step_obs", "drl_env_obs", "drl_env_get_state", "drl_env_set_state", "drl_env_state",
+           "drl_env_errors"]
 
 
 class DrlParams(ctypes.Structure):

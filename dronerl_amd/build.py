@@ -10,7 +10,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdronerl.so")
-SOURCES = [os.path.join(CSRC, "dronerl_kernels.hip"), os.path.join(CSRC, "dronerl_api.cpp")]
+SOURCES = [os.path.join(CSRC, "dronerl_kernels.hip"), os.path.join(CSRC, "dronerl_api.cpp"),
+           os.path.join(CSRC, "dronerl_env.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, "dronerl_internal.h"), os.path.join(REPO, "include", "dronerl.h")]
 ARCH = os.environ.get("DRL_OFFLOAD_ARCH", "gfx950")
 

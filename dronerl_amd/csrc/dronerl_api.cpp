@@ -184,6 +184,9 @@ drl::StepArgs step_args(const drl_params* p, const drl_state* s, const drl_layou
 
 extern "C" {
 
+// error text for dronerl_env.cpp (hidden: not part of the ABI)
+__attribute__((visibility("hidden"))) int drl_internal_fail(const char* msg) { return fail("%s", msg); }
+
 int32_t drl_abi_version(void) { return DRL_ABI_VERSION; }
 
 const char* drl_last_error(void) { return g_err.c_str(); }

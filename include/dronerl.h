@@ -15,6 +15,10 @@
  *   jax_impl/env/env.py:11-35      DroneEnvParams/State   drl_params / drl_state + drl_decode
  *   torch_impl/helpers/rl_helpers.py:12-18 set_seed       drl_reset(reseed=1)
  *
+ * Two layers: stateless calls on caller-owned buffers (drl_reset, drl_step,
+ * ...) and library-owned env handles (drl_env_*) that
+ * forward to them.
+ *
  * Semantics are torch_impl's, bit-exact (state, dict order, done flags, RNG
  * stream), with each env carrying its own CPython-compatible MT19937 stream:
  * env e behaves exactly like `random.seed(seed_base + e); env.reset()` followed
@@ -88,7 +92,7 @@ typedef struct drl_layout {
     int32_t obs_window;     /* 2*radius+1 */
     int32_t obs_floats;     /* floats per observed drone: window^2 * 6 */
     int32_t step_group_lanes; /* wavefront lanes per env in drl_step */
-    int32_t step_lds_bytes;   /* dynamic LDS per 256-thread block of drl_step */
+    int32_t step_lds_bytes;   /* dynamic LDS per block (one wavefront) of drl_step */
 } drl_layout;
 
 /* Device state of num_envs envs (structure of arrays, env-major).
@@ -150,6 +154,64 @@ int drl_encode(const drl_params* p, const drl_state* s, const int32_t* d_order, 
  * (seed, step, env_offset + e, drone) — identical to the oracle's stream. */
 int drl_synth_actions(uint64_t seed, uint64_t step, int64_t env_offset, int64_t num_envs, int32_t n_drones,
                       int32_t* d_actions, hipStream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Env handles: the library owns the state of num_envs
+ * envs on one device; the caller owns actions/rewards/dones/obs.  Every call
+ * except create/destroy/errors is asynchronous on `stream` and allocation-free.
+ * A handle is single-threaded; use one per device/process.
+ *
+ *   B2 row                      here
+ *   drl_create/drl_destroy      drl_env_create / drl_env_destroy
+ *   drl_reset(env, mask)        drl_env_reset (set_seed: drl_env_seed)
+ *   drl_step(env, ...)          drl_env_step / drl_env_step_obs (fused obs)
+ *   drl_obs(env, k, obs)        drl_env_obs
+ *   drl_get_state/set_state     drl_env_get_state / drl_env_set_state
+ * ------------------------------------------------------------------------ */
+typedef struct drl_env drl_env;
+
+/* SoA view of an env batch (device pointers, dense, env-major):
+ *  ground u8 [E][side*side]; order/y/x/charge i32 [E][n_drones] (order = drone
+ *  index at dict position, the rest by drone index); carry u8 [E][n_drones];
+ *  mt u32 [E][625] = CPython's getstate() words 0..623 + index. */
+typedef struct drl_state_view {
+    uint8_t* ground;
+    int32_t* order;
+    int32_t* y;
+    int32_t* x;
+    int32_t* charge;
+    uint8_t* carry;
+    uint32_t* mt;
+} drl_state_view;
+
+/* Allocate the state of num_envs envs on `device`.  Global env index of env e
+ * is env_offset + e (train_jax.py:196-212 sharding); the first drl_env_reset
+ * seeds env e as random.seed(base_seed + env_offset + e). */
+int drl_env_create(const drl_params* p, int32_t device, int64_t num_envs, int64_t env_offset, uint64_t base_seed,
+                   drl_env** out);
+int drl_env_destroy(drl_env* env);
+/* set_seed (rl_helpers.py:12-18): the next reset re-seeds from base_seed. */
+int drl_env_seed(drl_env* env, uint64_t base_seed);
+/* reset() (env.py:68-101) of every env, or of envs with d_env_mask[e] != 0
+ * (the first reset after create/seed must cover every env). */
+int drl_env_reset(drl_env* env, const uint8_t* d_env_mask, hipStream_t stream);
+/* step() (env.py:112-215): actions i32, rewards f32, dones u8, [E][n_drones]. */
+int drl_env_step(drl_env* env, const int32_t* d_actions, float* d_rewards, uint8_t* d_dones, hipStream_t stream);
+/* step() + the WindowedGridView observation of drone indices 0..k-1 after it. */
+int drl_env_step_obs(drl_env* env, const int32_t* d_actions, float* d_rewards, uint8_t* d_dones, int32_t k,
+                     float* d_obs, hipStream_t stream);
+/* WindowedGridView observation (wrappers.py:55-73): f32 [E][k][W][W][6]. */
+int drl_env_obs(drl_env* env, int32_t k, float* d_obs, hipStream_t stream);
+/* Copy the state out to / in from a caller-owned SoA view (NULL fields are
+ * skipped by get_state; set_state needs all of them and trusts their
+ * validity: positions on the grid, distinct cells, charge in [0, 100]). */
+int drl_env_get_state(drl_env* env, const drl_state_view* v, hipStream_t stream);
+int drl_env_set_state(drl_env* env, const drl_state_view* v, hipStream_t stream);
+/* The handle's raw buffers, params and layout (any output may be NULL). */
+int drl_env_state(const drl_env* env, drl_state* s, drl_params* p, drl_layout* L);
+/* Synchronise `stream`, read the OR of DRL_ERR_* bits raised by steps, and
+ * clear them when `clear` != 0. */
+int drl_env_errors(drl_env* env, int32_t* flags, int32_t clear, hipStream_t stream);
 
 #ifdef __cplusplus
 }

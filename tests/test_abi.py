@@ -5,6 +5,7 @@ import re
 import subprocess
 
 import pytest
+import torch
 
 from dronerl_amd import EnvParams, side_from_density
 from dronerl_amd._native import EXPORTS, LIB_PATH, DrlLayout, lib
@@ -85,3 +86,12 @@ def test_from_torch_config():
     p = EnvParams.from_torch_config({'n_drones': 6})
     assert p.side == 11 and p.charge_reward == -0.1
     assert isinstance(DrlLayout(), ctypes.Structure)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-device path")
+def test_env_handle_without_device_fails_cleanly():
+    from dronerl_amd._native import DroneRLError
+    from dronerl_amd.handle import DrlEnvHandle
+    from dronerl_amd.params import EnvParams
+    with pytest.raises(DroneRLError, match="device"):
+        DrlEnvHandle(EnvParams(n_drones=4, grid_size=8), 4)

@@ -435,3 +435,76 @@ def test_gpu_eval_runner_matches_oracle():
     g_agent, g_rnd, g_table = evaluate_sharded(gpu_episode_runner(p, 50, 100), num_evals=7)
     o_agent, o_rnd, o_table = evaluate_sharded(oracle_runner(3, 8, 50, 100), num_evals=7)
     np.testing.assert_allclose(g_table.cpu().numpy(), o_table.numpy(), rtol=0, atol=1e-6)
+
+
+# ------------------------------------------------------ env handles (B2) ---
+def test_env_handle_matches_oracle_and_roundtrips_state():
+    """drl_env_* (library-owned state) == oracle; get_state/set_state round trip
+    continues bit-identically; set_seed re-seeds like random.seed."""
+    from dronerl_amd.handle import DrlEnvHandle
+    p = EnvParams(n_drones=8, grid_size=16)
+    E, off = 257, 1000
+    h = DrlEnvHandle(p, E, env_offset=off, base_seed=5)
+    h.reset()
+    o = OracleMulti(oparams(p), E)
+    o.reset(5 + off + np.arange(E))
+    from dronerl_amd import BatchedDeliveryDrones
+    helper = BatchedDeliveryDrones(p, E, env_offset=off)   # synthetic actions only
+    for t in range(1, 31):
+        a = helper.synth_actions(seed=3, step=t)
+        r, dn, ob = h.step(a, obs_k=1)
+        ro, do = o.step(a.cpu().numpy())
+        assert_rewards(r.cpu().numpy(), ro, f"handle step {t}")
+        np.testing.assert_array_equal(dn.cpu().numpy().astype(bool), do)
+        np.testing.assert_array_equal(ob.cpu().numpy(), o.obs(3, 1))
+    st = h.get_state()
+    want = o.state()
+    np.testing.assert_array_equal(st["ground"].cpu().numpy(), want["ground"])
+    np.testing.assert_array_equal(st["order"].cpu().numpy(), want["order"])
+    np.testing.assert_array_equal(st["y"].cpu().numpy(), want["y"])
+    np.testing.assert_array_equal(st["x"].cpu().numpy(), want["x"])
+    np.testing.assert_array_equal(st["charge"].cpu().numpy(), want["charge"])
+    np.testing.assert_array_equal(st["carry"].cpu().numpy().astype(bool), want["packet"])
+    np.testing.assert_array_equal(st["mt"].cpu().numpy().astype(np.uint32), want["mt"])
+    np.testing.assert_array_equal(h.obs(2).cpu().numpy(), o.obs(3, 2))
+    # round trip into a second handle, then both continue identically
+    h2 = DrlEnvHandle(p, E, env_offset=off)
+    h2.set_state(st)
+    for t in range(31, 41):
+        a = helper.synth_actions(seed=3, step=t)
+        r1, d1 = h.step(a)
+        r2, d2 = h2.step(a)
+        assert torch.equal(r1, r2) and torch.equal(d1, d2)
+    for k in st:
+        assert torch.equal(h.get_state()[k], h2.get_state()[k]), k
+    # masked reset continues the stream; seed() makes the next reset re-seed
+    mask = torch.zeros(E, dtype=torch.uint8, device="cuda")
+    mask[::3] = 1
+    h.reset(mask)
+    h.seed(5)
+    h.reset()
+    o2 = OracleMulti(oparams(p), E)
+    o2.reset(5 + off + np.arange(E))
+    np.testing.assert_array_equal(h.get_state()["ground"].cpu().numpy(), o2.state()["ground"])
+    assert h.errors() == 0
+    bad = torch.full((E, 8), 7, dtype=torch.int32, device="cuda")
+    h.step(bad)
+    assert h.errors() == 1 and h.errors() == 0
+    h.close()
+    h2.close()
+
+
+def test_env_handle_argument_errors():
+    from dronerl_amd._native import DroneRLError
+    from dronerl_amd.handle import DrlEnvHandle
+    p = EnvParams(n_drones=4, grid_size=8)
+    with pytest.raises(DroneRLError, match="num_envs"):
+        DrlEnvHandle(p, 0)
+    with pytest.raises(DroneRLError, match="device"):
+        DrlEnvHandle(p, 4, device=99)
+    h = DrlEnvHandle(p, 4)
+    with pytest.raises(DroneRLError, match="before the first reset"):
+        h.step(torch.zeros((4, 4), dtype=torch.int32, device="cuda"))
+    with pytest.raises(DroneRLError, match="first reset"):
+        h.reset(torch.ones(4, dtype=torch.uint8, device="cuda"))
+    h.close()
