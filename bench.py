@@ -137,6 +137,49 @@ def cpu_baseline(G, N, K, seconds: float):
             "cpu_model": cpu_model()}
 
 
+def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream):
+    """the C3 loop's consumer of the observation, timed
+    separately from the env step.  (1) drl_qnet_act alone on the resident obs
+    (dense 294->128->64->5 on MFMA, epsilon-greedy, writes actions[:, 0]):
+    HBM-bound on reading the obs (E * W*W*6 f32); (2) the train_jax.py:42-64
+    loop shape per step: act -> step + obs -> replay add_many (capacity 10000)."""
+    from dronerl_amd.dqn import QNetwork, ReplayBuffer
+    E = env.num_envs
+    D = obs[0].numel()
+    net = QNetwork(D, (128, 64), device=env.device, generator=torch.Generator().manual_seed(0))
+    rb = ReplayBuffer(10000, D, env.device)
+    flat = obs.reshape(E, -1)
+    a0 = actions[0]
+    for t in range(warmup):
+        net.act(flat, 0.1, seed=1, step=t, actions=a0)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record(stream)
+    for t in range(steps):
+        net.act(flat, 0.1, seed=1, step=t, actions=a0)
+    ev[1].record(stream)
+    # loop shape: act on obs_t, step writing obs_t+1 into the other buffer, add the transition
+    bufs = [obs, torch.empty_like(obs)]
+    ev[2].record(stream)
+    for t in range(steps):
+        cur, nxt = bufs[t & 1], bufs[(t + 1) & 1]
+        a = actions[t % actions.shape[0]]
+        net.act(cur.reshape(E, -1), 0.1, seed=1, step=t, actions=a)
+        env.step(a, obs_k=1, rewards=rewards, dones=dones, obs=nxt)
+        rb.add_many(cur, a, rewards, nxt, dones)
+    ev[3].record(stream)
+    torch.cuda.synchronize()
+    env.check_errors()
+    act_s = ev[0].elapsed_time(ev[1]) / 1e3 / steps
+    loop_s = ev[2].elapsed_time(ev[3]) / 1e3 / steps
+    read = E * D * 4
+    return {"net": f"dense {D}->128->64->5, bf16 MFMA (f32 accumulate)", "act_us": act_s * 1e6,
+            "act_roofline": {"bound": "hbm", "achieved": read / act_s / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": read / act_s / 1e9 / PEAK_HBM_GBS,
+                             "algorithmic_bytes_per_env": D * 4 + 4},
+            "loop_us_per_step": loop_s * 1e6, "loop_env_steps_per_s": E / loop_s,
+            "loop": "act(obs_t) -> step + obs(K=1) -> replay add_many(obs_t, a, r, obs_t+1, done), capacity 10000"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,6 +190,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-reset-bench", action="store_true")
+    ap.add_argument("--no-dqn", action="store_true", help="skip the DQN-consumer measurement (SURVEY.md §8 F1)")
     ap.add_argument("--obs-k", type=int, default=-1,
                     help="diagnostic: observed drones per step (default: the config's; 0 = step without obs)")
     args = ap.parse_args()
@@ -235,6 +279,10 @@ def main():
         torch.cuda.synchronize()
         resets_per_s = E * world * nres / (r0.elapsed_time(r1) / 1e3)
 
+    dqn = None
+    if K >= 1 and not args.no_dqn:
+        dqn = dqn_consumer_bench(env, actions, rewards, dones, obs, args.warmup, min(args.steps, 200), stream)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(G, N, K, args.cpu_seconds)
@@ -270,6 +318,7 @@ def main():
                          "frac_read_plus_write": achieved_rw / PEAK_HBM_GBS},
             "cpu_baseline": cpu,
             "resets_per_s": resets_per_s,
+            "dqn_consumer": dqn,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -25,7 +25,9 @@ EXPORTS = ["drl_abi_version", "drl_last_error", "drl_side_from_density", "drl_la
            # library-owned env handles
            "drl_env_create", "drl_env_destroy", "drl_env_seed", "drl_env_reset", "drl_env_step",
            "drl_env_step_obs", "drl_env_obs", "drl_env_get_state", "drl_env_set_state", "drl_env_state",
-           "drl_env_errors"]
+           "drl_env_errors",
+           # DQN consumer
+           "drl_qnet_packed_bytes", "drl_qnet_pack", "drl_qnet_act", "drl_replay_add"]
 
 
 class DrlParams(ctypes.Structure):

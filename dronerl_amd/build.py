@@ -11,7 +11,8 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdronerl.so")
 SOURCES = [os.path.join(CSRC, "dronerl_kernels.hip"), os.path.join(CSRC, "dronerl_api.cpp"),
-           os.path.join(CSRC, "dronerl_env.cpp")]
+           os.path.join(CSRC, "dronerl_env.cpp"), os.path.join(CSRC, "dronerl_qnet.hip"),
+           os.path.join(CSRC, "dronerl_qnet_api.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, "dronerl_internal.h"), os.path.join(REPO, "include", "dronerl.h")]
 ARCH = os.environ.get("DRL_OFFLOAD_ARCH", "gfx950")
 

@@ -105,6 +105,73 @@ struct ResetArgs {
     FastDiv div_side;
 };
 
+// Q-network (dronerl_qnet.hip).  Layer 0 = input -> hidden[0], ..., layer
+// n_hidden = last hidden -> actions.  Fragment offsets in 16-B units (one
+// fragment = 64 lanes x 16 B), bias offsets in floats after the fragments.
+constexpr int QN_MAX_LAYERS = 4;
+struct QnetLayout {
+    int n_layers;
+    int nt[QN_MAX_LAYERS];        // 32-row output tiles
+    int kt[QN_MAX_LAYERS];        // 16-wide K slices
+    int in[QN_MAX_LAYERS], out[QN_MAX_LAYERS];
+    int frag_off[QN_MAX_LAYERS];  // uint4 offset of the layer's fragments
+    int bias_off[QN_MAX_LAYERS];  // float offset of the layer's biases (padded to 32 * nt)
+    int frag_total;               // uint4s of fragments
+    int n_bias;                   // floats of biases
+    int lds_vec;                  // uint4s of the whole packed net
+};
+
+struct QnetPack {
+    int n_layers;
+    int frag_off[QN_MAX_LAYERS], kt[QN_MAX_LAYERS], in[QN_MAX_LAYERS], out[QN_MAX_LAYERS];
+    int bias_off[QN_MAX_LAYERS];
+    const float* w[QN_MAX_LAYERS];
+    const float* b[QN_MAX_LAYERS];
+    int64_t n_wfrag_elems, n_bias;
+    uint16_t* packed_w;  // bf16 bits
+    float* packed_b;
+};
+
+struct QnetArgs {
+    int in_features, kt0, n_hidden, n_actions;
+    int nt[QN_MAX_LAYERS];
+    int frag_off[QN_MAX_LAYERS], bias_off[QN_MAX_LAYERS];
+    int frag_total, lds_vec, n_bias;
+    const uint4* packed;
+    const float* obs;
+    int64_t obs_stride, E;
+    float epsilon;
+    uint64_t seed, step;
+    int64_t env_offset;
+    int32_t* actions;
+    int64_t action_stride;
+    float* q;
+};
+
+struct ReplayArgs {
+    int64_t first, n, cursor, capacity;
+    int obs_floats;
+    const float* obs;
+    int64_t obs_stride;
+    const float* next_obs;
+    int64_t next_obs_stride;
+    const int32_t* actions;
+    int64_t action_stride;
+    const float* rewards;
+    int64_t reward_stride;
+    const uint8_t* dones;
+    int64_t done_stride;
+    float* buf_obs;
+    float* buf_next_obs;
+    int32_t* buf_actions;
+    float* buf_rewards;
+    uint8_t* buf_dones;
+};
+
+hipError_t launch_qnet_pack(const QnetPack& p, hipStream_t s);
+hipError_t launch_qnet_act(const QnetArgs& a, int num_cus, hipStream_t s);
+hipError_t launch_replay_add(const ReplayArgs& a, hipStream_t s);
+
 hipError_t launch_step(const StepArgs& a, int P, hipStream_t s, bool obs_only);
 hipError_t launch_reset(const ResetArgs& a, hipStream_t s);
 hipError_t launch_decode(const uint32_t* drones, int64_t E, int N, int32_t* order, int32_t* y, int32_t* x,

@@ -1,0 +1,194 @@
+// dronerl_qnet_api.cpp — C ABI of the DQN consumer (include/dronerl.h,
+// drl_qnet_* / drl_replay_add; kernels in dronerl_qnet.hip).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../../include/dronerl.h"
+#include "dronerl_internal.h"
+
+extern "C" __attribute__((visibility("hidden"))) int drl_internal_fail(const char* msg);
+
+namespace {
+
+constexpr int kQnetLdsMax = 160 * 1024;
+
+int fail(const char* m) { return drl_internal_fail(m); }
+
+// Validate a description and lay the packed net out (see QnetLayout).
+int qnet_layout(const drl_qnet_desc* d, drl::QnetLayout* L) {
+    if (!d) return fail("qnet desc is NULL");
+    if (d->in_features < 4 || d->in_features > 512 || (d->in_features & 1))
+        return fail("in_features must be even and in [4, 512]");
+    if (d->n_hidden < 1 || d->n_hidden > 3) return fail("n_hidden must be 1, 2 or 3");
+    for (int i = 0; i < d->n_hidden; ++i)
+        if (d->hidden[i] < 32 || d->hidden[i] > 128 || d->hidden[i] % 32)
+            return fail("hidden widths must be multiples of 32 in [32, 128]");
+    if (d->n_actions < 1 || d->n_actions > 8) return fail("n_actions must be in [1, 8]");
+    memset(L, 0, sizeof *L);
+    L->n_layers = d->n_hidden + 1;
+    int frag = 0, bias = 0;
+    for (int l = 0; l < L->n_layers; ++l) {
+        L->in[l] = l == 0 ? d->in_features : d->hidden[l - 1];
+        L->out[l] = l < d->n_hidden ? d->hidden[l] : d->n_actions;
+        L->nt[l] = (L->out[l] + 31) / 32;
+        // layer 0: K-slices padded to a multiple of the act kernel's slice ring (5)
+        L->kt[l] = l == 0 ? ((d->in_features + 15) / 16 + 4) / 5 * 5 : 2 * L->nt[l - 1];
+        L->frag_off[l] = frag * 64;
+        L->bias_off[l] = bias;
+        frag += L->nt[l] * L->kt[l];
+        bias += 32 * L->nt[l];
+    }
+    L->frag_total = frag * 64;
+    L->n_bias = bias;
+    L->lds_vec = L->frag_total + (bias + 3) / 4;
+    if (L->lds_vec * 16 > kQnetLdsMax) return fail("the packed network does not fit the 160 KB LDS of a CU");
+    return 0;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    char buf[256];
+    snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+    return fail(buf);
+}
+
+int num_cus() {
+    static std::mutex mu;
+    static std::vector<int> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    std::lock_guard<std::mutex> g(mu);
+    if ((int)cache.size() <= dev) cache.resize(dev + 1, 0);
+    if (!cache[dev]) {
+        int n = 0;
+        cache[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+    }
+    return cache[dev];
+}
+
+}  // namespace
+
+extern "C" {
+
+int drl_qnet_packed_bytes(const drl_qnet_desc* d, int64_t* bytes) {
+    drl::QnetLayout L;
+    if (qnet_layout(d, &L)) return -1;
+    if (!bytes) return fail("bytes is NULL");
+    *bytes = (int64_t)L.lds_vec * 16;
+    return 0;
+}
+
+int drl_qnet_pack(const drl_qnet_desc* d, const float* const* d_weights, const float* const* d_biases, void* d_packed,
+                  hipStream_t stream) {
+    drl::QnetLayout L;
+    if (qnet_layout(d, &L)) return -1;
+    if (!d_weights || !d_biases || !d_packed) return fail("weights/biases/packed must be non-NULL");
+    if ((uintptr_t)d_packed % 16) return fail("packed buffer must be 16-byte aligned");
+    drl::QnetPack p;
+    memset(&p, 0, sizeof p);
+    p.n_layers = L.n_layers;
+    for (int l = 0; l < L.n_layers; ++l) {
+        if (!d_weights[l] || !d_biases[l]) return fail("a weight or bias pointer is NULL");
+        p.frag_off[l] = L.frag_off[l];
+        p.kt[l] = L.kt[l];
+        p.in[l] = L.in[l];
+        p.out[l] = L.out[l];
+        p.bias_off[l] = L.bias_off[l];
+        p.w[l] = d_weights[l];
+        p.b[l] = d_biases[l];
+    }
+    p.n_wfrag_elems = (int64_t)L.frag_total * 8;
+    p.n_bias = L.n_bias;
+    p.packed_w = static_cast<uint16_t*>(d_packed);
+    p.packed_b = reinterpret_cast<float*>(static_cast<uint8_t*>(d_packed) + (size_t)L.frag_total * 16);
+    hipError_t e = drl::launch_qnet_pack(p, stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_qnet_pack launch");
+}
+
+int drl_qnet_act(const drl_qnet_desc* d, const void* d_packed, const float* d_obs, int64_t num_envs,
+                 int64_t obs_stride, float epsilon, uint64_t seed, uint64_t step, int64_t env_offset,
+                 int32_t* d_actions, int64_t action_stride, float* d_q, hipStream_t stream) {
+    drl::QnetLayout L;
+    if (qnet_layout(d, &L)) return -1;
+    if (num_envs < 0) return fail("num_envs < 0");
+    if (num_envs == 0) return 0;
+    if (!d_packed || !d_obs || !d_actions) return fail("packed/obs/actions must be non-NULL");
+    if ((uintptr_t)d_packed % 16) return fail("packed buffer must be 16-byte aligned");
+    if ((uintptr_t)d_obs % 8 || obs_stride % 2) return fail("obs rows must be 8-byte aligned (even obs_stride)");
+    if (obs_stride < d->in_features) return fail("obs_stride < in_features");
+    if (num_envs * obs_stride * 4 >= ((int64_t)1 << 32)) return fail("obs larger than 4 GiB (32-bit row offsets)");
+    if (action_stride < 1) return fail("action_stride must be >= 1");
+    drl::QnetArgs a;
+    memset(&a, 0, sizeof a);
+    a.in_features = d->in_features;
+    a.kt0 = L.kt[0];
+    a.n_hidden = d->n_hidden;
+    a.n_actions = d->n_actions;
+    for (int l = 0; l < L.n_layers; ++l) {
+        a.nt[l] = L.nt[l];
+        a.frag_off[l] = L.frag_off[l];
+        a.bias_off[l] = L.bias_off[l];
+    }
+    a.frag_total = L.frag_total;
+    a.lds_vec = L.lds_vec;
+    a.n_bias = L.n_bias;
+    a.packed = static_cast<const uint4*>(d_packed);
+    a.obs = d_obs;
+    a.obs_stride = obs_stride;
+    a.E = num_envs;
+    a.epsilon = epsilon;
+    a.seed = seed;
+    a.step = step;
+    a.env_offset = env_offset;
+    a.actions = d_actions;
+    a.action_stride = action_stride;
+    a.q = d_q;
+    hipError_t e = drl::launch_qnet_act(a, num_cus(), stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_qnet_act launch");
+}
+
+int drl_replay_add(const drl_replay* r, int64_t cursor, int64_t n, const float* d_obs, int64_t obs_stride,
+                   const float* d_next_obs, int64_t next_obs_stride, const int32_t* d_actions, int64_t action_stride,
+                   const float* d_rewards, int64_t reward_stride, const uint8_t* d_dones, int64_t done_stride,
+                   hipStream_t stream) {
+    if (!r) return fail("replay is NULL");
+    if (r->capacity < 1 || r->obs_floats < 2 || (r->obs_floats & 1))
+        return fail("replay capacity must be >= 1 and obs_floats even");
+    if (!r->obs || !r->next_obs || !r->actions || !r->rewards || !r->dones) return fail("replay buffers are NULL");
+    if (n < 0 || cursor < 0) return fail("n and cursor must be >= 0");
+    if (n == 0) return 0;
+    if (!d_obs || !d_next_obs || !d_actions || !d_rewards || !d_dones) return fail("batch pointers are NULL");
+    if ((uintptr_t)d_obs % 8 || (uintptr_t)d_next_obs % 8 || (uintptr_t)r->obs % 8 || (uintptr_t)r->next_obs % 8 ||
+        obs_stride % 2 || next_obs_stride % 2)
+        return fail("observation rows must be 8-byte aligned");
+    drl::ReplayArgs a;
+    memset(&a, 0, sizeof a);
+    a.n = n;
+    a.first = n > r->capacity ? n - r->capacity : 0;  // earlier ones would be overwritten in the same call
+    a.cursor = cursor % r->capacity;
+    a.capacity = r->capacity;
+    a.obs_floats = r->obs_floats;
+    a.obs = d_obs;
+    a.obs_stride = obs_stride;
+    a.next_obs = d_next_obs;
+    a.next_obs_stride = next_obs_stride;
+    a.actions = d_actions;
+    a.action_stride = action_stride;
+    a.rewards = d_rewards;
+    a.reward_stride = reward_stride;
+    a.dones = d_dones;
+    a.done_stride = done_stride;
+    a.buf_obs = r->obs;
+    a.buf_next_obs = r->next_obs;
+    a.buf_actions = r->actions;
+    a.buf_rewards = r->rewards;
+    a.buf_dones = r->dones;
+    hipError_t e = drl::launch_replay_add(a, stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_replay_add launch");
+}
+
+}  // extern "C"

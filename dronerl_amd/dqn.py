@@ -1,0 +1,184 @@
+"""On-device DQN consumer of the observation.
+
+Reference: jax_impl/agents/dqn.py DenseQNetwork (:47-63) and DQNAgent.act
+(:132-146), train_jax.py:42-64 (drone 0 of every env follows the agent; the
+transition of drone 0 goes to the replay buffer), jax_impl/buffers.py:18-93.
+
+`QNetwork` holds fp32 parameters (torch nn.Linear layout [out][in]; a flax
+Dense kernel is the transpose) and packs them for the MFMA kernel
+(drl_qnet_pack) whenever they change; `act` runs the forward + epsilon-greedy
+choice for every env in one launch (drl_qnet_act, bf16 operands with f32
+accumulation).  `ReplayBuffer.add_many` is drl_replay_add; `sample` is plain
+torch indexing (64 rows).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import torch
+
+from ._native import DroneRLError, lib
+
+NUM_ACTIONS = 5  # common/constants.py Action
+
+
+class DrlQnetDesc(ctypes.Structure):
+    _fields_ = [("in_features", ctypes.c_int32), ("n_hidden", ctypes.c_int32),
+                ("hidden", ctypes.c_int32 * 3), ("n_actions", ctypes.c_int32)]
+
+
+class DrlReplay(ctypes.Structure):
+    _fields_ = [("capacity", ctypes.c_int64), ("obs_floats", ctypes.c_int32), ("obs", ctypes.c_void_p),
+                ("next_obs", ctypes.c_void_p), ("actions", ctypes.c_void_p), ("rewards", ctypes.c_void_p),
+                ("dones", ctypes.c_void_p)]
+
+
+_vp = ctypes.c_void_p
+
+
+def _bind(L):
+    if getattr(L, "_qnet_ready", False):
+        return L
+    i32, i64, u64, f32 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float
+    D = ctypes.POINTER(DrlQnetDesc)
+    sig = {
+        "drl_qnet_packed_bytes": [D, ctypes.POINTER(i64)],
+        "drl_qnet_pack": [D, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp, _vp],
+        "drl_qnet_act": [D, _vp, _vp, i64, i64, f32, u64, u64, i64, _vp, i64, _vp, _vp],
+        "drl_replay_add": [ctypes.POINTER(DrlReplay), i64, i64, _vp, i64, _vp, i64, _vp, i64, _vp, i64, _vp, i64, _vp],
+    }
+    for name, args in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = ctypes.c_int
+    L._qnet_ready = True
+    return L
+
+
+def _check(L, rc):
+    if rc:
+        raise DroneRLError(L.drl_last_error().decode())
+
+
+def _stream(device):
+    return _vp(torch.cuda.current_stream(device).cuda_stream)
+
+
+class QNetwork:
+    """Dense Q-network: in_features -> hidden... (ReLU) -> n_actions."""
+
+    def __init__(self, in_features: int, hidden: Sequence[int] = (32, 32), n_actions: int = NUM_ACTIONS,
+                 device=None, generator: Optional[torch.Generator] = None):
+        self.L = _bind(lib())
+        self.device = torch.device(device if device is not None else "cuda")
+        self.in_features, self.hidden, self.n_actions = in_features, tuple(hidden), n_actions
+        sizes = [in_features, *self.hidden, n_actions]
+        self.weights, self.biases = [], []
+        for i in range(len(sizes) - 1):
+            fan_in = sizes[i]
+            # he_normal for the hidden layers (dqn.py:53), lecun-normal-like for the output
+            std = (2.0 / fan_in) ** 0.5 if i < len(sizes) - 2 else (1.0 / fan_in) ** 0.5
+            w = torch.randn((sizes[i + 1], fan_in), generator=generator) * std
+            self.weights.append(w.to(self.device))
+            self.biases.append(torch.zeros(sizes[i + 1], device=self.device))
+        self.desc = DrlQnetDesc(in_features, len(self.hidden), (ctypes.c_int32 * 3)(*self.hidden, *[0] * (3 - len(self.hidden))),
+                                n_actions)
+        nb = ctypes.c_int64()
+        _check(self.L, self.L.drl_qnet_packed_bytes(ctypes.byref(self.desc), ctypes.byref(nb)))
+        self.packed = torch.empty(nb.value // 4, dtype=torch.int32, device=self.device)  # 16-B aligned
+        self.pack()
+
+    def load(self, weights: Sequence[torch.Tensor], biases: Sequence[torch.Tensor]):
+        """Set parameters (torch layout [out][in]) and re-pack."""
+        if len(weights) != len(self.weights) or len(biases) != len(self.biases):
+            raise ValueError("layer count mismatch")
+        for i, (w, b) in enumerate(zip(weights, biases)):
+            if tuple(w.shape) != tuple(self.weights[i].shape) or tuple(b.shape) != tuple(self.biases[i].shape):
+                raise ValueError(f"layer {i}: shape {tuple(w.shape)} != {tuple(self.weights[i].shape)}")
+            self.weights[i] = w.detach().to(self.device, torch.float32).contiguous()
+            self.biases[i] = b.detach().to(self.device, torch.float32).contiguous()
+        self.pack()
+
+    def pack(self):
+        n = len(self.weights)
+        wp = (_vp * n)(*[w.data_ptr() for w in self.weights])
+        bp = (_vp * n)(*[b.data_ptr() for b in self.biases])
+        _check(self.L, self.L.drl_qnet_pack(ctypes.byref(self.desc), wp, bp, _vp(self.packed.data_ptr()),
+                                            _stream(self.device)))
+
+    def reference_q(self, obs: torch.Tensor, bf16_operands: bool = False) -> torch.Tensor:
+        """Plain torch forward (checker for tests); bf16_operands rounds the
+        weights, inputs and hidden activations to bf16 as the MFMA path does."""
+        r = (lambda t: t.to(torch.bfloat16).to(torch.float32)) if bf16_operands else (lambda t: t)
+        x = r(obs.reshape(obs.shape[0], -1).to(torch.float32))
+        for i, (w, b) in enumerate(zip(self.weights, self.biases)):
+            x = x @ r(w).t() + b
+            if i < len(self.weights) - 1:
+                x = r(torch.relu(x))
+        return x
+
+    def act(self, obs: torch.Tensor, epsilon: float, seed: int = 0, step: int = 0, env_offset: int = 0,
+            actions: Optional[torch.Tensor] = None, q_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Epsilon-greedy action for each row of obs [E, ..., in_features].
+        `actions` may be an [E, n_drones] int32 tensor: column 0 is written (the
+        other drones keep their actions, train_jax.py:47-49)."""
+        E = obs.shape[0]
+        flat = obs.reshape(E, -1)
+        if flat.shape[1] < self.in_features or flat.dtype != torch.float32:
+            raise ValueError("obs must be float32 with at least in_features values per env")
+        if actions is None:
+            actions = torch.empty((E, 1), dtype=torch.int32, device=self.device)
+        if actions.dtype != torch.int32 or actions.shape[0] != E or not actions.is_contiguous():
+            raise ValueError("actions must be a contiguous int32 [E, n] tensor")
+        stride_a = actions.shape[1] if actions.dim() == 2 else 1
+        _check(self.L, self.L.drl_qnet_act(ctypes.byref(self.desc), _vp(self.packed.data_ptr()), _vp(flat.data_ptr()),
+                                           E, flat.stride(0), float(epsilon), seed & (2**64 - 1), step, env_offset,
+                                           _vp(actions.data_ptr()), stride_a,
+                                           None if q_out is None else _vp(q_out.data_ptr()), _stream(self.device)))
+        return actions
+
+
+@dataclass
+class ReplayBuffer:
+    """jax_impl/buffers.py ReplayBuffer on device tensors (drone-0 transitions)."""
+    capacity: int
+    obs_floats: int
+    device: torch.device
+
+    def __post_init__(self):
+        self.L = _bind(lib())
+        d = torch.device(self.device)
+        self.obs = torch.zeros((self.capacity, self.obs_floats), device=d)
+        self.next_obs = torch.zeros((self.capacity, self.obs_floats), device=d)
+        self.actions = torch.zeros(self.capacity, dtype=torch.int32, device=d)
+        self.rewards = torch.zeros(self.capacity, device=d)
+        self.dones = torch.zeros(self.capacity, dtype=torch.uint8, device=d)
+        self.cursor = 0          # current_idx
+        self.size = 0            # current_size
+        self._c = DrlReplay(self.capacity, self.obs_floats, self.obs.data_ptr(), self.next_obs.data_ptr(),
+                            self.actions.data_ptr(), self.rewards.data_ptr(), self.dones.data_ptr())
+
+    def add_many(self, obs: torch.Tensor, actions: torch.Tensor, rewards: torch.Tensor, next_obs: torch.Tensor,
+                 dones: torch.Tensor):
+        """buffers.py:57-80.  obs/next_obs [E, >= obs_floats] f32 rows; actions
+        i32, rewards f32, dones u8 as [E] or [E, n_drones] (column 0 taken)."""
+        E = obs.shape[0]
+        o, no = obs.reshape(E, -1), next_obs.reshape(E, -1)
+        col = lambda t: t.shape[1] if t.dim() == 2 else 1  # noqa: E731
+        _check(self.L, self.L.drl_replay_add(ctypes.byref(self._c), self.cursor, E, _vp(o.data_ptr()), o.stride(0),
+                                             _vp(no.data_ptr()), no.stride(0), _vp(actions.data_ptr()), col(actions),
+                                             _vp(rewards.data_ptr()), col(rewards), _vp(dones.data_ptr()), col(dones),
+                                             _stream(self.obs.device)))
+        self.cursor = (self.cursor + E) % self.capacity
+        self.size = min(self.size + E, self.capacity)
+
+    def can_sample(self, batch: int = 64) -> bool:
+        return self.size >= batch
+
+    def sample(self, batch: int = 64, generator: Optional[torch.Generator] = None) -> dict:
+        """buffers.py:82-93: uniform indices in [0, size)."""
+        idx = torch.randint(0, self.size, (batch,), device=self.obs.device, generator=generator)
+        return dict(obs=self.obs[idx], actions=self.actions[idx], rewards=self.rewards[idx],
+                    next_obs=self.next_obs[idx], dones=self.dones[idx])

@@ -213,6 +213,58 @@ int drl_env_state(const drl_env* env, drl_state* s, drl_params* p, drl_layout* L
  * clear them when `clear` != 0. */
 int drl_env_errors(drl_env* env, int32_t* flags, int32_t clear, hipStream_t stream);
 
+/* ------------------------------------------------------------------------
+ * DQN consumer of the observation, on MFMA (bf16 operands,
+ * f32 accumulate): the dense Q-network of jax_impl/agents/dqn.py:47-63
+ * (Dense(h) + ReLU per hidden layer, then Dense(n_actions)) and the
+ * epsilon-greedy act of dqn.py:132-146 for every env (train_jax.py:42-49:
+ * drone 0 follows the agent), plus ReplayBuffer.add_many (buffers.py:57-80).
+ * ------------------------------------------------------------------------ */
+typedef struct drl_qnet_desc {
+    int32_t in_features;  /* observation floats, W*W*6 (even, <= 512) */
+    int32_t n_hidden;     /* 1..3 hidden layers */
+    int32_t hidden[3];    /* widths: multiples of 32 in [32, 128] */
+    int32_t n_actions;    /* 1..8 (Action.num_actions() = 5) */
+} drl_qnet_desc;
+
+/* Bytes of the packed network (bf16 weight fragments + f32 biases). */
+int drl_qnet_packed_bytes(const drl_qnet_desc* d, int64_t* bytes);
+/* Pack the network once per weight update.  d_weights / d_biases: host arrays
+ * of n_hidden + 1 device pointers; layer l weights f32 [out][in] row-major
+ * (torch nn.Linear; a flax Dense kernel is its transpose), biases f32 [out].
+ * d_packed: 16-byte aligned device buffer of drl_qnet_packed_bytes. */
+int drl_qnet_pack(const drl_qnet_desc* d, const float* const* d_weights, const float* const* d_biases, void* d_packed,
+                  hipStream_t stream);
+/* actions[e * action_stride] = u_e < epsilon ? random action : argmax_a Q(obs_e)
+ * for e < num_envs (first maximum on ties, like jnp.argmax).  obs f32 rows of
+ * obs_stride floats (8-byte aligned).  u_e and the random action come from a
+ * counter hash of (seed, step, env_offset + e).  d_q (nullable): Q f32
+ * [num_envs][n_actions]. */
+int drl_qnet_act(const drl_qnet_desc* d, const void* d_packed, const float* d_obs, int64_t num_envs,
+                 int64_t obs_stride, float epsilon, uint64_t seed, uint64_t step, int64_t env_offset,
+                 int32_t* d_actions, int64_t action_stride, float* d_q, hipStream_t stream);
+
+/* Replay ring buffer storage (device, caller-owned): obs/next_obs f32
+ * [capacity][obs_floats], actions i32, rewards f32, dones u8 [capacity]. */
+typedef struct drl_replay {
+    int64_t capacity;
+    int32_t obs_floats;
+    float* obs;
+    float* next_obs;
+    int32_t* actions;
+    float* rewards;
+    uint8_t* dones;
+} drl_replay;
+
+/* add_many: transition i -> slot (cursor + i) % capacity, i < n; strides in
+ * elements (e.g. action_stride = n_drones to take drone 0 of [E][n_drones]).
+ * With n > capacity only the last `capacity` transitions are written (what a
+ * sequential add() loop leaves).  The caller advances cursor by n. */
+int drl_replay_add(const drl_replay* r, int64_t cursor, int64_t n, const float* d_obs, int64_t obs_stride,
+                   const float* d_next_obs, int64_t next_obs_stride, const int32_t* d_actions, int64_t action_stride,
+                   const float* d_rewards, int64_t reward_stride, const uint8_t* d_dones, int64_t done_stride,
+                   hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
