@@ -111,11 +111,11 @@ struct ResetArgs {
 constexpr int QN_MAX_LAYERS = 4;
 struct QnetLayout {
     int n_layers;
-    int nt[QN_MAX_LAYERS];        // 32-row output tiles
-    int kt[QN_MAX_LAYERS];        // 16-wide K slices
+    int nt[QN_MAX_LAYERS];        // 16-row output tiles
+    int kt[QN_MAX_LAYERS];        // 32-wide K slices
     int in[QN_MAX_LAYERS], out[QN_MAX_LAYERS];
     int frag_off[QN_MAX_LAYERS];  // uint4 offset of the layer's fragments
-    int bias_off[QN_MAX_LAYERS];  // float offset of the layer's biases (padded to 32 * nt)
+    int bias_off[QN_MAX_LAYERS];  // float offset of the layer's biases (padded to 16 * nt)
     int frag_total;               // uint4s of fragments
     int n_bias;                   // floats of biases
     int lds_vec;                  // uint4s of the whole packed net

@@ -7,16 +7,17 @@
 // action : argmax Q), train_jax.py:42-49 (drone 0 of every env follows the
 // agent), jax_impl/buffers.py:57-80 ReplayBuffer.add_many.
 //
-// MFMA layout (gfx950 v_mfma_f32_32x32x16_bf16, bf16 operands, f32 accumulate):
-// envs are the MFMA column dimension, so layer l computes H_lᵀ = W_l · H_{l-1}ᵀ
-// in 32(units) x 32(envs) tiles.  Lane l (r = l&31, h = l>>5) holds
-// A[row r][k = 8h+j] and B[k = 8h+j][col r] (j = 0..7); the accumulator holds
-// rows (i&3) + 8(i>>2) + 4h of column r in register i.  Registers 8s..8s+7 of
-// an accumulator tile are therefore exactly the B fragment of K-slice s of the
-// next layer when that layer's weights are packed with the matching K order
-// (unit 16s + (j<4 ? 4h+j : 8+4h+j-4)): activations never leave registers.
-// Weights are packed once (drl_qnet_pack) into lane-fragment order and staged
-// into LDS per workgroup (one 16-B ds_read per lane per MFMA, conflict-free).
+// MFMA layout (gfx950 v_mfma_f32_16x16x32_bf16, bf16 operands, f32
+// accumulate): envs are the MFMA column dimension, so layer l computes
+// H_lᵀ = W_l · H_{l-1}ᵀ in 16(units) x 16(envs) tiles over 32-wide K-slices.
+// Lane l (c = l&15, g = l>>4) holds A[row c][k(g, j)] and B[k(g, j)][col c]
+// for j = 0..7, and the accumulator holds rows 4g + i of column c in register
+// i.  With the K order k(g, j) = j<4 ? 4g+j : 16+4g+(j-4), registers 0..3 of
+// accumulator tiles 2s and 2s+1 are exactly the B fragment of the next
+// layer's K-slice s (activations never leave registers), and for the input
+// layer the four lanes of an env read 64 contiguous bytes of its row per load.
+// Weights are packed once (drl_qnet_pack) into that lane-fragment order and
+// staged into LDS per workgroup (one 16-B ds_read per lane per MFMA).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -27,7 +28,7 @@
 namespace drl {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint64_t qn_splitmix64(uint64_t z) {
     z += 0x9e3779b97f4a7c15ull;
@@ -36,17 +37,15 @@ __device__ __forceinline__ uint64_t qn_splitmix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
-// A-operand K index (within a 16-wide slice) of fragment element j for lane
-// half h, for layers fed by an accumulator (see the header comment).
-__device__ __forceinline__ int acc_k(int h, int j) { return j < 4 ? 4 * h + j : 8 + 4 * h + (j - 4); }
+// K index within a 32-wide slice of fragment element j for lane group g (see
+// the header comment).
+__device__ __forceinline__ int frag_k(int g, int j) { return j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4); }
 
 // ------------------------------------------------------------------ pack ---
 // One thread per packed bf16 element: fragment (m, t) of layer l is 64 lanes x
-// 8 elements, element j of lane (r, h) = W_l[32m + r][16t + acc_k(h, j)]
+// 8 elements, element j of lane (c, g) = W_l[16m + c][32t + frag_k(g, j)]
 // (torch nn.Linear layout [out][in]); zero outside the matrix.  Biases follow
-// as f32.  Layer 0 uses the same K order: its B fragment is loaded as two
-// quads, features 16t+4h.. and 16t+8+4h.., so a lane pair reads 32 contiguous
-// bytes of a row per load instruction.
+// as f32.
 __global__ void drl_qnet_pack_kernel(QnetPack p) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < p.n_wfrag_elems) {
@@ -57,9 +56,9 @@ __global__ void drl_qnet_pack_kernel(QnetPack p) {
         const int64_t frag = e >> 9;                       // m * kt + t
         const int kt = p.kt[l];
         const int m = (int)(frag / kt), t = (int)(frag % kt);
-        const int r = lane & 31, h = lane >> 5;
-        const int row = 32 * m + r;
-        const int k = 16 * t + acc_k(h, j);  // every layer: the act kernel's B-fragment K order
+        const int c = lane & 15, g = lane >> 4;
+        const int row = 16 * m + c;
+        const int k = 32 * t + frag_k(g, j);
         const float w = (row < p.out[l] && k < p.in[l]) ? p.w[l][(int64_t)row * p.in[l] + k] : 0.0f;
         reinterpret_cast<__bf16*>(p.packed_w)[i] = (__bf16)w;
     } else if (i < p.n_wfrag_elems + p.n_bias) {
@@ -72,17 +71,16 @@ __global__ void drl_qnet_pack_kernel(QnetPack p) {
 }
 
 // ------------------------------------------------------------------- act ---
-// One workgroup of QN_WAVES waves per CU: the packed net (97 KB for the C3
-// net) is staged into LDS once per workgroup, and each wave runs 32-env tiles.
-// Input K-slices stream from HBM into a ring of QN_RING register buffers that
-// rolls across tile boundaries: a buffer is re-issued for the slice QN_RING
-// positions ahead as soon as it is consumed, so QN_RING slices (10 KB per
-// wave) are always in flight.  The slice count per tile is padded to a
-// multiple of QN_RING (padding slices are neither loaded nor multiplied), so
-// ring positions are static.
+// One workgroup of QN_WAVES waves per CU: the packed net (99 KB for the C3
+// net) is staged into LDS once per workgroup, and each wave runs 16-env
+// tiles.  Input K-slices stream from HBM into a ring of QN_RING register
+// buffers that rolls across tile boundaries: a buffer is re-issued for the
+// slice QN_RING positions ahead as soon as it is consumed.  The slice count is
+// padded to a multiple of QN_RING (zero weight fragments), so ring positions
+// are static and the loads need no masks or branches.
 constexpr int QN_WAVES = 8;
-constexpr int QN_MAXT = 4;    // 32-unit tiles per hidden layer (hidden <= 128)
-constexpr int QN_RING = 5;    // K-slices in flight per wave (larger rings spill at 4 tiles)
+constexpr int QN_MAXT = 8;    // 16-unit tiles per hidden layer (hidden <= 128)
+constexpr int QN_RING = 5;    // K-slices in flight per wave
 
 __device__ __forceinline__ bf16x8 lds_frag(const uint4* base, int frag, int lane) {
     const uint4 v = base[frag * 64 + lane];
@@ -91,43 +89,29 @@ __device__ __forceinline__ bf16x8 lds_frag(const uint4* base, int frag, int lane
     return f;
 }
 
-// Activation of accumulator tile `acc` (hidden layer, units 32m..) + bias,
-// ReLU, as the two B fragments (K-slices 2m, 2m+1) of the next layer.
-__device__ __forceinline__ void hidden_to_frags(const f32x16& acc, const float* bias, int m, int h, bf16x8& f0,
-                                                bf16x8& f1) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int unit = 32 * m + (i & 3) + 8 * (i >> 2) + 4 * h;
-        const float v = fmaxf(acc[i] + bias[unit], 0.0f);
-        if (i < 8) f0[i] = (__bf16)v;
-        else f1[i - 8] = (__bf16)v;
-    }
-}
-
 template <int NT0>
 __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_kernel(QnetArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint4 wl[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int r = lane & 31, h = lane >> 5;
+    const int c = lane & 15, g = lane >> 4;
     constexpr int nt0 = NT0;  // first-layer tiles (compile time: no branches around its MFMAs)
-    const int64_t ntiles = (a.E + 31) / 32;
+    const int64_t ntiles = (a.E + 15) / 16;
     const int64_t tstride = (int64_t)gridDim.x * QN_WAVES;
-    const int rounds = a.kt0 / QN_RING;  // kt0 is padded to a multiple of QN_RING (zero weight fragments)
-    const int KP = a.kt0;
+    const int KP = a.kt0;                 // padded to a multiple of QN_RING
+    const int rounds = KP / QN_RING;
     float raw[QN_RING][8];
-    // slice t (features 16t + 8h .. +7) of the env row at byte offset `rowb`
-    // from obs, as two 16-B loads (rows are only 8-B aligned at 294 floats:
-    // gfx950 serves 8-B aligned dwordx4 loads, tools/unaligned_probe.hip).  A
-    // quad past in_features reads the row's last quad instead: the packed
-    // weights are zero at those K positions, so it adds nothing; the one quad
-    // that straddles in_features (in_features % 4 == 2) takes its valid pair
-    // from the upper half of the last quad.  No branches: the compiler counts
-    // the outstanding loads exactly.
+    // slice t (features 32t + frag_k(g, 0..7)) of the env row at byte offset
+    // `rowb` from obs: two 16-B loads; the four lanes of the env cover 64
+    // contiguous bytes per load (rows are 8-B aligned at 294 floats: gfx950
+    // serves 8-B aligned dwordx4, tools/unaligned_probe.hip).  A quad past
+    // in_features reads the row's last quad (zero weights there); the quad that
+    // straddles in_features (in_features % 4 == 2) takes its valid pair from
+    // the upper half of that last quad.
     const char* obase = reinterpret_cast<const char*>(a.obs);
     auto load_slice = [&](uint32_t rowb, int t, float (&dst)[8]) {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-            const int ks = 16 * t + 8 * q + 4 * h;  // fragment elements 4q..4q+3 (acc_k order)
+            const int ks = 32 * t + 16 * q + 4 * g;
             const uint32_t off = rowb + 4u * (uint32_t)min(ks, a.in_features - 4);
             float4 v;
             __builtin_memcpy(&v, __builtin_assume_aligned(obase + off, 8), 16);
@@ -139,7 +123,7 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_kernel(QnetArgs a)
         }
     };
     auto row_of = [&](int64_t t) {
-        const int64_t env = t * 32 + r;
+        const int64_t env = t * 16 + c;
         return (uint32_t)((env < a.E ? env : a.E - 1) * a.obs_stride * 4);
     };
     int64_t tile = (int64_t)blockIdx.x * QN_WAVES + wave;
@@ -159,16 +143,13 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_kernel(QnetArgs a)
 
     for (; tile < ntiles; tile += tstride) {
         const int64_t ntile = tile + tstride;
-        const uint32_t nrow = row_of(ntile < ntiles ? ntile : tile);  // past the last tile: harmless re-reads
-        f32x16 acc[QN_MAXT];
+        const uint32_t nrow = row_of(ntile < ntiles ? ntile : tile);
+        f32x4 acc[QN_MAXT];
 #pragma unroll
-        for (int m = 0; m < QN_MAXT; ++m)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) acc[m][i] = 0.0f;
-        // ---- layer 0 over the ring; the last round refills from the next
-        // tile only when this wave has one (uniform branch)
-        // refill mode per round (compile time): 0 = slice t + RING of this tile
-        // (every round but the last), 1 = of the next tile, 2 = none
+        for (int m = 0; m < QN_MAXT; ++m) acc[m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        // ---- layer 0 over the ring.  Refill mode per round (compile time):
+        // 0 = slice t + RING of this tile (all rounds but the last), 1 = of the
+        // next tile, 2 = none (this wave's last tile)
         auto round = [&](int rd, auto mode) {
             constexpr int MODE = decltype(mode)::value;
 #pragma unroll
@@ -180,60 +161,66 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_kernel(QnetArgs a)
                 if constexpr (MODE == 0) load_slice(row, t + QN_RING, raw[i]);
                 else if constexpr (MODE == 1) load_slice(nrow, t + QN_RING - KP, raw[i]);
 #pragma unroll
-                for (int m = 0; m < QN_MAXT; ++m)
-                    if (m < nt0) acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_frag(W0, m * KP + t, lane), b,
-                                                                                   acc[m], 0, 0, 0);
-                // keep each slice's A reads next to its MFMAs (hoisting a whole
-                // round's fragments costs 160 VGPRs and spills)
-                __builtin_amdgcn_sched_barrier(0);
+                for (int m = 0; m < nt0; ++m)
+                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_frag(W0, m * KP + t, lane), b, acc[m], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);  // A reads next to their MFMAs (register pressure)
             }
         };
         for (int rd = 0; rd + 1 < rounds; ++rd) round(rd, std::integral_constant<int, 0>{});
         if (ntile < ntiles) round(rounds - 1, std::integral_constant<int, 1>{});
         else round(rounds - 1, std::integral_constant<int, 2>{});
-        const int64_t env = tile * 32 + r;
+        const int64_t env = tile * 16 + c;
         row = nrow;
         // ---- hidden layers 1..n_hidden-1 and the output layer: B operands in registers
         int nt_prev = nt0;
         const float* bprev = bias + a.bias_off[0];
         for (int l = 1; l <= a.n_hidden; ++l) {
-            bf16x8 bf[2 * QN_MAXT];
+            // activation (bias + ReLU) of the previous layer as bf16 B fragments:
+            // K-slice s = registers of tiles 2s (j < 4) and 2s + 1 (j >= 4)
+            bf16x8 bf[QN_MAXT / 2];
 #pragma unroll
-            for (int m = 0; m < QN_MAXT; ++m)
-                if (m < nt_prev) hidden_to_frags(acc[m], bprev, m, h, bf[2 * m], bf[2 * m + 1]);
-            const int nt_l = (l < a.n_hidden) ? a.nt[l] : 1;  // output layer: one tile (<= 32 actions)
-            const int kt = 2 * nt_prev;
+            for (int s = 0; s < QN_MAXT / 2; ++s) {
+                if (2 * s < nt_prev) {
 #pragma unroll
-            for (int m = 0; m < QN_MAXT; ++m)
+                    for (int j = 0; j < 8; ++j) {
+                        const int m = 2 * s + (j >> 2), i = j & 3;
+                        bf[s][j] = (__bf16)fmaxf(acc[m][i] + bprev[16 * m + 4 * g + i], 0.0f);
+                    }
+                }
+            }
+            const int nt_l = (l < a.n_hidden) ? a.nt[l] : 1;  // output layer: one tile (<= 16 actions)
+            const int kt = nt_prev / 2;
 #pragma unroll
-                for (int i = 0; i < 16; ++i) acc[m][i] = 0.0f;
+            for (int m = 0; m < QN_MAXT; ++m) acc[m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            const uint4* Wl = wl + a.frag_off[l];
 #pragma unroll
-            for (int t = 0; t < 2 * QN_MAXT; ++t) {
+            for (int t = 0; t < QN_MAXT / 2; ++t) {
                 if (t < kt) {
 #pragma unroll
                     for (int m = 0; m < QN_MAXT; ++m)
-                        if (m < nt_l) acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                                             lds_frag(wl + a.frag_off[l], m * kt + t, lane), bf[t], acc[m], 0, 0, 0);
+                        if (m < nt_l)
+                            acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_frag(Wl, m * kt + t, lane), bf[t],
+                                                                            acc[m], 0, 0, 0);
                 }
             }
             nt_prev = nt_l;
             bprev = bias + a.bias_off[l];
         }
-        // ---- Q values: action rows 0..3 in registers 0..3 of the h = 0 lanes,
-        // rows 4..7 in registers 0..3 of the h = 1 lanes (column = env)
+        // ---- Q values: actions 0..3 in registers 0..3 of the g = 0 lanes,
+        // 4..7 in those of the g = 1 lanes (column = env)
         float q[8];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const float own = acc[0][i] + bprev[i + 4 * h];
-            const float other = __shfl(own, lane ^ 32);
-            q[i] = h ? other : own;
-            q[i + 4] = h ? own : other;
+            const float own = acc[0][i] + bprev[4 * g + i];
+            const float hi = __shfl(own, c + 16);  // g = 1 lane of this env
+            q[i] = own;
+            q[i + 4] = hi;
         }
-        if (h == 0 && env < a.E) {
+        if (g == 0 && env < a.E) {
             int best = 0;  // jnp.argmax: first maximum
             for (int i = 1; i < a.n_actions; ++i) best = q[i] > q[best] ? i : best;
-            const uint64_t g = (uint64_t)(a.env_offset + env);
-            const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (g << 8) ^ 0xa5ull));
+            const uint64_t ge = (uint64_t)(a.env_offset + env);
+            const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (ge << 8) ^ 0xa5ull));
             const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
             const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
             a.actions[env * a.action_stride] = (u < a.epsilon) ? rnd : best;
@@ -275,16 +262,16 @@ hipError_t launch_qnet_pack(const QnetPack& p, hipStream_t s) {
 }
 
 hipError_t launch_qnet_act(const QnetArgs& a, int num_cus, hipStream_t s) {
-    const int64_t ntiles = (a.E + 31) / 32;
+    const int64_t ntiles = (a.E + 15) / 16;
     int64_t blocks = (ntiles + QN_WAVES - 1) / QN_WAVES;
     if (blocks > num_cus) blocks = num_cus;
     const dim3 grid((unsigned)blocks), block(64 * QN_WAVES);
     const size_t lds = (size_t)a.lds_vec * 16;
     switch (a.nt[0]) {
-        case 1: hipLaunchKernelGGL(drl_qnet_act_kernel<1>, grid, block, lds, s, a); break;
         case 2: hipLaunchKernelGGL(drl_qnet_act_kernel<2>, grid, block, lds, s, a); break;
-        case 3: hipLaunchKernelGGL(drl_qnet_act_kernel<3>, grid, block, lds, s, a); break;
         case 4: hipLaunchKernelGGL(drl_qnet_act_kernel<4>, grid, block, lds, s, a); break;
+        case 6: hipLaunchKernelGGL(drl_qnet_act_kernel<6>, grid, block, lds, s, a); break;
+        case 8: hipLaunchKernelGGL(drl_qnet_act_kernel<8>, grid, block, lds, s, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -35,13 +35,13 @@ int qnet_layout(const drl_qnet_desc* d, drl::QnetLayout* L) {
     for (int l = 0; l < L->n_layers; ++l) {
         L->in[l] = l == 0 ? d->in_features : d->hidden[l - 1];
         L->out[l] = l < d->n_hidden ? d->hidden[l] : d->n_actions;
-        L->nt[l] = (L->out[l] + 31) / 32;
-        // layer 0: K-slices padded to a multiple of the act kernel's slice ring (5)
-        L->kt[l] = l == 0 ? ((d->in_features + 15) / 16 + 4) / 5 * 5 : 2 * L->nt[l - 1];
+        L->nt[l] = (L->out[l] + 15) / 16;  // 16-row MFMA tiles
+        // 32-wide K-slices; layer 0 padded to a multiple of the act kernel's slice ring (5)
+        L->kt[l] = l == 0 ? ((d->in_features + 31) / 32 + 4) / 5 * 5 : L->in[l] / 32;
         L->frag_off[l] = frag * 64;
         L->bias_off[l] = bias;
         frag += L->nt[l] * L->kt[l];
-        bias += 32 * L->nt[l];
+        bias += 16 * L->nt[l];
     }
     L->frag_total = frag * 64;
     L->n_bias = bias;

@@ -47,8 +47,8 @@ def test_qnet_packed_size_formula():
     L = _bind(lib())
     nb = ctypes.c_int64()
     assert L.drl_qnet_packed_bytes(ctypes.byref(_desc(294, (128, 64))), ctypes.byref(nb)) == 0
-    frags = 4 * 20 + 2 * 8 + 1 * 4          # (tiles x K-slices) per layer, 1 KB each (19 input slices padded to 20)
-    biases = (128 + 64 + 32) * 4
+    frags = 8 * 10 + 4 * 4 + 1 * 2          # (16-row tiles x 32-wide K-slices) per layer, 1 KB each
+    biases = (128 + 64 + 16) * 4
     assert nb.value == frags * 1024 + biases
 
 

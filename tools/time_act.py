@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""Diagnostic: time drl_qnet_act alone (HIP events) for a library variant."""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", default="")
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--hidden", default="128,64")
+    ap.add_argument("--iters", type=int, default=200)
+    args = ap.parse_args()
+    if args.lib:
+        import dronerl_amd._native as nat
+        nat.LIB_PATH = os.path.abspath(args.lib)
+    from dronerl_amd.dqn import QNetwork
+    E = args.envs
+    obs = torch.rand((E, 1, 7, 7, 6), device="cuda")
+    net = QNetwork(294, tuple(int(x) for x in args.hidden.split(",")), generator=torch.Generator().manual_seed(0))
+    a = torch.zeros((E, 8), dtype=torch.int32, device="cuda")
+    flat = obs.reshape(E, -1)
+    for _ in range(20):
+        net.act(flat, 0.1, actions=a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for t in range(args.iters):
+        net.act(flat, 0.1, step=t, actions=a)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / args.iters
+    print(f"{os.path.basename(args.lib) or 'libdronerl.so'} E={E} hidden={args.hidden}: {us:.2f} us/launch, "
+          f"{E * 1176 / us / 1e3:.0f} GB/s obs read")
+
+
+if __name__ == "__main__":
+    main()
