@@ -2,7 +2,7 @@
 
 Mirrors /root/reference torch_impl/env/env.py (``Drone`` :8-15,
 ``DeliveryDrones`` :18-310) and torch_impl/env/wrappers.py
-(``WindowedGridView`` :46-73) so evaluator-style callers
+(``GridView`` :34-43, ``WindowedGridView`` :46-73) so evaluator-style callers
 (drone_evaluator.py:106-162, train_torch.py:41-120) can switch imports:
 
     from dronerl_amd.compat import DeliveryDrones, WindowedGridView
@@ -16,7 +16,7 @@ reproduces the reference bit for bit.  Every step runs on the GPU
 
 Differences (documented, deliberate): env_params is copied, not an alias of the
 class-level DEFAULT_CONFIG (the reference's env.py:54-55 leaks params across
-instances); ``GridView`` is not provided (unused by the reference's drivers).
+instances).
 """
 from __future__ import annotations
 
@@ -185,6 +185,11 @@ class DeliveryDrones:
         o = g.get_obs().cpu().numpy()[0].astype(np.float64)
         return {drone.index: o[drone.index].copy() for drone in self.drones.values()}
 
+    def _grid_obs(self) -> dict:
+        """GridView grids for every drone, {index: float32 [G,G,6]} in dict order."""
+        grid = self._gpu.get_grid().cpu().numpy()[0]
+        return {drone.index: grid.copy() for drone in self.drones.values()}
+
     # ------------------------------------------------------------ helpers --
     def render(self, mode='ansi'):
         return self.__str__()
@@ -257,6 +262,18 @@ class WindowedGridView:
 
     def render(self, mode='ansi'):
         return self.env.render(mode)
+
+
+class GridView(WindowedGridView):
+    """torch_impl GridView (wrappers.py:34-43): every drone sees the whole
+    [side, side, 6] float32 grid (no wall padding)."""
+
+    def __init__(self, env: DeliveryDrones):
+        self.env = env
+        self.observation_space = Box(0, 1, shape=(env.side_size, env.side_size, 6), dtype=float)
+
+    def observation(self, _):
+        return self.env._grid_obs()
 
 
 def set_seed(env, seed):

@@ -286,6 +286,17 @@ int drl_decode(const drl_params* p, const drl_state* s, int32_t* d_order, int32_
     return e == hipSuccess ? 0 : hip_fail(e, "drl_decode launch");
 }
 
+int drl_grid_obs(const drl_params* p, const drl_state* s, float* d_grid, hipStream_t stream) {
+    drl_layout L;
+    if (validate(p, &L) || check_state(s, L)) return -1;
+    if (s->num_envs == 0) return 0;
+    if (!d_grid) return fail("grid is NULL");
+    if ((uintptr_t)d_grid % 8) return fail("grid must be 8-byte aligned");
+    hipError_t e = drl::launch_grid_obs(s->ground, s->drones, s->num_envs, p->side, p->n_drones, L.ground_stride, d_grid,
+                                        stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_grid_obs launch");
+}
+
 int drl_encode(const drl_params* p, const drl_state* s, const int32_t* d_order, const int32_t* d_y, const int32_t* d_x,
                const int32_t* d_charge, const uint8_t* d_carry, hipStream_t stream) {
     drl_layout L;

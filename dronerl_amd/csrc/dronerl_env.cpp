@@ -159,6 +159,13 @@ int drl_env_obs(drl_env* env, int32_t k, float* d_obs, hipStream_t stream) {
     });
 }
 
+int drl_env_grid_obs(drl_env* env, float* d_grid, hipStream_t stream) {
+    return on_device(env, [&]() -> int {
+        if (!env->seeded) return drl_internal_fail("obs before the first reset");
+        return drl_grid_obs(&env->p, &env->s, d_grid, stream);
+    });
+}
+
 int drl_env_get_state(drl_env* env, const drl_state_view* v, hipStream_t stream) {
     return on_device(env, [&]() -> int {
         if (!v) return drl_internal_fail("view is NULL");

@@ -176,6 +176,8 @@ hipError_t launch_step(const StepArgs& a, int P, hipStream_t s, bool obs_only);
 hipError_t launch_reset(const ResetArgs& a, hipStream_t s);
 hipError_t launch_decode(const uint32_t* drones, int64_t E, int N, int32_t* order, int32_t* y, int32_t* x,
                          int32_t* c, uint8_t* k, hipStream_t s);
+hipError_t launch_grid_obs(const uint8_t* ground, const uint32_t* drones, int64_t E, int side, int N, int gstride,
+                           float* out, hipStream_t s);
 hipError_t launch_encode(uint32_t* drones, int64_t E, int N, const int32_t* order, const int32_t* y,
                          const int32_t* x, const int32_t* c, const uint8_t* k, hipStream_t s);
 hipError_t launch_synth(uint64_t seed, uint64_t step, int64_t env_offset, int64_t E, int N, int32_t* out,

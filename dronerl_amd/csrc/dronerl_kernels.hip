@@ -1005,6 +1005,36 @@ __global__ void __launch_bounds__(64) drl_reset_kernel(ResetArgs a) {
     }
 }
 
+// ------------------------------------------------------------ full grid ---
+// GridView observation (wrappers.py:10-31,34-43): the [side][side][6] base grid
+// of every env, the same grid every drone of the env sees.  One 256-thread
+// block per env: drones paint their air byte ((charge+1) | carry<<7) into an
+// LDS image of the cells, then every cell is written as 6 floats (three 8-B
+// stores).  ch4 = charge/100 exactly as the windowed observation computes it.
+__global__ void __launch_bounds__(256) drl_grid_obs_kernel(const uint8_t* __restrict__ ground,
+                                                           const uint32_t* __restrict__ drones, int side, int N,
+                                                           int gstride, float* __restrict__ out) {
+    extern __shared__ uint8_t air[];
+    const int64_t e = blockIdx.x;
+    const int cells = side * side;
+    for (int c = threadIdx.x; c < cells; c += blockDim.x) air[c] = 0;
+    __syncthreads();
+    if ((int)threadIdx.x < N) {
+        const uint32_t r = drones[e * N + threadIdx.x];
+        const int y = r & 255u, x = (r >> 8) & 255u;
+        if (y < side && x < side) air[y * side + x] = (uint8_t)((((r >> 16) & 255u) + 1) | (((r >> 24) & 1u) << 7));
+    }
+    __syncthreads();
+    const uint8_t* g = ground + e * gstride;
+    float2* o = reinterpret_cast<float2*>(out + e * (int64_t)cells * 6);
+    for (int c = threadIdx.x; c < cells; c += blockDim.x) {
+        const uint32_t obj = g[c], a = air[c];
+        o[3 * c] = make_float2(a ? 1.0f : 0.0f, (obj == OBJ_PACKET || (a & 0x80u)) ? 1.0f : 0.0f);
+        o[3 * c + 1] = make_float2(obj == OBJ_DROPZONE ? 1.0f : 0.0f, obj == OBJ_STATION ? 1.0f : 0.0f);
+        o[3 * c + 2] = make_float2(a ? div100((int)(a & 0x7fu) - 1) : 0.0f, obj == OBJ_SKYSCRAPER ? 1.0f : 0.0f);
+    }
+}
+
 // ------------------------------------------------------- decode / encode ---
 __global__ void drl_decode_kernel(const uint32_t* __restrict__ drones, int64_t total, int N, int32_t* order,
                                   int32_t* yv, int32_t* xv, int32_t* cv, uint8_t* kv) {
@@ -1113,6 +1143,13 @@ hipError_t launch_decode(const uint32_t* drones, int64_t E, int N, int32_t* orde
     const int64_t total = E * N;
     hipLaunchKernelGGL(drl_decode_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, drones, total, N,
                        order, y, x, c, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_grid_obs(const uint8_t* ground, const uint32_t* drones, int64_t E, int side, int N, int gstride,
+                           float* out, hipStream_t s) {
+    hipLaunchKernelGGL(drl_grid_obs_kernel, dim3((unsigned)E), dim3(256), (size_t)side * side, s, ground, drones, side,
+                       N, gstride, out);
     return hipGetLastError();
 }
 

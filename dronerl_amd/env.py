@@ -143,6 +143,17 @@ class BatchedDeliveryDrones:
         check(lib().drl_obs(ctypes.byref(self._cp), ctypes.byref(s), k, _ptr(out), _stream(self.device)), "drl_obs")
         return out
 
+    def get_grid(self, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """GridView observation (wrappers.py:34-43): the base grid f32 [E, side, side, 6]
+        that every drone of an env sees."""
+        G = self.params.side
+        if out is None:
+            out = torch.empty((self.num_envs, G, G, 6), dtype=torch.float32, device=self.device)
+        s = self.state.c()
+        check(lib().drl_grid_obs(ctypes.byref(self._cp), ctypes.byref(s), _ptr(out), _stream(self.device)),
+              "drl_grid_obs")
+        return out
+
     def synth_actions(self, seed: int, step: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Uniform synthetic actions (counter hash; identical stream to the oracle's)."""
         if out is None:

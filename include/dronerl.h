@@ -9,6 +9,7 @@
  *   torch_impl/env/env.py:68-101   DeliveryDrones.reset   drl_reset
  *   torch_impl/env/env.py:112-215  DeliveryDrones.step    drl_step
  *   torch_impl/env/wrappers.py:55-73 WindowedGridView     drl_obs (or drl_step's fused obs)
+ *   torch_impl/env/wrappers.py:34-43 GridView             drl_grid_obs
  *   jax_impl/env/env.py:89-135     DeliveryDrones.reset   drl_reset (batched over envs)
  *   jax_impl/env/env.py:137-250    DeliveryDrones.step    drl_step  (batched over envs)
  *   jax_impl/env/env.py:274-309    DeliveryDrones.get_obs drl_obs
@@ -139,6 +140,11 @@ int drl_step(const drl_params* p, const drl_state* s, const int32_t* d_actions, 
  * 0..k-1: f32 [E][k][W][W][6]. */
 int drl_obs(const drl_params* p, const drl_state* s, int32_t k, float* d_obs, hipStream_t stream);
 
+/* GridView observation (wrappers.py:10-31,34-43): the [side][side][6] f32
+ * base grid of every env (each drone of an env sees the same grid):
+ * d_grid f32 [E][side][side][6], channels as drl_obs, no wall padding. */
+int drl_grid_obs(const drl_params* p, const drl_state* s, float* d_grid, hipStream_t stream);
+
 /* Decode drone records to per-index vectors (jax DroneEnvState fields):
  * d_order[E][N] = drone index at dict position; y/x/charge/carry [E][N] by
  * drone index.  Any output may be NULL. */
@@ -202,6 +208,8 @@ int drl_env_step_obs(drl_env* env, const int32_t* d_actions, float* d_rewards, u
                      float* d_obs, hipStream_t stream);
 /* WindowedGridView observation (wrappers.py:55-73): f32 [E][k][W][W][6]. */
 int drl_env_obs(drl_env* env, int32_t k, float* d_obs, hipStream_t stream);
+/* GridView observation (wrappers.py:34-43): f32 [E][side][side][6]. */
+int drl_env_grid_obs(drl_env* env, float* d_grid, hipStream_t stream);
 /* Copy the state out to / in from a caller-owned SoA view (NULL fields are
  * skipped by get_state; set_state needs all of them and trusts their
  * validity: positions on the grid, distinct cells, charge in [0, 100]). */
