@@ -416,9 +416,9 @@ __device__ __forceinline__ int hibit(uint64_t m) { return 63 - __clzll((long lon
 // resident at once (at 6 waves/SIMD a second, tail-heavy generation formed).
 // Wider groups are LDS-limited below 8 waves/SIMD: no cap (it only spilled).
 // Global addressing: 64-bit wave bases (scalar) + 32-bit lane offsets.
+// One batch (the wave's GPW envs starting at wenv0) of the step.
 template <int P, class GEO>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : 1, 8)))
-drl_step_kernel(StepArgs a) {
+__device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     using GMask = typename GMaskT<P>::type;
     constexpr int GPW = 64 / P;
     constexpr int D = step_draws(P);             // draws per lane per respawn round
@@ -431,7 +431,6 @@ drl_step_kernel(StepArgs a) {
     const int lane = threadIdx.x & 63;
     const int grp = lane / P;
     const int j = lane % P;
-    const int64_t wenv0 = (int64_t)blockIdx.x * GPW;
     const int nenv_w = (int)min((int64_t)GPW, a.E - wenv0);
     if (nenv_w <= 0) return;
     const bool env_ok = grp < nenv_w;
@@ -772,16 +771,13 @@ drl_step_kernel(StepArgs a) {
         const uint32_t nc = W.cnt[grp * 4];
         const uint16_t* ch = W.chg + grp * nchg;
         uint8_t* gdst = ground_w + (uint32_t)(grp * gstride);
-        // (usually one trip: keep these loops rolled, unrolled/vectorized
-        // copies of them cost registers the whole kernel pays for)
-        if (nc <= (uint32_t)nchg) {
+        // Changes per step <= 4N (N pickups/deliveries, 2N respawned packets and
+        // dropzones, N pick-after-respawn) < the list's 6N + 2 entries, so the
+        // list never overflows (chg_push drops past capacity regardless).  The
+        // loop usually runs once: keep it rolled, unrolled/vectorised copies
+        // cost registers the whole kernel pays for.
 #pragma clang loop unroll(disable) vectorize(disable)
-            for (uint32_t q = j; q < nc; q += P) gdst[ch[q]] = gl[ch[q]];
-        } else {  // cannot happen (<= 6N changes per step); whole-row fallback
-#pragma clang loop unroll(disable) vectorize(disable)
-            for (int v = j; v < gstride / 16; v += P)
-                reinterpret_cast<uint4*>(gdst)[v] = reinterpret_cast<const uint4*>(gl)[v];
-        }
+        for (uint32_t q = j; q < min(nc, (uint32_t)nchg); q += P) gdst[ch[q]] = gl[ch[q]];
     }
     DRL_STAMP(5);
     if (GEO::kObs && a.obs) {
@@ -791,6 +787,15 @@ drl_step_kernel(StepArgs a) {
         write_obs_wave(a.obs + wenv0 * (int64_t)(6u * g.env_cells()), nenv_w, g, W, a.obs_wide, lane);
     }
     DRL_STAMP(6);
+}
+
+// One wave per batch of GPW envs.  (Persistent waves looping over 2-4 batches
+// were measured slower at C3/C4/C5: halving the resident waves costs more
+// latency hiding than the longer waves gain in balance.)
+template <int P, class GEO>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : 1, 8)))
+drl_step_kernel(StepArgs a) {
+    step_batch<P, GEO>(a, (int64_t)blockIdx.x * (64 / P));
 }
 
 // ------------------------------------------------------------ observation ---
