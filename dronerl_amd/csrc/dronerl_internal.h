@@ -102,6 +102,7 @@ struct ResetArgs {
     uint64_t seed_base;
     const uint8_t* mask;
     int lanes, lane_lds, list_cap, block_lds, pool_branch;
+    int wave_per_env, wave_lds;  // drl_reset_wave_kernel (large grids) and its LDS bytes
     FastDiv div_side;
 };
 

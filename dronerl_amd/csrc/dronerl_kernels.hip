@@ -77,19 +77,13 @@ __device__ __forceinline__ uint32_t pack_drone(int y, int x, int c, int carry, i
            ((uint32_t)idx << 25);
 }
 
-// In-place MT19937 twist of one env's state by all 64 lanes of the wave,
-// register-resident: lane l holds x[c] = mt[64c + l].  Chunks are processed in
+// MT19937 twist of one env's state held by all 64 lanes of the wave in
+// registers: lane l holds x[c] = mt[64c + l].  Chunks are processed in
 // ascending order, each computed from old/new values exactly as the sequential
 // generator sees them: mt[i+1] and mt[i+397] (i < 227) are still old (chunks
 // > c), mt[i-227] (i >= 227) and mt[0] (i = 623) are already new (chunks < c).
 // Lane offsets are constants (397 = 6*64 + 13, 227 = 4*64 - 29).
-__device__ __noinline__ void twist_wave(uint32_t* row, int lane) {
-    uint32_t x[10];
-#pragma unroll
-    for (int c = 0; c < 10; ++c) {
-        const int i = 64 * c + lane;
-        x[c] = (i < MT_N) ? load_l2(row + i) : 0u;
-    }
+__device__ __forceinline__ void twist_regs(uint32_t (&x)[10], int lane) {
 #pragma unroll
     for (int c = 0; c < 10; ++c) {
         const int i = 64 * c + lane;
@@ -110,6 +104,17 @@ __device__ __noinline__ void twist_wave(uint32_t* row, int lane) {
         const uint32_t y = (x[c] & 0x80000000u) | (nxt & 0x7fffffffu);
         x[c] = far ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
     }
+}
+
+// In-place twist of the env row in global memory (register-resident).
+__device__ __noinline__ void twist_wave(uint32_t* row, int lane) {
+    uint32_t x[10];
+#pragma unroll
+    for (int c = 0; c < 10; ++c) {
+        const int i = 64 * c + lane;
+        x[c] = (i < MT_N) ? load_l2(row + i) : 0u;
+    }
+    twist_regs(x, lane);
 #pragma unroll
     for (int c = 0; c < 10; ++c) {
         const int i = 64 * c + lane;
@@ -1010,6 +1015,160 @@ __global__ void __launch_bounds__(64) drl_reset_kernel(ResetArgs a) {
     }
 }
 
+// ------------------------------------------------------- reset (wave/env) ---
+// One wavefront per env, for large grids (the lane-per-env kernel above is
+// LDS-bound to a few envs per CU there, and each of its ~22k serial draws at
+// 64x64 is a memory round trip).  The env's MT state stays in registers
+// (lane l holds words 64c + l) and twists in registers; a draw is a readlane
+// of the current tempered 64-word chunk, so the shuffle chain is uniform
+// scalar control flow plus single-lane LDS swaps.  Same draws, same order,
+// same results as the lane kernel (and the reference).
+__global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x;
+    const int64_t env = blockIdx.x;
+    if (env >= a.E || (a.mask != nullptr && a.mask[env] == 0)) return;  // whole wave, uniform
+    uint16_t* list = reinterpret_cast<uint16_t*>(smem);
+    uint16_t* sel = list + a.list_cap;
+    uint16_t* pool = sel + 64;
+    const int GG = a.cells, N = a.n_drones;
+    uint32_t* mrow = a.mt + env * MT_WORDS;
+    uint8_t* grow = a.ground + env * a.gstride;
+
+    if (a.reseed) {
+        if (lane == 0) mt_seed_row(mrow, a.seed_base + (uint64_t)env);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        wave_sync();
+    }
+    uint32_t x[10];
+#pragma unroll
+    for (int c = 0; c < 10; ++c) x[c] = (64 * c + lane < MT_N) ? load_l2(mrow + 64 * c + lane) : 0u;
+    for (int v = lane; v < a.gstride / 16; v += 64) reinterpret_cast<uint4*>(grow)[v] = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = lane; i < GG; i += 64) list[i] = (uint16_t)i;
+    int midx = a.reseed ? MT_N : (int)a.mt_index[env];
+    int chunk = -1;
+    uint32_t tcur = 0;
+    wave_sync();
+
+    // The reset as a phase machine with ONE draw site (the register twist is
+    // inlined once): 0 shuffle for the skyscrapers, 1 sample the drones, 2-4
+    // shuffles for packets / dropzones / stations (env.py:68-101, random.py
+    // shuffle :380-395 and sample :480-504).
+    const int kb = bitlen((uint32_t)(GG - a.n_sky));  // sample's set branch: randbelow(n) bits
+    int n = GG, phase = 0, si = GG - 1;
+    uint32_t mine = 0xffffffffu;  // set branch: lane q < N holds selection q
+    auto place = [&](int count, uint8_t code) __attribute__((always_inline)) {  // pop `count` from the end
+        wave_sync();
+        for (int t = lane; t < count; t += 64) grow[list[n - 1 - t]] = code;
+        n -= count;
+    };
+    // finish phases that need no (more) draws; set up the next one
+    auto settle = [&]() __attribute__((always_inline)) {
+        for (;;) {
+            if (phase == 0 && si < 1) {
+                place(a.n_sky, OBJ_SKYSCRAPER);
+                phase = 1;
+                si = 0;
+                if (a.pool_branch) {
+                    for (int i = lane; i < n; i += 64) pool[i] = list[i];
+                    wave_sync();
+                }
+            } else if (phase == 1 && si >= N) {
+                if (!a.pool_branch && lane < N) sel[lane] = list[mine];
+                wave_sync();
+                phase = 2;
+                si = n - 1;
+            } else if (phase >= 2 && phase <= 4 && si < 1) {
+                place(phase == 2 ? a.n_pack : phase == 3 ? a.n_drop : a.n_stat,
+                      phase == 2 ? OBJ_PACKET : phase == 3 ? OBJ_DROPZONE : OBJ_STATION);
+                ++phase;
+                si = n - 1;
+            } else {
+                return;
+            }
+        }
+    };
+    settle();
+    while (phase <= 4) {
+        // ---- the current 64-word chunk of the env's stream (twist first when
+        // it is used up): the single twist site
+        if (midx >= MT_N) {
+            twist_regs(x, lane);
+            midx = 0;
+            chunk = -1;
+        }
+        const int c = midx >> 6;
+        if (c != chunk) {
+            uint32_t v = x[0];
+#pragma unroll
+            for (int q = 1; q < 10; ++q) v = (c == q) ? x[q] : v;
+            tcur = temper(v);
+            chunk = c;
+        }
+        const int end = min(64 * c + 64, MT_N);
+        // ---- consume the chunk's draws for the current phase (tight loops;
+        // si / midx stay uniform; readlane returns int: shift it as uint32)
+        if (phase != 1) {  // Fisher-Yates steps of a shuffle; lane 0 swaps
+            int kb_s = bitlen((uint32_t)si + 1u);
+            while (midx < end && si >= 1) {
+                const uint32_t rr = (uint32_t)__builtin_amdgcn_readlane(tcur, midx & 63) >> (32 - kb_s);
+                ++midx;
+                if ((int)rr <= si) {
+                    const uint16_t vi = list[si], vr = list[rr];  // broadcast reads
+                    if (lane == 0) {
+                        list[si] = vr;
+                        list[rr] = vi;
+                    }
+                    --si;
+                    kb_s = bitlen((uint32_t)si + 1u);
+                }
+            }
+        } else if (a.pool_branch) {
+            while (midx < end && si < N) {
+                const uint32_t m = (uint32_t)(n - si);
+                const uint32_t rr = (uint32_t)__builtin_amdgcn_readlane(tcur, midx & 63) >> (32 - bitlen(m));
+                ++midx;
+                if (rr < m) {
+                    const uint16_t pr = pool[rr], pl = pool[m - 1u];
+                    if (lane == 0) {
+                        sel[si] = pr;
+                        pool[rr] = pl;
+                    }
+                    ++si;
+                }
+            }
+        } else {
+            while (midx < end && si < N) {
+                const uint32_t rr = (uint32_t)__builtin_amdgcn_readlane(tcur, midx & 63) >> (32 - kb);
+                ++midx;
+                if ((int)rr < n && !__ballot(lane < si && mine == rr)) {
+                    if (lane == si) mine = rr;
+                    ++si;
+                }
+            }
+        }
+        settle();
+    }
+    wave_sync();
+
+    // drones in index order (dict order 0..N-1), then _pick_packets_after_respawn
+    // (distinct cells: parallel)
+    if (lane < N) {
+        const int cell = sel[lane];
+        int carry = 0;
+        if (grow[cell] == OBJ_PACKET) {
+            carry = 1;
+            grow[cell] = OBJ_EMPTY;
+        }
+        const uint32_t py = fdiv((uint32_t)cell, a.div_side);
+        a.drones[env * N + lane] = pack_drone((int)py, cell - (int)py * a.side, 100, carry, lane);
+    }
+#pragma unroll
+    for (int c = 0; c < 10; ++c)
+        if (64 * c + lane < MT_N) mrow[64 * c + lane] = x[c];
+    if (lane == 0) a.mt_index[env] = (uint32_t)midx;
+}
+
 // ------------------------------------------------------------ full grid ---
 // GridView observation (wrappers.py:10-31,34-43): the [side][side][6] base grid
 // of every env, the same grid every drone of the env sees.  One 256-thread
@@ -1138,8 +1297,12 @@ extern "C" int drl_debug_set_stamps(void* p) {
 #endif
 
 hipError_t launch_reset(const ResetArgs& a, hipStream_t s) {
-    const int64_t blocks = (a.E + a.lanes - 1) / a.lanes;
-    hipLaunchKernelGGL(drl_reset_kernel, dim3((unsigned)blocks), dim3(64), a.block_lds, s, a);
+    if (a.wave_per_env) {
+        hipLaunchKernelGGL(drl_reset_wave_kernel, dim3((unsigned)a.E), dim3(64), a.wave_lds, s, a);
+    } else {
+        const int64_t blocks = (a.E + a.lanes - 1) / a.lanes;
+        hipLaunchKernelGGL(drl_reset_kernel, dim3((unsigned)blocks), dim3(64), a.block_lds, s, a);
+    }
     return hipGetLastError();
 }
 
