@@ -39,6 +39,8 @@ constexpr int paint_bytes(int k, int w) { return k > 0 ? r16(k * w * w) : 0; }  
 constexpr int nchg(int n_drones) { return 6 * n_drones + 2; }                  // changed-cell capacity
 constexpr int chg_bytes(int n_drones) { return r16(2 * nchg(n_drones)); }
 constexpr int bit_length(int v) { return v ? 1 + bit_length(v >> 1) : 0; }
+constexpr int fy_buckets = 256;                                   // reset: j-hash buckets (x2 hashes)
+constexpr int fy_table_bytes = (2 * fy_buckets + 64) * 4;        // ... + the 64 i slots, u32 each
 }  // namespace lay
 
 enum : int { OBJ_EMPTY = 0, OBJ_SKYSCRAPER = 2, OBJ_STATION = 3, OBJ_DROPZONE = 4, OBJ_PACKET = 5 };
@@ -103,6 +105,7 @@ struct ResetArgs {
     const uint8_t* mask;
     int lanes, lane_lds, list_cap, block_lds, pool_branch;
     int wave_per_env, wave_lds;  // drl_reset_wave_kernel (large grids) and its LDS bytes
+    int fy_batch_min;            // wave kernel: shuffle 64 draws at a time while si >= this
     FastDiv div_side;
 };
 

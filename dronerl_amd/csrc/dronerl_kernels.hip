@@ -87,12 +87,13 @@ __device__ __forceinline__ void twist_regs(uint32_t (&x)[10], int lane) {
 #pragma unroll
     for (int c = 0; c < 10; ++c) {
         const int i = 64 * c + lane;
-        uint32_t nxt = __shfl(x[c], (lane + 1) & 63);
+        // mt[i+1]: DPP wave_shl:1 (lane l reads lane l+1); lane 63 takes lane 0 of the next chunk
+        uint32_t nxt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x[c], 0x130, 0xf, 0xf, false);
         if (c < 9) {
-            const uint32_t n0 = __shfl(x[c + 1], 0);
+            const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)x[c + 1], 0);
             if (lane == 63) nxt = n0;
         } else {
-            const uint32_t m0 = __shfl(x[0], 0);  // new mt[0]
+            const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)x[0], 0);  // new mt[0]
             if (i == MT_N - 1) nxt = m0;
         }
         const int l13 = lane + 13, l29 = lane + 29;
@@ -1016,6 +1017,104 @@ __global__ void __launch_bounds__(64) drl_reset_kernel(ResetArgs a) {
 }
 
 // ------------------------------------------------------- reset (wave/env) ---
+constexpr int kFyBuckets = lay::fy_buckets;
+
+__device__ __forceinline__ int mbcnt64(uint64_t m) {  // set bits of m below this lane
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Up to 64 consecutive Fisher-Yates steps of Random.shuffle (random.py:380-395)
+// at once: lane l holds the stream's draw 64c + l (u, tempered), lanes
+// [l0, l1) are unconsumed.  Returns the first lane NOT consumed; si and the
+// list advance exactly as the one-draw-at-a-time loop would leave them.
+//  1. acceptance: draw k is consumed iff fewer than si0 draws before it were
+//     accepted, and accepted iff r_k = u_k >> (32 - bitlen(s_k + 1)) <= s_k
+//     with s_k = si0 - (#accepted before k).  Membership of k depends only on
+//     lanes below k, so iterating the ballot from any start reaches the
+//     sequential answer, lanes settling left to right (usually 2-3 rounds).
+//  2. accepted draw t (rank t among them) swaps i_t = si0 - t with j_t = r_t.
+//     With A_t / B_t the values at i_t / j_t just before step t: i_t ends as
+//     B_t (later steps only touch smaller positions); A_t = A_p, p = the last
+//     earlier step whose j was i_t (else the original list[i_t]); B_t = A_q,
+//     q = the last earlier step with the same j (else the original list[j_t]);
+//     each j position ends as A of its last writer.  p comes from a 64-slot
+//     table over the i range (max writer lane, tagged with the batch epoch).
+//     For q, two 256-bucket tables keep the max writer lane per bucket of two
+//     hashes of j: a lane that is the max of either bucket has no later lane
+//     with its j (it is the last writer); the others -- every lane with a
+//     later duplicate, plus rare double hash collisions -- are the sources of
+//     an exact readlane loop that sets q for the later lanes with the same j.
+__device__ __forceinline__ int fy_chunk(uint16_t* list, uint32_t* htab, uint32_t* ptab, uint32_t u, int lane, int l0,
+                                        int l1, int& si, int epoch, bool count_only) {
+    const int si0 = si;
+    const bool valid = lane >= l0 && lane < l1;
+    uint64_t S = __ballot(valid);
+    for (;;) {
+        const int tk = mbcnt64(S), sk = si0 - tk;
+        const uint32_t rk = u >> (32 - bitlen((uint32_t)max(sk, 1) + 1u));
+        const uint64_t S2 = __ballot(valid && sk >= 1 && (int)rk <= sk);
+        if (S2 == S) break;
+        S = S2;
+    }
+    const int m = popc(S);
+    si = si0 - m;
+    const int consumed = si == 0 ? hibit(S) + 1 : l1;
+    if (m == 0 || count_only) return consumed;
+    const bool acc = (S >> lane) & 1ull;
+    const int t = mbcnt64(S), s = si0 - t;
+    const uint32_t r = u >> (32 - bitlen((uint32_t)max(s, 1) + 1u));
+    const uint32_t tag = (uint32_t)epoch << 7, me = tag | (uint32_t)(lane + 1);
+    const int j = (int)r, ii = si0 - t, slot = si0 - j;  // slot: j's rank if j lies in the i range
+    const int h1 = j & (kFyBuckets - 1), h2 = kFyBuckets + (int)(((uint32_t)j * 0x9e3779b1u) >> 24);
+    uint32_t a0 = 0, l0j = 0, hv1 = 0, hv2 = 0, pv = 0;
+    if (acc) {
+        a0 = list[ii];
+        l0j = list[j];
+        atomicMax(&htab[h1], me);
+        atomicMax(&htab[h2], me);
+        if (slot < m && slot != t) atomicMax(&ptab[slot], me);
+    }
+    wave_sync();
+    if (acc) {
+        hv1 = htab[h1];
+        hv2 = htab[h2];
+        pv = ptab[t];
+    }
+    const int p = (acc && (pv >> 7) == (uint32_t)epoch) ? (int)(pv & 127u) - 1 : -1;  // writer lane
+    uint32_t A = a0;
+    if (__ballot(p >= 0)) {  // chains of p: jump to the root, whose A is its original list[i]
+        int f = p >= 0 ? p : lane;
+        for (;;) {
+            const int f2 = __shfl(f, f);
+            if (!__ballot(f2 != f)) break;
+            f = f2;
+        }
+        A = __shfl(a0, f);
+    }
+    int q = -1;
+    uint64_t notlast = 0;
+    uint64_t src = __ballot(acc && hv1 != me && hv2 != me);
+    while (src) {  // ascending: q ends as the last earlier lane with the same j
+        const int k = lobit(src);
+        src &= src - 1;
+        const int jk = __builtin_amdgcn_readlane(j, k);
+        const uint64_t later = __ballot(j == jk) & S & (~1ull << k);
+        if (later) {
+            notlast |= 1ull << k;
+            if ((later >> lane) & 1ull) q = k;
+        }
+    }
+    uint32_t B = l0j;
+    if (__ballot(q >= 0)) {
+        const uint32_t Aq = __shfl(A, q >= 0 ? q : lane);
+        if (q >= 0) B = Aq;
+    }
+    if (acc && !((notlast >> lane) & 1ull)) list[j] = (uint16_t)A;  // j positions (i-range ones are rewritten next)
+    if (acc) list[ii] = (uint16_t)B;
+    wave_sync();
+    return consumed;
+}
+
 // One wavefront per env, for large grids (the lane-per-env kernel above is
 // LDS-bound to a few envs per CU there, and each of its ~22k serial draws at
 // 64x64 is a memory round trip).  The env's MT state stays in registers
@@ -1028,26 +1127,40 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
     const int lane = threadIdx.x;
     const int64_t env = blockIdx.x;
     if (env >= a.E || (a.mask != nullptr && a.mask[env] == 0)) return;  // whole wave, uniform
-    uint16_t* list = reinterpret_cast<uint16_t*>(smem);
+    uint32_t* htab = reinterpret_cast<uint32_t*>(smem);  // batched shuffle: last writer per j bucket (2 hashes)
+    uint32_t* ptab = htab + 2 * kFyBuckets;               // ... and per i slot
+    uint16_t* list = reinterpret_cast<uint16_t*>(ptab + 64);
     uint16_t* sel = list + a.list_cap;
     uint16_t* pool = sel + 64;
     const int GG = a.cells, N = a.n_drones;
     uint32_t* mrow = a.mt + env * MT_WORDS;
     uint8_t* grow = a.ground + env * a.gstride;
+    for (int i = lane; i < 2 * kFyBuckets + 64; i += 64) htab[i] = 0u;
 
     if (a.reseed) {
         if (lane == 0) mt_seed_row(mrow, a.seed_base + (uint64_t)env);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         wave_sync();
     }
+    // x[k] holds words 64 * ((k + rot) % 10) + lane: the current chunk is
+    // always x[0] (moving to the next chunk rotates the array by one register)
+    int midx = a.reseed ? MT_N : (int)a.mt_index[env];
+    int rot = midx < MT_N ? midx >> 6 : 0;
     uint32_t x[10];
 #pragma unroll
-    for (int c = 0; c < 10; ++c) x[c] = (64 * c + lane < MT_N) ? load_l2(mrow + 64 * c + lane) : 0u;
+    for (int k = 0; k < 10; ++k) {
+        const int c = k + rot < 10 ? k + rot : k + rot - 10;
+        x[k] = (64 * c + lane < MT_N) ? load_l2(mrow + 64 * c + lane) : 0u;
+    }
     for (int v = lane; v < a.gstride / 16; v += 64) reinterpret_cast<uint4*>(grow)[v] = make_uint4(0u, 0u, 0u, 0u);
     for (int i = lane; i < GG; i += 64) list[i] = (uint16_t)i;
-    int midx = a.reseed ? MT_N : (int)a.mt_index[env];
-    int chunk = -1;
-    uint32_t tcur = 0;
+    uint32_t tcur = temper(x[0]);
+    auto rotate = [&]() __attribute__((always_inline)) {
+        const uint32_t x0 = x[0];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) x[k] = x[k + 1];
+        x[9] = x0;
+    };
     wave_sync();
 
     // The reset as a phase machine with ONE draw site (the register twist is
@@ -1055,7 +1168,7 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
     // shuffles for packets / dropzones / stations (env.py:68-101, random.py
     // shuffle :380-395 and sample :480-504).
     const int kb = bitlen((uint32_t)(GG - a.n_sky));  // sample's set branch: randbelow(n) bits
-    int n = GG, phase = 0, si = GG - 1;
+    int n = GG, phase = 0, si = GG - 1, epoch = 0;
     uint32_t mine = 0xffffffffu;  // set branch: lane q < N holds selection q
     auto place = [&](int count, uint8_t code) __attribute__((always_inline)) {  // pop `count` from the end
         wave_sync();
@@ -1093,22 +1206,29 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
         // ---- the current 64-word chunk of the env's stream (twist first when
         // it is used up): the single twist site
         if (midx >= MT_N) {
+            if (rot)
+                for (; rot < 10; ++rot) rotate();  // back to canonical order (rot is 9 here)
             twist_regs(x, lane);
             midx = 0;
-            chunk = -1;
+            rot = 0;
+            tcur = temper(x[0]);
+        } else if ((midx >> 6) != rot) {  // next chunk
+            rotate();
+            ++rot;
+            tcur = temper(x[0]);
         }
-        const int c = midx >> 6;
-        if (c != chunk) {
-            uint32_t v = x[0];
-#pragma unroll
-            for (int q = 1; q < 10; ++q) v = (c == q) ? x[q] : v;
-            tcur = temper(v);
-            chunk = c;
-        }
+        const int c = rot;
         const int end = min(64 * c + 64, MT_N);
         // ---- consume the chunk's draws for the current phase (tight loops;
         // si / midx stay uniform; readlane returns int: shift it as uint32)
-        if (phase != 1) {  // Fisher-Yates steps of a shuffle; lane 0 swaps
+        if (phase != 1 && si >= a.fy_batch_min) {
+            // the last shuffle only needs its top n_stat positions: below them
+            // the draws are consumed without swapping
+            const bool count_only = phase == 4 && si < n - a.n_stat;
+            midx = 64 * c + fy_chunk(list, htab, ptab, tcur, lane, midx - 64 * c, end - 64 * c, si, ++epoch,
+                                     count_only);
+            if (si != 0) continue;  // the shuffle goes on: nothing to settle
+        } else if (phase != 1) {  // Fisher-Yates steps of a shuffle, one draw at a time; lane 0 swaps
             int kb_s = bitlen((uint32_t)si + 1u);
             while (midx < end && si >= 1) {
                 const uint32_t rr = (uint32_t)__builtin_amdgcn_readlane(tcur, midx & 63) >> (32 - kb_s);
@@ -1164,8 +1284,10 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
         a.drones[env * N + lane] = pack_drone((int)py, cell - (int)py * a.side, 100, carry, lane);
     }
 #pragma unroll
-    for (int c = 0; c < 10; ++c)
-        if (64 * c + lane < MT_N) mrow[64 * c + lane] = x[c];
+    for (int k = 0; k < 10; ++k) {
+        const int c = k + rot < 10 ? k + rot : k + rot - 10;
+        if (64 * c + lane < MT_N) mrow[64 * c + lane] = x[k];
+    }
     if (lane == 0) a.mt_index[env] = (uint32_t)midx;
 }
 

@@ -148,15 +148,32 @@ CONFIGS = {
 }
 
 
+RESET_KERNELS = {
+    "wave": {},                                                  # default: wave per env, batched shuffle
+    "wave_serial": {"DRL_FY_BATCH_MIN": "1000000"},              # wave per env, one draw at a time
+    "wave_fy64": {"DRL_FY_BATCH_MIN": "64"},                     # batched only while si >= 64
+    "lane": {"DRL_RESET_WAVE": "0"},                             # lane per env
+}
+
+
+@pytest.mark.parametrize("kernel", list(RESET_KERNELS))
 @pytest.mark.parametrize("name", list(CONFIGS))
-def test_reset_matches_oracle(name):
+def test_reset_matches_oracle(name, kernel, monkeypatch):
+    """Reseeded reset, then two resets continuing the stream (the second one
+    starts mid-way through an MT block), on every reset kernel variant."""
+    for k, v in RESET_KERNELS[kernel].items():
+        monkeypatch.setenv(k, v)
     p = EnvParams(**CONFIGS[name])
-    E = 300
+    E = 300 if kernel == "wave" else 97
     env = Env(p, E)
     env.reset(seed=1000)
     o = OracleMulti(oparams(p), E)
     o.reset(1000 + np.arange(E))
     assert_state(gpu_state(env), o.state(), f"{name} reset")
+    for r in range(2):
+        env.reset(seed=None)
+        o.reset(None)
+        assert_state(gpu_state(env), o.state(), f"{name} reset {r + 2}")
 
 
 @pytest.mark.parametrize("name,E,steps,every", [
@@ -254,7 +271,10 @@ def test_shard_invariance():
         assert torch.equal(getattr(full.state, k), torch.cat([getattr(h.state, k) for h in halves]))
 
 
-def test_masked_reset_continues_stream():
+@pytest.mark.parametrize("kernel", ["wave", "lane"])
+def test_masked_reset_continues_stream(kernel, monkeypatch):
+    for k, v in RESET_KERNELS[kernel].items():
+        monkeypatch.setenv(k, v)
     p = EnvParams(n_drones=8, grid_size=16)
     E = 200
     env = Env(p, E)
