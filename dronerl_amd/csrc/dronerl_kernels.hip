@@ -893,6 +893,52 @@ __device__ void mt_seed_row(uint32_t* row, uint64_t seed) {
     row[0] = 0x80000000u;
 }
 
+// random.seed(seed) for a whole wave's register copy of the row (x[c] lane l
+// = mt[64c + l], as twist_regs): the same init_by_array passes as mt_seed_row,
+// run as a scalar chain -- each step reads its word with readlane, mixes it in
+// SGPRs and writes it back into its lane (no memory round trips).
+__device__ __forceinline__ void mt_seed_regs(uint32_t (&x)[10], uint64_t seed, int lane) {
+#pragma unroll
+    for (int c = 0; c < 10; ++c) x[c] = (64 * c + lane < MT_N) ? kMtInit.v[64 * c + lane] : 0u;
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    const uint32_t two = k1 ? 1u : 0u;  // key length 2: key words alternate, j = 0, 1, 0, ...
+    uint32_t prev = kMtInit.v[0], jj = 0;
+    auto rd = [](uint32_t v, int l) __attribute__((always_inline)) {
+        return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+    };
+    auto wr = [lane](uint32_t v, int l, uint32_t old) __attribute__((always_inline)) { return lane == l ? v : old; };
+    // pass 1 (random.c init_by_array: k = max(N, keylen) steps): i = 1..623 ...
+#pragma unroll
+    for (int c = 0; c < 10; ++c) {
+        const int lend = c == 9 ? MT_N - 576 : 64;
+        for (int l = c == 0 ? 1 : 0; l < lend; ++l) {
+            const uint32_t v = (rd(x[c], l) ^ ((prev ^ (prev >> 30)) * 1664525u)) + (jj ? k1 + 1u : k0);
+            x[c] = wr(v, l, x[c]);
+            prev = v;
+            jj ^= two;
+        }
+    }
+    prev = rd(x[9], MT_N - 577);  // ... mt[0] = mt[623], then i = 1 once more
+    x[0] = wr(prev, 0, x[0]);
+    prev = (rd(x[0], 1) ^ ((prev ^ (prev >> 30)) * 1664525u)) + (jj ? k1 + 1u : k0);
+    x[0] = wr(prev, 1, x[0]);
+    // pass 2 (N - 1 steps): i = 2..623, mt[0] = mt[623], i = 1
+#pragma unroll
+    for (int c = 0; c < 10; ++c) {
+        const int lend = c == 9 ? MT_N - 576 : 64;
+        for (int l = c == 0 ? 2 : 0; l < lend; ++l) {
+            const uint32_t v = (rd(x[c], l) ^ ((prev ^ (prev >> 30)) * 1566083941u)) - (uint32_t)(64 * c + l);
+            x[c] = wr(v, l, x[c]);
+            prev = v;
+        }
+    }
+    prev = rd(x[9], MT_N - 577);
+    x[0] = wr(prev, 0, x[0]);
+    prev = (rd(x[0], 1) ^ ((prev ^ (prev >> 30)) * 1566083941u)) - 1u;
+    x[0] = wr(prev, 1, x[0]);
+    x[0] = wr(0x80000000u, 0, x[0]);  // mt[0] = 0x80000000
+}
+
 __global__ void __launch_bounds__(64) drl_reset_kernel(ResetArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
@@ -1137,20 +1183,19 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
     uint8_t* grow = a.ground + env * a.gstride;
     for (int i = lane; i < 2 * kFyBuckets + 64; i += 64) htab[i] = 0u;
 
-    if (a.reseed) {
-        if (lane == 0) mt_seed_row(mrow, a.seed_base + (uint64_t)env);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        wave_sync();
-    }
     // x[k] holds words 64 * ((k + rot) % 10) + lane: the current chunk is
     // always x[0] (moving to the next chunk rotates the array by one register)
     int midx = a.reseed ? MT_N : (int)a.mt_index[env];
     int rot = midx < MT_N ? midx >> 6 : 0;
     uint32_t x[10];
+    if (a.reseed) {
+        mt_seed_regs(x, a.seed_base + (uint64_t)env, lane);
+    } else {
 #pragma unroll
-    for (int k = 0; k < 10; ++k) {
-        const int c = k + rot < 10 ? k + rot : k + rot - 10;
-        x[k] = (64 * c + lane < MT_N) ? load_l2(mrow + 64 * c + lane) : 0u;
+        for (int k = 0; k < 10; ++k) {
+            const int c = k + rot < 10 ? k + rot : k + rot - 10;
+            x[k] = (64 * c + lane < MT_N) ? load_l2(mrow + 64 * c + lane) : 0u;
+        }
     }
     for (int v = lane; v < a.gstride / 16; v += 64) reinterpret_cast<uint4*>(grow)[v] = make_uint4(0u, 0u, 0u, 0u);
     for (int i = lane; i < GG; i += 64) list[i] = (uint16_t)i;

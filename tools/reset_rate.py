@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--envs", type=int, default=0, help="override num_envs")
+    ap.add_argument("--reseed", action="store_true", help="also time reset(seed=...) (random.seed per env)")
     args = ap.parse_args()
     variants = args.variants.split(",")
     for cfg in args.configs.split(","):
@@ -59,6 +60,7 @@ def main():
         env.reset(seed=0)
         seeded = env.state.clone()
         rates = {v: [] for v in variants}
+        reseed = {v: [] for v in variants}
         states = {}
         for _ in range(args.rounds):
             for v in variants:
@@ -74,12 +76,23 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 rates[v].append(E * args.reps / (e0.elapsed_time(e1) / 1e3))
+                if args.reseed:
+                    e0.record()
+                    env.reset(seed=12345)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    reseed[v].append(E / (e0.elapsed_time(e1) / 1e3))
+                    states.setdefault(v + "/reseed", snap(env))
         set_knobs(None)
         ref = states[variants[0]]
         for v in variants:
             same = all(torch.equal(a, b) for a, b in zip(ref, states[v]))
             print(f"{cfg} G={G} N={N} E={E} {v:>14}: median {statistics.median(rates[v]):14,.0f}  "
                   f"max {max(rates[v]):14,.0f} resets/s  state==first:{same}", flush=True)
+            if args.reseed:
+                same = all(torch.equal(a, b) for a, b in zip(states[variants[0] + "/reseed"], states[v + "/reseed"]))
+                print(f"{cfg} G={G} N={N} E={E} {v:>14}: reseeding reset {statistics.median(reseed[v]):14,.0f} "
+                      f"resets/s  state==first:{same}", flush=True)
 
 
 if __name__ == "__main__":
