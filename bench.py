@@ -75,6 +75,10 @@ def max_over_ranks(v: float, world: int) -> float:
     return float(t.item())
 
 
+def min_over_ranks(v: float, world: int) -> float:
+    return -max_over_ranks(-v, world)
+
+
 def load_traffic(cfg_name: str):
     """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/),
     FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, or None."""
@@ -180,6 +184,63 @@ def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream)
             "loop": "act(obs_t) -> step + obs(K=1) -> replay add_many(obs_t, a, r, obs_t+1, done), capacity 10000"}
 
 
+def train_loop_bench(env, reps: int, seg: int = 100):
+    """SURVEY.md §8 D2 (C5 shape: "multi-step loop, hipGraph of step+obs+act")
+    and train_jax.py:38-113 minus the learner: per step, synthetic actions for
+    every drone, epsilon-greedy DQN action for drone 0 (dense 294->128->64->5),
+    step + obs(K=1), replay add_many of the drone-0 transition; after `seg`
+    steps a reset of every env (reset_env_every, train_jax.py:101-113) and its
+    first observation.  One segment is captured once as a HIP graph (no host
+    work per step) and replayed.  Counters (action stream step, epsilon draws,
+    replay cursor) are baked into the capture, so replays repeat them: the
+    work per step is the same, the action stream repeats every segment."""
+    from dronerl_amd.dqn import QNetwork, ReplayBuffer
+    E, N, dev = env.num_envs, env.n_drones, env.device
+    W = env.layout.obs_window
+    D = W * W * 6
+    net = QNetwork(D, (128, 64), device=dev, generator=torch.Generator().manual_seed(0))
+    rb = ReplayBuffer(10000, D, dev)
+    acts = torch.empty((E, N), dtype=torch.int32, device=dev)
+    rewards = torch.empty((E, N), dtype=torch.float32, device=dev)
+    dones = torch.empty((E, N), dtype=torch.uint8, device=dev)
+    bufs = [torch.empty((E, 1, W, W, 6), dtype=torch.float32, device=dev) for _ in range(2)]
+    env.get_obs(1, out=bufs[0])
+
+    def segment():
+        for t in range(seg):
+            cur, nxt = bufs[t & 1], bufs[(t + 1) & 1]
+            env.synth_actions(seed=2024, step=t, out=acts)
+            net.act(cur.reshape(E, -1), 0.1, seed=7, step=t, actions=acts)
+            env.step(acts, obs_k=1, rewards=rewards, dones=dones, obs=nxt)
+            rb.add_many(cur, acts, rewards, nxt, dones)
+        env.reset(seed=None)
+        env.get_obs(1, out=bufs[seg & 1])
+
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        segment()  # eager warm-up on the capture stream
+    torch.cuda.current_stream(dev).wait_stream(side)
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        segment()
+    g.replay()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    env.check_errors()
+    dt = e0.elapsed_time(e1) / 1e3
+    return {"env_steps_per_s": E * seg * reps / dt, "us_per_step": dt / (seg * reps) * 1e6,
+            "segments": reps, "steps_per_segment": seg,
+            "loop": f"hipGraph of {seg} x [synth actions -> qnet act (drone 0) -> step + obs(K=1) -> "
+                    f"replay add_many] + reset + obs, replayed {reps}x (learner not included)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -191,6 +252,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-reset-bench", action="store_true")
     ap.add_argument("--no-dqn", action="store_true", help="skip the DQN-consumer measurement (SURVEY.md §8 F1)")
+    ap.add_argument("--loop-segments", type=int, default=3,
+                    help="train-loop graph replays (100 steps + reset each; 0 = skip)")
     ap.add_argument("--obs-k", type=int, default=-1,
                     help="diagnostic: observed drones per step (default: the config's; 0 = step without obs)")
     args = ap.parse_args()
@@ -283,6 +346,12 @@ def main():
     if K >= 1 and not args.no_dqn:
         dqn = dqn_consumer_bench(env, actions, rewards, dones, obs, args.warmup, min(args.steps, 200), stream)
 
+    loop = None
+    if args.loop_segments > 0 and not args.no_dqn and K >= 1:
+        loop = train_loop_bench(env, args.loop_segments)
+        loop["env_steps_per_s"] = min_over_ranks(loop["env_steps_per_s"], world) * world
+        loop["n_gpus"] = world
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(G, N, K, args.cpu_seconds)
@@ -319,6 +388,7 @@ def main():
             "cpu_baseline": cpu,
             "resets_per_s": resets_per_s,
             "dqn_consumer": dqn,
+            "train_loop": loop,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
