@@ -184,6 +184,56 @@ def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream)
             "loop": "act(obs_t) -> step + obs(K=1) -> replay add_many(obs_t, a, r, obs_t+1, done), capacity 10000"}
 
 
+def rollout_bench(env, actions, K, warmup_steps, steps, chunk: int, R: int, Wb: int, world: int):
+    """drl_rollout (jax run_steps shape, env.py:252-272, plus every step's
+    rewards, dones and obs(K)): `chunk` steps per launch with the state on chip
+    between them, the same pre-generated actions as the per-step loop, every
+    step's outputs stored ([chunk, E, ...] buffers).  Timed like the main loop
+    (barrier + synchronize, max over ranks)."""
+    E, N, dev = env.num_envs, env.n_drones, env.device
+    W = env.layout.obs_window
+    rew = torch.empty((chunk, E, N), dtype=torch.float32, device=dev)
+    don = torch.empty((chunk, E, N), dtype=torch.uint8, device=dev)
+    obs = torch.empty((chunk, E, max(K, 1), W, W, 6), dtype=torch.float32, device=dev) if K else None
+    T = actions.shape[0]
+
+    def run(t0, n):
+        a = actions[t0 % T: t0 % T + n] if t0 % T + n <= T else actions[:n]
+        env.rollout(a, obs_k=K, rewards=rew[:n], dones=don[:n], obs=obs[:n] if K else None)
+
+    for t0 in range(0, warmup_steps, chunk):
+        run(t0, min(chunk, warmup_steps - t0))
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t_wall = time.perf_counter()
+    e0.record(stream)
+    done = 0
+    while done < steps:
+        n = min(chunk, steps - done)
+        run(warmup_steps + done, n)
+        done += n
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    wall = max_over_ranks(time.perf_counter() - t_wall, world)
+    env.check_errors()
+    ev_s = e0.elapsed_time(e1) / 1e3
+    per_step = ev_s / steps
+    return {"value": E * world * steps / wall, "unit": "env-steps/s", "steps": steps, "steps_per_launch": chunk,
+            "ms_per_step": wall / steps * 1e3,
+            "kernel": "drl_rollout_kernel", "avg_launch_us": ev_s / -(-steps // chunk) * 1e6,
+            "roofline": {"bound": "hbm", "achieved": E * R / per_step / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": E * R / per_step / 1e9 / PEAK_HBM_GBS,
+                         "achieved_read_plus_write": E * (R + Wb) / per_step / 1e9,
+                         "frac_read_plus_write": E * (R + Wb) / per_step / 1e9 / PEAK_HBM_GBS,
+                         "note": "same per-env-step algorithmic bytes as drl_step (SURVEY.md §8 D3); the state is "
+                                 "read and written once per launch, so HBM traffic per step is lower"}}
+
+
 def train_loop_bench(env, reps: int, seg: int = 100):
     """SURVEY.md §8 D2 (C5 shape: "multi-step loop, hipGraph of step+obs+act")
     and train_jax.py:38-113 minus the learner: per step, synthetic actions for
@@ -252,6 +302,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-reset-bench", action="store_true")
     ap.add_argument("--no-dqn", action="store_true", help="skip the DQN-consumer measurement (SURVEY.md §8 F1)")
+    ap.add_argument("--rollout-chunk", type=int, default=100,
+                    help="steps per drl_rollout launch for the rollout measurement (0 = skip)")
     ap.add_argument("--loop-segments", type=int, default=3,
                     help="train-loop graph replays (100 steps + reset each; 0 = skip)")
     ap.add_argument("--obs-k", type=int, default=-1,
@@ -346,6 +398,11 @@ def main():
     if K >= 1 and not args.no_dqn:
         dqn = dqn_consumer_bench(env, actions, rewards, dones, obs, args.warmup, min(args.steps, 200), stream)
 
+    roll = None
+    if args.rollout_chunk > 0:
+        env.reset(seed=0)
+        roll = rollout_bench(env, actions, K, args.warmup, args.steps, args.rollout_chunk, R, Wb, world)
+
     loop = None
     if args.loop_segments > 0 and not args.no_dqn and K >= 1:
         loop = train_loop_bench(env, args.loop_segments)
@@ -388,6 +445,7 @@ def main():
             "cpu_baseline": cpu,
             "resets_per_s": resets_per_s,
             "dqn_consumer": dqn,
+            "rollout": roll,
             "train_loop": loop,
         }
         print(json.dumps(out), flush=True)

@@ -268,8 +268,43 @@ int drl_step(const drl_params* p, const drl_state* s, const int32_t* d_actions, 
     a.obs = d_obs;
     a.err = d_err;
     a.og = obs_geom(p, L, d_obs ? obs_k : 1);
-    hipError_t e = drl::launch_step(a, L.step_group_lanes, stream, false);
+    hipError_t e = drl::launch_step(a, L.step_group_lanes, stream, drl::kStepMode);
     return e == hipSuccess ? 0 : hip_fail(e, "drl_step launch");
+}
+
+int drl_rollout(const drl_params* p, const drl_state* s, int32_t num_steps, const int32_t* d_actions,
+                int64_t act_step_stride, float* d_rewards, uint8_t* d_dones, int64_t out_step_stride, float* d_obs,
+                int32_t obs_k, int64_t obs_step_stride, int32_t* d_err, hipStream_t stream) {
+    drl_layout L;
+    if (validate(p, &L) || check_state(s, L)) return -1;
+    if (num_steps < 0) return fail("num_steps < 0");
+    if (s->num_envs == 0 || num_steps == 0) return 0;
+    if (!d_actions || !d_rewards || !d_dones) return fail("actions/rewards/dones must be non-NULL");
+    const int64_t EN = s->num_envs * (int64_t)p->n_drones;
+    if (num_steps > 1 && act_step_stride < EN) return fail("act_step_stride must be >= num_envs * n_drones");
+    if (out_step_stride != 0 && out_step_stride < EN) return fail("out_step_stride must be 0 or >= num_envs * n_drones");
+    if (d_obs) {
+        if (obs_k < 1 || obs_k > p->n_drones) return fail("obs_k %d outside [1, n_drones]", obs_k);
+        // the base 16-B aligned like drl_step; later steps' bases are 8-B aligned (strides are multiples of 6
+        // floats), which the observation writer handles (16-B stores where a wave's base allows them)
+        if ((uintptr_t)d_obs % 16 || obs_step_stride % 2) return fail("obs must be 16-byte aligned, obs_step_stride even");
+        const int64_t per = s->num_envs * (int64_t)obs_k * L.obs_floats;
+        if (obs_step_stride != 0 && obs_step_stride < per) return fail("obs_step_stride must be 0 or >= one step's obs");
+    }
+    drl::StepArgs a = step_args(p, s, L, d_obs ? obs_k : 0);
+    if (a.wave_lds > kLdsMax) return fail("obs_k %d needs %d B of LDS per wave", obs_k, a.wave_lds);
+    a.actions = d_actions;
+    a.rewards = d_rewards;
+    a.dones = d_dones;
+    a.obs = d_obs;
+    a.err = d_err;
+    a.og = obs_geom(p, L, d_obs ? obs_k : 1);
+    a.steps = num_steps;
+    a.act_tstride = act_step_stride;
+    a.out_tstride = out_step_stride;
+    a.obs_tstride = d_obs ? obs_step_stride : 0;
+    hipError_t e = drl::launch_step(a, L.step_group_lanes, stream, drl::kRolloutMode);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_rollout launch");
 }
 
 int drl_obs(const drl_params* p, const drl_state* s, int32_t k, float* d_obs, hipStream_t stream) {
@@ -283,7 +318,7 @@ int drl_obs(const drl_params* p, const drl_state* s, int32_t k, float* d_obs, hi
     if (a.wave_lds > kLdsMax) return fail("k %d needs %d B of LDS per wave", k, a.wave_lds);
     a.obs = d_obs;
     a.og = obs_geom(p, L, k);
-    hipError_t e = drl::launch_step(a, L.step_group_lanes, stream, true);
+    hipError_t e = drl::launch_step(a, L.step_group_lanes, stream, drl::kObsMode);
     return e == hipSuccess ? 0 : hip_fail(e, "drl_obs launch");
 }
 

@@ -90,6 +90,10 @@ struct StepArgs {
     uint32_t max_rounds;
     FastDiv div_side;
     ObsGeom og;
+    // drl_rollout (several steps per launch, state resident on chip): steps and
+    // per-step element strides of actions / rewards+dones / obs (0 = reuse)
+    int steps;
+    int64_t act_tstride, out_tstride, obs_tstride;
 };
 
 struct ResetArgs {
@@ -176,7 +180,8 @@ hipError_t launch_qnet_pack(const QnetPack& p, hipStream_t s);
 hipError_t launch_qnet_act(const QnetArgs& a, int num_cus, hipStream_t s);
 hipError_t launch_replay_add(const ReplayArgs& a, hipStream_t s);
 
-hipError_t launch_step(const StepArgs& a, int P, hipStream_t s, bool obs_only);
+enum StepMode : int { kStepMode = 0, kObsMode = 1, kRolloutMode = 2 };
+hipError_t launch_step(const StepArgs& a, int P, hipStream_t s, int mode);
 hipError_t launch_reset(const ResetArgs& a, hipStream_t s);
 hipError_t launch_decode(const uint32_t* drones, int64_t E, int N, int32_t* order, int32_t* y, int32_t* x,
                          int32_t* c, uint8_t* k, hipStream_t s);

@@ -416,14 +416,25 @@ __device__ __forceinline__ int lobit(uint64_t m) { return __ffsll((unsigned long
 __device__ __forceinline__ int hibit(uint32_t m) { return 31 - __clz(m); }
 __device__ __forceinline__ int hibit(uint64_t m) { return 63 - __clzll((long long)m); }
 
+// __shfl(v, src, P) with the lane id passed in (so a caller can keep the
+// address math from being hoisted; see step_batch)
+template <int P>
+__device__ __forceinline__ int gshfl(int v, int src, int lane) {
+    return __builtin_amdgcn_ds_bpermute(((lane & ~(P - 1)) + (src & (P - 1))) << 2, v);
+}
+
 // ------------------------------------------------------------------ step ---
 // One wave per block.  P <= 8 (small grids, LDS <= 5 KB/wave): cap registers
 // at 64 so 8 waves fit a SIMD and every wave of a 65536-env C3 launch is
 // resident at once (at 6 waves/SIMD a second, tail-heavy generation formed).
 // Wider groups are LDS-limited below 8 waves/SIMD: no cap (it only spilled).
 // Global addressing: 64-bit wave bases (scalar) + 32-bit lane offsets.
-// One batch (the wave's GPW envs starting at wenv0) of the step.
-template <int P, class GEO>
+// One batch (the wave's GPW envs starting at wenv0) of the step.  ROLL: a
+// rollout of a.steps steps (drl_rollout) with the state kept on chip between
+// them -- ground in LDS, drone records in the scratch area (O order) and the
+// MT index in a register -- and written back once at the end; the actions of
+// step t+1 are loaded during step t.
+template <int P, class GEO, bool ROLL>
 __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     using GMask = typename GMaskT<P>::type;
     constexpr int GPW = 64 / P;
@@ -434,23 +445,19 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     constexpr int CH = P < 16 ? P : 16;        // shuffle batch
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const GEO g{a};
-    const int lane = threadIdx.x & 63;
-    const int grp = lane / P;
-    const int j = lane % P;
+    const int lane0 = threadIdx.x & 63;
+    const int grp0 = lane0 / P;
+    const int j0 = lane0 % P;
     const int nenv_w = (int)min((int64_t)GPW, a.E - wenv0);
     if (nenv_w <= 0) return;
-    const bool env_ok = grp < nenv_w;
+    const bool env_ok0 = grp0 < nenv_w;
     const int G = g.side(), N = g.n(), gstride = g.gstride(), nchg = g.nchg();
     const WaveLds W = carve(smem, GPW, PF, g);
-    uint8_t* gl = W.gl + grp * gstride;
-    uint32_t* bm = W.bm + grp * (g.lds_bm() / 4);
-    uint32_t* mtw = W.mtw + grp * PF;
-    uint16_t* posidx = W.posidx + grp * g.np();
     // the wave's slices of the state (scalar bases)
     uint32_t* const drones_w = a.drones + wenv0 * N;
     uint32_t* const mt_w = a.mt + wenv0 * MT_WORDS;
     uint8_t* const ground_w = a.ground + wenv0 * gstride;
-    const uint32_t rl = (uint32_t)(grp * N);  // lane's env offset in [env][drone] arrays of the wave
+    const uint32_t rl0 = (uint32_t)(grp0 * N);  // lane's env offset in [env][drone] arrays of the wave
 
     DRL_STAMP(0);
     // ---- loads, in one round trip plus the MT-word prefetch: the env's MT
@@ -462,33 +469,62 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     uint32_t mi[GPW];  // uniform addresses, nothing written before: scalar loads (lgkmcnt)
 #pragma unroll
     for (int e = 0; e < GPW; ++e) mi[e] = a.mt_index[wenv0 + min(e, nenv_w - 1)];
-    lds_zero(W.bm, GPW * g.lds_bm(), lane);
-    if (GEO::kObs && a.obs) lds_zero(W.paint, GPW * g.lds_paint(), lane);
-    if (lane < GPW) W.cnt[lane * 4] = 0u;
+    lds_zero(W.bm, GPW * g.lds_bm(), lane0);
+    if (GEO::kObs && a.obs) lds_zero(W.paint, GPW * g.lds_paint(), lane0);
+    if (lane0 < GPW) W.cnt[lane0 * 4] = 0u;
     wave_sync();
-    const bool active = env_ok && j < N;
+    const bool active0 = env_ok0 && j0 < N;
     // unconditional loads at clamped indices (no exec-mask branches around
     // them, so the wait counts stay exact); inactive lanes discard the values
-    const uint32_t li = min(rl + (uint32_t)j, (uint32_t)(nenv_w * N - 1));
-    const uint32_t rec_ld = drones_w[li];
-    const int act_ld = a.actions[wenv0 * N + li];
-    if constexpr (GEO::kGstride > 0) stage_ground_dma_n<GPW * GEO::kGstride / 16>(ground_w, nenv_w * gstride, W.gl, lane);
-    else stage_ground_dma(ground_w, nenv_w * gstride, W.gl, lane);
+    const uint32_t li0 = min(rl0 + (uint32_t)j0, (uint32_t)(nenv_w * N - 1));
+    const uint32_t rec_ld = drones_w[li0];
+    const int act_ld = a.actions[wenv0 * N + li0];
+    if constexpr (GEO::kGstride > 0) stage_ground_dma_n<GPW * GEO::kGstride / 16>(ground_w, nenv_w * gstride, W.gl, lane0);
+    else stage_ground_dma(ground_w, nenv_w * gstride, W.gl, lane0);
     __builtin_amdgcn_sched_barrier(0);  // issue every load above before waiting for the MT index
     int midx = (int)mi[0];
 #pragma unroll
-    for (int e = 1; e < GPW; ++e) midx = (grp >= e) ? (int)mi[e] : midx;
-    const uint32_t rec = active ? rec_ld : 0u;
-    const int my_action = active ? act_ld : 4;
-    if (!env_ok) midx = MT_N;
+    for (int e = 1; e < GPW; ++e) midx = (grp0 >= e) ? (int)mi[e] : midx;
+    uint32_t rec = active0 ? rec_ld : 0u;
+    int my_action = active0 ? act_ld : 4;
+    if (!env_ok0) midx = MT_N;
+    uint32_t* const stash = W.mtw;  // ROLL: records between steps ([GPW][P], O order)
+    int act_next = 4;
+    const int T = ROLL ? a.steps : 1;
+    for (int t = 0; t < T; ++t) {
+    // per-lane indices and LDS pointers, re-derived every step from an opaque
+    // copy of the lane id: in a rollout under the 64-VGPR cap (P <= 8),
+    // hoisting them (and the shuffle addresses) out of the loop spills
+    int lane_l = lane0;
+    if constexpr (ROLL && P <= 8) asm volatile("" : "+v"(lane_l));
+    const int lane = lane_l, grp = lane / P, j = lane % P;
+    const bool env_ok = grp < nenv_w;
+    const bool active = env_ok && j < N;
+    const uint32_t rl = (uint32_t)(grp * N);
+    const uint32_t li = min(rl + (uint32_t)j, (uint32_t)(nenv_w * N - 1));
+    uint8_t* gl = W.gl + grp * gstride;
+    uint32_t* bm = W.bm + grp * (g.lds_bm() / 4);
+    uint32_t* mtw = W.mtw + grp * PF;
+    uint16_t* posidx = W.posidx + grp * g.np();
     const uint32_t* mrow = mt_w + (uint32_t)(env_ok ? grp : 0) * MT_WORDS;
+    if constexpr (ROLL) {
+        if (t > 0) {  // the previous step left its records in the stash
+            rec = active ? stash[lane] : 0u;
+            my_action = active ? act_next : 4;
+            wave_sync();
+            lds_zero(W.bm, GPW * g.lds_bm(), lane);
+            if (GEO::kObs && a.obs) lds_zero(W.paint, GPW * g.lds_paint(), lane);
+            wave_sync();
+        }
+        if (t + 1 < T) act_next = a.actions[(t + 1) * a.act_tstride + wenv0 * N + li];
+    }
 
     DRL_STAMP(1);
     const int y = rec & 255u, x = (rec >> 8) & 255u;
     const int idx = ((int)(rec >> 25) < N) ? (int)(rec >> 25) : j;  // corrupt records never index out of bounds
     int c = (rec >> 16) & 255u;
     int carry = (rec >> 24) & 1u;
-    int act = __shfl(my_action, idx, P);  // actions are by drone index (env.py:125)
+    int act = gshfl<P>(my_action, idx, lane);  // actions are by drone index (env.py:125)
     // MT-word prefetch: issued once the records have landed (LDS-DMA makes the
     // compiler wait for every outstanding load before the first record use),
     // so its latency overlaps the claim / effect / ordering phases
@@ -520,7 +556,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     for (int s0 = 0; s0 < P; s0 += CH) {
         int ts[CH];
 #pragma unroll
-        for (int t = 0; t < CH; ++t) ts[t] = __shfl(tcell, s0 + t, P);
+        for (int t = 0; t < CH; ++t) ts[t] = gshfl<P>(tcell, s0 + t, lane);
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
             const int s = s0 + t;
@@ -552,13 +588,13 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
             reward = a.r_pickup;
             carry = 1;
             gl[tcell] = OBJ_EMPTY;
-            chg_push(W, grp, nchg, tcell);
+            if constexpr (!ROLL) chg_push(W, grp, nchg, tcell);
         } else if (obj == OBJ_DROPZONE && carry) {
             reward = a.r_delivery;
             carry = 0;
             gl[tcell] = OBJ_EMPTY;
             deliver = true;
-            chg_push(W, grp, nchg, tcell);
+            if constexpr (!ROLL) chg_push(W, grp, nchg, tcell);
         }
         if (obj == OBJ_SKYSCRAPER) dead = true;
     }
@@ -584,7 +620,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         for (int s0 = 0; s0 < P; s0 += CH) {
             int ks[CH];
 #pragma unroll
-            for (int t = 0; t < CH; ++t) ks[t] = __shfl(bkey, s0 + t, P);
+            for (int t = 0; t < CH; ++t) ks[t] = gshfl<P>(bkey, s0 + t, lane);
 #pragma unroll
             for (int t = 0; t < CH; ++t) rankB += (ks[t] < bkey);
         }
@@ -663,10 +699,10 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         }
         // value r at a round position (group-uniform b)
         auto r_at = [&](int b) {
-            int v = __shfl(rq[0], b % P, P);
+            int v = gshfl<P>(rq[0], b % P, lane);
 #pragma unroll
             for (int q = 1; q < D; ++q) {
-                const int vq = __shfl(rq[q], b % P, P);
+                const int vq = gshfl<P>(rq[q], b % P, lane);
                 v = (b / P == q) ? vq : v;
             }
             return v;
@@ -703,10 +739,10 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
                     more = false;
                 } else {
                     const int b = lobit(m);
-                    int cell = __shfl(ccq[0], b % P, P);
+                    int cell = gshfl<P>(ccq[0], b % P, lane);
 #pragma unroll
                     for (int q = 1; q < D; ++q) {
-                        const int cq = __shfl(ccq[q], b % P, P);
+                        const int cq = gshfl<P>(ccq[q], b % P, lane);
                         cell = (b / P == q) ? cq : cell;
                     }
                     CM same = 0;
@@ -719,7 +755,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
                     } else {
                         if (j == 0) {
                             gl[cell] = (w < nR + n_pack) ? OBJ_PACKET : OBJ_DROPZONE;
-                            chg_push(W, grp, nchg, cell);
+                            if constexpr (!ROLL) chg_push(W, grp, nchg, cell);
                         }
                         okgc &= ~same;
                     }
@@ -758,22 +794,23 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     if (active && !carry && gl[pos] == OBJ_PACKET) {
         carry = 1;
         gl[pos] = OBJ_EMPTY;
-        chg_push(W, grp, nchg, pos);
+        if constexpr (!ROLL) chg_push(W, grp, nchg, pos);
     }
 
     // ---- write back: records permuted to O', rewards/dones by drone index,
     // changed ground cells as bytes
     const uint32_t py = g.div_side((uint32_t)(pos > 0 ? pos : 0));
     const uint32_t px = (uint32_t)(pos > 0 ? pos : 0) - py * (uint32_t)G;
+    const uint32_t rec_out = pack_drone((int)py, (int)px, c, carry, idx);
     if (active) {
-        drones_w[rl + newslot] = pack_drone((int)py, (int)px, c, carry, idx);
-        a.rewards[wenv0 * N + (rl + idx)] = reward;
-        a.dones[wenv0 * N + (rl + idx)] = crashed ? 1 : 0;
+        if constexpr (!ROLL) drones_w[rl + newslot] = rec_out;
+        a.rewards[t * a.out_tstride + wenv0 * N + (rl + idx)] = reward;
+        a.dones[t * a.out_tstride + wenv0 * N + (rl + idx)] = crashed ? 1 : 0;
         posidx[idx] = (uint16_t)pos;
     }
-    if (env_ok && j == 0) a.mt_index[wenv0 + grp] = (uint32_t)midx;
+    if (!ROLL && env_ok && j == 0) a.mt_index[wenv0 + grp] = (uint32_t)midx;
     wave_sync();
-    if (env_ok) {
+    if (!ROLL && env_ok) {
         const uint32_t nc = W.cnt[grp * 4];
         const uint16_t* ch = W.chg + grp * nchg;
         uint8_t* gdst = ground_w + (uint32_t)(grp * gstride);
@@ -790,9 +827,23 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         if (active) paint_windows(W.paint + grp * g.lds_paint(), posidx, (int)py, (int)px,
                                   (uint8_t)((c + 1) | (carry << 7)), g);
         wave_sync();
-        write_obs_wave(a.obs + wenv0 * (int64_t)(6u * g.env_cells()), nenv_w, g, W, a.obs_wide, lane);
+        write_obs_wave(a.obs + t * a.obs_tstride + wenv0 * (int64_t)(6u * g.env_cells()), nenv_w, g, W, a.obs_wide,
+                       lane);
     }
     DRL_STAMP(6);
+    if constexpr (ROLL) {  // records to the stash (the observation stage aliased it until here)
+        wave_sync();
+        if (active) stash[grp * P + newslot] = rec_out;
+    }
+    }  // steps
+    if constexpr (ROLL) {  // write the state back once: records, MT index, whole grounds
+        wave_sync();
+        if (active0) drones_w[rl0 + j0] = stash[lane0];
+        if (env_ok0 && j0 == 0) a.mt_index[wenv0 + grp0] = (uint32_t)midx;
+        const uint4* src = reinterpret_cast<const uint4*>(W.gl);
+        uint4* dst = reinterpret_cast<uint4*>(ground_w);
+        for (int v = lane0; v < nenv_w * gstride / 16; v += 64) dst[v] = src[v];
+    }
 }
 
 // One wave per batch of GPW envs.  (Persistent waves looping over 2-4 batches
@@ -801,7 +852,14 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
 template <int P, class GEO>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : 1, 8)))
 drl_step_kernel(StepArgs a) {
-    step_batch<P, GEO>(a, (int64_t)blockIdx.x * (64 / P));
+    step_batch<P, GEO, false>(a, (int64_t)blockIdx.x * (64 / P));
+}
+
+// drl_rollout: a.steps steps per launch, same wave layout.
+template <int P, class GEO>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : 1, 8)))
+drl_rollout_kernel(StepArgs a) {
+    step_batch<P, GEO, true>(a, (int64_t)blockIdx.x * (64 / P));
 }
 
 // ------------------------------------------------------------ observation ---
@@ -1413,12 +1471,14 @@ __global__ void drl_synth_actions_kernel(uint64_t seed, uint64_t step, int64_t e
 
 // ---------------------------------------------------------------- launch ---
 template <int P, class GEO>
-static hipError_t launch_step_t(const StepArgs& a, hipStream_t s, bool obs_only) {
+static hipError_t launch_step_t(const StepArgs& a, hipStream_t s, int mode) {
     const int64_t blocks = (a.E + (64 / P) - 1) / (64 / P);
     const dim3 grid((unsigned)blocks), block(64);
-    if (obs_only) {
+    if (mode == kObsMode) {
         if constexpr (GEO::kObs) hipLaunchKernelGGL((drl_obs_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
         else return hipErrorInvalidValue;
+    } else if (mode == kRolloutMode) {
+        hipLaunchKernelGGL((drl_rollout_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
     } else {
         hipLaunchKernelGGL((drl_step_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
     }
@@ -1428,31 +1488,31 @@ static hipError_t launch_step_t(const StepArgs& a, hipStream_t s, bool obs_only)
 // Compile-time-geometry instances for the benchmark shapes (side, drones,
 // radius; observation of drone 0 or none), the runtime-geometry one otherwise.
 template <int P, int G, int N, int R>
-static bool launch_spec(const StepArgs& a, hipStream_t s, bool obs_only, hipError_t* e) {
+static bool launch_spec(const StepArgs& a, hipStream_t s, int mode, hipError_t* e) {
     if (a.side != G || a.n_drones != N || a.og.radius != R) return false;
-    if (a.obs_k == 0 && !obs_only) *e = launch_step_t<P, Geo<G, N, R, 0>>(a, s, obs_only);
-    else if (a.obs_k == 1) *e = launch_step_t<P, Geo<G, N, R, 1>>(a, s, obs_only);
+    if (a.obs_k == 0 && mode != kObsMode) *e = launch_step_t<P, Geo<G, N, R, 0>>(a, s, mode);
+    else if (a.obs_k == 1) *e = launch_step_t<P, Geo<G, N, R, 1>>(a, s, mode);
     else return false;
     return true;
 }
 
-hipError_t launch_step(const StepArgs& a, int P, hipStream_t s, bool obs_only) {
+hipError_t launch_step(const StepArgs& a, int P, hipStream_t s, int mode) {
     hipError_t e = hipSuccess;
     const bool spec = a.specialize;
     switch (P) {
         case 4:
-            if (spec && launch_spec<4, 8, 4, 3>(a, s, obs_only, &e)) return e;
-            return launch_step_t<4, GeoRT>(a, s, obs_only);
+            if (spec && launch_spec<4, 8, 4, 3>(a, s, mode, &e)) return e;
+            return launch_step_t<4, GeoRT>(a, s, mode);
         case 8:
-            if (spec && launch_spec<8, 16, 8, 3>(a, s, obs_only, &e)) return e;
-            return launch_step_t<8, GeoRT>(a, s, obs_only);
+            if (spec && launch_spec<8, 16, 8, 3>(a, s, mode, &e)) return e;
+            return launch_step_t<8, GeoRT>(a, s, mode);
         case 16:
-            if (spec && launch_spec<16, 32, 16, 3>(a, s, obs_only, &e)) return e;
-            return launch_step_t<16, GeoRT>(a, s, obs_only);
+            if (spec && launch_spec<16, 32, 16, 3>(a, s, mode, &e)) return e;
+            return launch_step_t<16, GeoRT>(a, s, mode);
         case 32:
-            if (spec && launch_spec<32, 64, 32, 3>(a, s, obs_only, &e)) return e;
-            return launch_step_t<32, GeoRT>(a, s, obs_only);
-        case 64: return launch_step_t<64, GeoRT>(a, s, obs_only);
+            if (spec && launch_spec<32, 64, 32, 3>(a, s, mode, &e)) return e;
+            return launch_step_t<32, GeoRT>(a, s, mode);
+        case 64: return launch_step_t<64, GeoRT>(a, s, mode);
         default: return hipErrorInvalidValue;
     }
 }

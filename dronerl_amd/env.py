@@ -133,6 +133,41 @@ class BatchedDeliveryDrones:
             return rewards, dones, obs
         return rewards, dones
 
+    def rollout(self, actions: torch.Tensor, obs_k: int = 0, every_step: bool = True,
+                rewards: Optional[torch.Tensor] = None, dones: Optional[torch.Tensor] = None,
+                obs: Optional[torch.Tensor] = None):
+        """T steps in one launch (jax run_steps, env.py:252-272, plus per-step
+        outputs): actions int32 [T, E, N].  Same results as T step() calls.
+
+        every_step: rewards/dones [T, E, N] and obs [T, E, obs_k, W, W, 6];
+        otherwise [E, N] / [E, obs_k, W, W, 6] holding the last step's.
+        """
+        E, N = self.num_envs, self.n_drones
+        if actions.dim() != 3 or actions.shape[1:] != (E, N):
+            raise ValueError(f"actions must be [T, {E}, {N}], got {tuple(actions.shape)}")
+        T = actions.shape[0]
+        actions = self._check(actions, torch.int32, (T, E, N), "actions")
+        lead = (T,) if every_step else ()
+        if rewards is None:
+            rewards = torch.empty(lead + (E, N), dtype=torch.float32, device=self.device)
+        if dones is None:
+            dones = torch.empty(lead + (E, N), dtype=torch.uint8, device=self.device)
+        W = self.layout.obs_window
+        if obs_k and obs is None:
+            obs = torch.empty(lead + (E, obs_k, W, W, 6), dtype=torch.float32, device=self.device)
+        self._check_out(rewards, torch.float32, lead + (E, N), "rewards")
+        self._check_out(dones, torch.uint8, lead + (E, N), "dones")
+        if obs_k:
+            self._check_out(obs, torch.float32, lead + (E, obs_k, W, W, 6), "obs")
+        ostride = E * obs_k * W * W * 6 if every_step else 0
+        s = self.state.c()
+        check(lib().drl_rollout(ctypes.byref(self._cp), ctypes.byref(s), T, _ptr(actions), E * N, _ptr(rewards),
+                                _ptr(dones), E * N if every_step else 0, _ptr(obs) if obs_k else None, int(obs_k),
+                                ostride, _ptr(self.err), _stream(self.device)), "drl_rollout")
+        if obs_k:
+            return rewards, dones, obs
+        return rewards, dones
+
     def get_obs(self, k: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """WindowedGridView observation of drone indices 0..k-1: f32 [E, k, W, W, 6]."""
         k = self.n_drones if k is None else int(k)
@@ -229,6 +264,12 @@ class BatchedDeliveryDrones:
             raise DroneRLError("; ".join(msgs))
 
     # ------------------------------------------------------------- helpers --
+    def _check_out(self, t: torch.Tensor, dtype, shape, name):
+        """Output buffers are written in place: no conversion, exact layout."""
+        if (not isinstance(t, torch.Tensor) or t.device != self.device or t.dtype != dtype
+                or tuple(t.shape) != tuple(shape) or not t.is_contiguous()):
+            raise ValueError(f"{name} must be a contiguous {dtype} tensor of shape {tuple(shape)} on {self.device}")
+
     def _check(self, t: torch.Tensor, dtype, shape, name):
         if not isinstance(t, torch.Tensor):
             t = torch.as_tensor(t)

@@ -136,6 +136,17 @@ int drl_reset(const drl_params* p, const drl_state* s, int32_t reseed, uint64_t 
 int drl_step(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
              uint8_t* d_dones, float* d_obs, int32_t obs_k, int32_t* d_err, hipStream_t stream);
 
+/* num_steps steps in one launch (jax_impl run_steps, env/env.py:252-272, with
+ * the rewards, dones and observation of every step): identical results to
+ * num_steps drl_step calls.  Step t reads d_actions + t * act_step_stride and
+ * writes d_rewards / d_dones + t * out_step_stride and d_obs + t *
+ * obs_step_stride (element strides; out/obs stride 0 = every step overwrites
+ * the same buffer, leaving the last step's).  The state stays on chip
+ * between steps and is written back once at the end. */
+int drl_rollout(const drl_params* p, const drl_state* s, int32_t num_steps, const int32_t* d_actions,
+                int64_t act_step_stride, float* d_rewards, uint8_t* d_dones, int64_t out_step_stride, float* d_obs,
+                int32_t obs_k, int64_t obs_step_stride, int32_t* d_err, hipStream_t stream);
+
 /* WindowedGridView observation (wrappers.py:10-31,55-73) of drone indices
  * 0..k-1: f32 [E][k][W][W][6]. */
 int drl_obs(const drl_params* p, const drl_state* s, int32_t k, float* d_obs, hipStream_t stream);

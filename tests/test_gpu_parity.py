@@ -592,3 +592,63 @@ def test_grid_obs_vs_oracle_state_and_compat_gridview():
     assert grid0.dtype == np.float32 and grid0.shape == (g.side_size, g.side_size, 6)
     for (y, x), dr in g.drones.items():
         assert grid0[y, x, 0] == 1 and grid0[y, x, 4] == np.float32(dr.charge / 100)
+
+
+# ------------------------------------------------------------- rollout ---
+@pytest.mark.parametrize("name,E,T,k", [
+    ("c1_8x8_n4", 64, 40, 1),
+    ("c2_16x16_n8", 1000, 60, 1),
+    ("c2_16x16_n8", 257, 30, 0),
+    ("c2_16x16_n8", 65, 25, 3),
+    ("c4_32x32_n16", 300, 30, 1),
+    ("c5_64x64_n32", 64, 20, 1),
+    ("n6_11x11", 129, 50, 2),
+    ("n33_26x26", 33, 20, 1),
+    ("pool_5x5_n2", 100, 80, 1),
+    ("dense_10x10_n8", 200, 60, 1),
+    ("c2_16x16_n8|rt", 333, 30, 1),
+])
+def test_rollout_equals_steps(name, E, T, k, monkeypatch):
+    """drl_rollout (T steps per launch, state on chip) == T drl_step calls:
+    per-step rewards, dones and observations, and the final state."""
+    name, _, rt = name.partition("|")
+    if rt:
+        monkeypatch.setenv("DRL_SPECIALIZE", "0")
+    p = EnvParams(**CONFIGS[name])
+    a_env, b_env = Env(p, E), Env(p, E)
+    a_env.reset(seed=21)
+    b_env.reset(seed=21)
+    for t in range(3):  # some history first
+        acts = a_env.synth_actions(seed=4, step=100 + t)
+        a_env.step(acts)
+        b_env.step(acts)
+    acts = torch.stack([a_env.synth_actions(seed=4, step=t) for t in range(T)])
+    out = b_env.rollout(acts, obs_k=k)
+    for t in range(T):
+        r = a_env.step(acts[t], obs_k=k)
+        assert torch.equal(r[0], out[0][t]), f"{name} step {t} rewards"
+        assert torch.equal(r[1], out[1][t]), f"{name} step {t} dones"
+        if k:
+            assert torch.equal(r[2], out[2][t]), f"{name} step {t} obs"
+    for f in ["ground", "drones", "mt", "mt_index"]:
+        assert torch.equal(getattr(a_env.state, f), getattr(b_env.state, f)), f"{name} final {f}"
+    a_env.check_errors()
+    b_env.check_errors()
+
+
+def test_rollout_last_step_outputs_and_oracle():
+    """every_step=False keeps the last step's outputs; the final state matches the oracle."""
+    p = EnvParams(**CONFIGS["c2_16x16_n8"])
+    E, T = 500, 40
+    env = Env(p, E)
+    env.reset(seed=9)
+    o = OracleMulti(oparams(p), E)
+    o.reset(9 + np.arange(E))
+    acts = torch.stack([env.synth_actions(seed=6, step=t) for t in range(T)])
+    r, d, ob = env.rollout(acts, obs_k=1, every_step=False)
+    for t in range(T):
+        ro, do = o.step(acts[t].cpu().numpy())
+    assert_rewards(r.cpu().numpy(), ro, "last step")
+    np.testing.assert_array_equal(d.cpu().numpy().astype(bool), do)
+    np.testing.assert_array_equal(ob.cpu().numpy(), o.obs(3, 1))
+    assert_state(gpu_state(env), o.state(), "rollout final")
