@@ -420,7 +420,11 @@ __device__ __forceinline__ int hibit(uint64_t m) { return 63 - __clzll((long lon
 // address math from being hoisted; see step_batch)
 template <int P>
 __device__ __forceinline__ int gshfl(int v, int src, int lane) {
+#ifdef DRL_HIP_SHFL  // diagnostic A/B: HIP's own __shfl
+    return __shfl(v, src, P);
+#else
     return __builtin_amdgcn_ds_bpermute(((lane & ~(P - 1)) + (src & (P - 1))) << 2, v);
+#endif
 }
 
 // ------------------------------------------------------------------ step ---
