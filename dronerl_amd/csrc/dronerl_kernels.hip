@@ -1463,11 +1463,18 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
 }
 
 __global__ void drl_synth_actions_kernel(uint64_t seed, uint64_t step, int64_t env_offset, int64_t total, int N,
-                                         int32_t* out) {
+                                         FastDiv dn, int fast, int32_t* out) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= total) return;
-    const uint64_t env = (uint64_t)(env_offset + t / N);
-    const uint64_t drone = (uint64_t)(t % N);
+    uint64_t env, drone;
+    if (fast) {  // total * N < 2^32: 32-bit multiply-shift division
+        const uint32_t e = fdiv((uint32_t)t, dn);
+        env = (uint64_t)(env_offset + e);
+        drone = (uint32_t)t - e * (uint32_t)N;
+    } else {
+        env = (uint64_t)(env_offset + t / N);
+        drone = (uint64_t)(t % N);
+    }
     const uint64_t ctr = (step << 40) ^ (env << 8) ^ drone;
     const uint64_t h = splitmix64(seed ^ splitmix64(ctr));
     out[t] = (int32_t)(((h >> 32) * 5ull) >> 32);
@@ -1563,8 +1570,9 @@ hipError_t launch_encode(uint32_t* drones, int64_t E, int N, const int32_t* orde
 hipError_t launch_synth(uint64_t seed, uint64_t step, int64_t env_offset, int64_t E, int N, int32_t* out,
                         hipStream_t s) {
     const int64_t total = E * N;
+    const int fast = (uint64_t)total * (uint64_t)N < (1ull << 32) ? 1 : 0;
     hipLaunchKernelGGL(drl_synth_actions_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, seed, step,
-                       env_offset, total, N, out);
+                       env_offset, total, N, make_fastdiv((uint32_t)N), fast, out);
     return hipGetLastError();
 }
 

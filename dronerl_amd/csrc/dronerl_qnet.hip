@@ -78,9 +78,9 @@ __global__ void drl_qnet_pack_kernel(QnetPack p) {
 // slice QN_RING positions ahead as soon as it is consumed.  The slice count is
 // padded to a multiple of QN_RING (zero weight fragments), so ring positions
 // are static and the loads need no masks or branches.
-constexpr int QN_WAVES = 8;
+constexpr int QN_WAVES = lay::qn_waves;
 constexpr int QN_MAXT = 8;    // 16-unit tiles per hidden layer (hidden <= 128)
-constexpr int QN_RING = 5;    // K-slices in flight per wave
+constexpr int QN_RING = lay::qn_ring;  // K-slices in flight per wave
 
 __device__ __forceinline__ bf16x8 lds_frag(const uint4* base, int frag, int lane) {
     const uint4 v = base[frag * 64 + lane];
@@ -234,8 +234,29 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_kernel(QnetArgs a)
 // Transition i of the batch goes to slot (cursor + i) % capacity; with more
 // transitions than slots only the last `capacity` are written (what a
 // sequential add() loop leaves; XLA's duplicate-index scatter in add_many
-// leaves the order unspecified).  One block per transition, float2 copies.
-__global__ void drl_replay_add_kernel(ReplayArgs a) {
+// leaves the order unspecified).
+// One thread per float2 of the rows that land (flattened [rows][obs_floats/2]:
+// coalesced over rows, ring-buffer slots contiguous except at the wrap); the
+// thread of column 0 also copies the row's action / reward / done.
+__global__ void __launch_bounds__(256) drl_replay_add_kernel(ReplayArgs a, FastDiv dcols, uint32_t total) {
+    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+    if (k >= total) return;
+    const uint32_t D2 = (uint32_t)a.obs_floats / 2u;
+    const uint32_t r = __umulhi(k, dcols.m), col = k - r * D2;  // D2 >= 1; dcols.one handled by the host
+    const int64_t i = a.first + r;
+    const int64_t slot = (a.cursor + i) % a.capacity;
+    const float2 o = reinterpret_cast<const float2*>(a.obs + i * a.obs_stride)[col];
+    const float2 nx = reinterpret_cast<const float2*>(a.next_obs + i * a.next_obs_stride)[col];
+    reinterpret_cast<float2*>(a.buf_obs + slot * a.obs_floats)[col] = o;
+    reinterpret_cast<float2*>(a.buf_next_obs + slot * a.obs_floats)[col] = nx;
+    if (col == 0) {
+        a.buf_actions[slot] = a.actions[i * a.action_stride];
+        a.buf_rewards[slot] = a.rewards[i * a.reward_stride];
+        a.buf_dones[slot] = a.dones[i * a.done_stride];
+    }
+}
+
+__global__ void drl_replay_add_rows_kernel(ReplayArgs a) {  // fallback for huge batches: block per row
     const int64_t i = a.first + blockIdx.x;
     if (i >= a.n) return;
     const int64_t slot = (a.cursor + i) % a.capacity;
@@ -280,7 +301,14 @@ hipError_t launch_qnet_act(const QnetArgs& a, int num_cus, hipStream_t s) {
 hipError_t launch_replay_add(const ReplayArgs& a, hipStream_t s) {
     const int64_t rows = a.n - a.first;
     if (rows <= 0) return hipSuccess;
-    hipLaunchKernelGGL(drl_replay_add_kernel, dim3((unsigned)rows), dim3(64), 0, s, a);
+    const uint64_t D2 = (uint64_t)a.obs_floats / 2;
+    const uint64_t total = (uint64_t)rows * D2;
+    if (D2 >= 2 && total * D2 < (1ull << 32)) {  // multiply-shift row index exact (FastDiv bound)
+        hipLaunchKernelGGL(drl_replay_add_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a,
+                           make_fastdiv((uint32_t)D2), (uint32_t)total);
+    } else {
+        hipLaunchKernelGGL(drl_replay_add_rows_kernel, dim3((unsigned)rows), dim3(64), 0, s, a);
+    }
     return hipGetLastError();
 }
 

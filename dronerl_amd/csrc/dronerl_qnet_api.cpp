@@ -36,8 +36,9 @@ int qnet_layout(const drl_qnet_desc* d, drl::QnetLayout* L) {
         L->in[l] = l == 0 ? d->in_features : d->hidden[l - 1];
         L->out[l] = l < d->n_hidden ? d->hidden[l] : d->n_actions;
         L->nt[l] = (L->out[l] + 15) / 16;  // 16-row MFMA tiles
-        // 32-wide K-slices; layer 0 padded to a multiple of the act kernel's slice ring (5)
-        L->kt[l] = l == 0 ? ((d->in_features + 31) / 32 + 4) / 5 * 5 : L->in[l] / 32;
+        // 32-wide K-slices; layer 0 padded to a multiple of the act kernel's slice ring
+        constexpr int R = drl::lay::qn_ring;
+        L->kt[l] = l == 0 ? ((d->in_features + 31) / 32 + R - 1) / R * R : L->in[l] / 32;
         L->frag_off[l] = frag * 64;
         L->bias_off[l] = bias;
         frag += L->nt[l] * L->kt[l];

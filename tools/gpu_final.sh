@@ -1,0 +1,11 @@
+# Round-end evidence on one GPU: parity tests, smoke, the default bench line
+# (C3), C4/C5 bench lines, and the rocprofv3 trace + PMC passes of C3.
+set -u
+cd /root/repo
+export TMPDIR=/tmp
+bash tools/gpu_check.sh || exit $?
+for c in c4 c5; do
+  timeout -k 10 300 python bench.py --config $c --no-cpu-baseline > gpurun_out/bench_$c.json 2> gpurun_out/bench_$c.err || exit $?
+done
+OUT=gpurun_out/prof CFG=c3 bash tools/profile.sh > gpurun_out/profile.log 2>&1 || { tail -5 gpurun_out/profile.log; exit 1; }
+echo done
