@@ -3,8 +3,9 @@
 
 python tools/ab.py --config c3 --rounds 5 --steps 100
 Variants (env knobs read per call): specN = DRL_SPECIALIZE (compile-time
-geometry instance on/off), noobs = step without observation, wide0 = 8-B
-observation stores.  Prints median/min µs per launch.
+geometry instance on/off), noobs = step without observation, wideN =
+observation store mode (0: 8-B stores, 1: 16-B via LDS transpose, the
+default).  Prints median/min µs per launch.
 """
 import argparse
 import ctypes
@@ -57,7 +58,7 @@ def main():
         for v in variants:
             parts = v.split("_")
             os.environ["DRL_SPECIALIZE"] = parts[0][4:] if parts[0].startswith("spec") else "1"
-            os.environ["DRL_OBS_WIDE"] = "0" if "wide0" in parts else "1"
+            os.environ["DRL_OBS_WIDE"] = next((x[4:] for x in parts if x.startswith("wide")), "1")
             k = 0 if "noobs" in parts else K
             o = op if k else None
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
