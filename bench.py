@@ -402,6 +402,11 @@ def main():
     if args.rollout_chunk > 0:
         env.reset(seed=0)
         roll = rollout_bench(env, actions, K, args.warmup, args.steps, args.rollout_chunk, R, Wb, world)
+        if K > 0:  # jax run_steps exactly (no observation): rewards/dones of every step only
+            env.reset(seed=0)
+            R0, W0 = algorithmic_bytes(G, N, 0, W)
+            r0 = rollout_bench(env, actions, 0, args.warmup, args.steps, args.rollout_chunk, R0, W0, world)
+            roll["no_obs"] = {k: r0[k] for k in ("value", "ms_per_step")}
 
     loop = None
     if args.loop_segments > 0 and not args.no_dqn and K >= 1:
