@@ -277,6 +277,22 @@ __device__ __forceinline__ void stage_ground_dma_n(const uint8_t* __restrict__ s
     }
 }
 
+// 16-B observation store.  NT: streaming (global_store_dwordx4 ... nt), for
+// drl_rollout, whose per-step observations are bulk output (C3 rollout 29.4
+// -> 26.2 us/step).  drl_step keeps ordinary stores: its observation is read
+// right away by the next kernel (the policy), which then hits the MALL (C3
+// train loop 73.6 us/step cached vs 76.5 streaming, although the step alone
+// is 11% faster streaming).
+template <bool NT>
+__device__ __forceinline__ void store_obs16(uint4* p, uint4 v) {
+    if constexpr (NT) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store((u32x4){v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(p));
+    } else {
+        *p = v;
+    }
+}
+
 // Zero [nbytes) of LDS (16-B multiple) cooperatively.
 __device__ __forceinline__ void lds_zero(void* p, int nbytes, int lane) {
     uint4* q = reinterpret_cast<uint4*>(p);
@@ -291,7 +307,7 @@ __device__ __forceinline__ void lds_zero(void* p, int nbytes, int lane) {
 // (true f32 division, == f32(double c/100)), ch5 skyscraper or wall.
 // `base` is the wave's first observation float (16-B aligned unless a wave
 // holds one env with an odd K*W*W).
-template <class GEO>
+template <bool NT = false, class GEO>
 __device__ __forceinline__ void write_obs_wave(float* __restrict__ base, int nenv_w, const GEO& g, const WaveLds& w,
                                                bool obs_wide, int lane) {
     const uint32_t W = g.W();
@@ -348,12 +364,12 @@ __device__ __forceinline__ void write_obs_wave(float* __restrict__ base, int nen
             if (q0 + 64u * OBS_U <= ncell) {  // full pass: 96*OBS_U 16-B pieces
 #pragma unroll
                 for (int t = 0; t < 96 * OBS_U; t += 64)
-                    if (96 * OBS_U - t >= 64 || lane < 96 * OBS_U - t) dst[t + lane] = sv[t + lane];
+                    if (96 * OBS_U - t >= 64 || lane < 96 * OBS_U - t) store_obs16<NT>(&dst[t + lane], sv[t + lane]);
             } else {
                 const uint32_t nbytes = (ncell - q0) * 24u;
                 for (uint32_t t = lane; t * 16u < nbytes; t += 64) {
                     if (t * 16u + 16u <= nbytes) {
-                        dst[t] = sv[t];
+                        store_obs16<NT>(&dst[t], sv[t]);
                     } else {  // 8-byte tail
                         reinterpret_cast<uint2*>(dst + t)[0] = reinterpret_cast<const uint2*>(sv + t)[0];
                     }
@@ -831,8 +847,8 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         if (active) paint_windows(W.paint + grp * g.lds_paint(), posidx, (int)py, (int)px,
                                   (uint8_t)((c + 1) | (carry << 7)), g);
         wave_sync();
-        write_obs_wave(a.obs + t * a.obs_tstride + wenv0 * (int64_t)(6u * g.env_cells()), nenv_w, g, W, a.obs_wide,
-                       lane);
+        write_obs_wave<ROLL>(a.obs + t * a.obs_tstride + wenv0 * (int64_t)(6u * g.env_cells()), nenv_w, g, W,
+                             a.obs_wide, lane);
     }
     DRL_STAMP(6);
     if constexpr (ROLL) {  // records to the stash (the observation stage aliased it until here)

@@ -7,10 +7,13 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
+import dronerl_amd._native as nat  # noqa: E402
 from bench import CONFIGS  # noqa: E402
 from dronerl_amd import BatchedDeliveryDrones, EnvParams  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+if len(sys.argv) > 2:  # alternative library (tools/variants.py)
+    nat.LIB_PATH = os.path.abspath(sys.argv[2])
 G, N, E, K = CONFIGS[cfg]
 env = BatchedDeliveryDrones(EnvParams(n_drones=N, grid_size=G), E)
 env.reset(seed=0)
@@ -25,4 +28,4 @@ for every in (True, False, True, False):
         env.rollout(acts, obs_k=K, every_step=every)
     e1.record()
     torch.cuda.synchronize()
-    print(f"{cfg} every_step={every}: {e0.elapsed_time(e1) * 1e3 / (3 * T):.2f} us/step")
+    print(f"{os.path.basename(nat.LIB_PATH)} {cfg} every_step={every}: {e0.elapsed_time(e1) * 1e3 / (3 * T):.2f} us/step")
