@@ -306,6 +306,8 @@ def main():
                     help="steps per drl_rollout launch for the rollout measurement (0 = skip)")
     ap.add_argument("--loop-segments", type=int, default=3,
                     help="train-loop graph replays (100 steps + reset each; 0 = skip)")
+    ap.add_argument("--obs-cached", action="store_true",
+                    help="write the per-step observation with cached stores (default: streaming, DRL_STEP_OBS_STREAM)")
     ap.add_argument("--obs-k", type=int, default=-1,
                     help="diagnostic: observed drones per step (default: the config's; 0 = step without obs)")
     args = ap.parse_args()
@@ -315,7 +317,7 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
     from dronerl_amd import BatchedDeliveryDrones, EnvParams
-    from dronerl_amd._native import lib
+    from dronerl_amd._native import DRL_STEP_OBS_STREAM, lib
 
     G, N, E, K = CONFIGS[args.config]
     if args.envs:
@@ -349,8 +351,14 @@ def main():
     stream = torch.cuda.current_stream(dev)
     s_p = ctypes.c_void_p(stream.cuda_stream)
 
+    # the observation is bulk output here (nothing reads it before the next
+    # step overwrites it): streaming stores unless --obs-cached.  The train
+    # loop below, whose policy reads the observation right away, keeps cached
+    # stores.
+    flags = 0 if args.obs_cached else DRL_STEP_OBS_STREAM
+
     def run(t):
-        rc = L.drl_step(cp, sp, a_ptrs[t], r_p, d_p, o_p, K, e_p, s_p)
+        rc = L.drl_step_ex(cp, sp, a_ptrs[t], r_p, d_p, o_p, K, e_p, flags, s_p)
         if rc:
             raise RuntimeError(L.drl_last_error().decode())
 
@@ -438,7 +446,8 @@ def main():
             "config": {"workload": f"{args.config.upper()}: {G}x{G} grid, {N} drones, {E} envs/GPU, "
                                    f"step + fused obs(K={K})",
                        "grid": G, "n_drones": N, "num_envs_per_gpu": E, "num_envs_total": E * world,
-                       "obs_k": K, "parallelism": f"env-shard x{world}"},
+                       "obs_k": K, "obs_stores": "cached" if args.obs_cached else "streaming",
+                       "parallelism": f"env-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS,
                          "traffic": traffic,

@@ -18,10 +18,11 @@ DRL_MAX_SIDE = 128
 DRL_MAX_RADIUS = 8
 DRL_ERR_BAD_ACTION = 1
 DRL_ERR_NO_FREE_CELL = 2
+DRL_STEP_OBS_STREAM = 1  # drl_step_ex flag: streaming (non-temporal) observation stores
 
 # Every symbol include/dronerl.h declares (tests check the .so exports them all).
 EXPORTS = ["drl_abi_version", "drl_last_error", "drl_side_from_density", "drl_layout_query", "drl_reset",
-           "drl_step", "drl_rollout", "drl_obs", "drl_grid_obs", "drl_decode", "drl_encode", "drl_synth_actions",
+           "drl_step", "drl_step_ex", "drl_rollout", "drl_obs", "drl_grid_obs", "drl_decode", "drl_encode", "drl_synth_actions",
            # library-owned env handles
            "drl_env_create", "drl_env_destroy", "drl_env_seed", "drl_env_reset", "drl_env_step",
            "drl_env_step_obs", "drl_env_obs", "drl_env_grid_obs", "drl_env_get_state", "drl_env_set_state", "drl_env_state",
@@ -90,13 +91,14 @@ def lib():
     L.drl_layout_query.argtypes = [P, ctypes.POINTER(DrlLayout)]
     L.drl_reset.argtypes = [P, S, i32, u64, vp, vp]
     L.drl_step.argtypes = [P, S, vp, vp, vp, vp, i32, vp, vp]
+    L.drl_step_ex.argtypes = [P, S, vp, vp, vp, vp, i32, vp, ctypes.c_uint32, vp]
     L.drl_rollout.argtypes = [P, S, i32, vp, i64, vp, vp, i64, vp, i32, i64, vp, vp]
     L.drl_obs.argtypes = [P, S, i32, vp, vp]
     L.drl_grid_obs.argtypes = [P, S, vp, vp]
     L.drl_decode.argtypes = [P, S, vp, vp, vp, vp, vp, vp]
     L.drl_encode.argtypes = [P, S, vp, vp, vp, vp, vp, vp]
     L.drl_synth_actions.argtypes = [u64, u64, i64, i64, i32, vp, vp]
-    for f in ["drl_layout_query", "drl_reset", "drl_step", "drl_rollout", "drl_obs", "drl_grid_obs", "drl_decode", "drl_encode",
+    for f in ["drl_layout_query", "drl_reset", "drl_step", "drl_step_ex", "drl_rollout", "drl_obs", "drl_grid_obs", "drl_decode", "drl_encode",
               "drl_synth_actions"]:
         getattr(L, f).restype = ctypes.c_int
     if L.drl_abi_version() != 2:

@@ -254,7 +254,14 @@ int drl_reset(const drl_params* p, const drl_state* s, int32_t reseed, uint64_t 
 
 int drl_step(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards, uint8_t* d_dones,
              float* d_obs, int32_t obs_k, int32_t* d_err, hipStream_t stream) {
+    return drl_step_ex(p, s, d_actions, d_rewards, d_dones, d_obs, obs_k, d_err, 0u, stream);
+}
+
+int drl_step_ex(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
+                uint8_t* d_dones, float* d_obs, int32_t obs_k, int32_t* d_err, uint32_t flags,
+                hipStream_t stream) {
     drl_layout L;
+    if (flags & ~DRL_STEP_OBS_STREAM) return fail("unknown drl_step flags 0x%x", flags);
     if (validate(p, &L) || check_state(s, L)) return -1;
     if (s->num_envs == 0) return 0;
     if (!d_actions || !d_rewards || !d_dones) return fail("actions/rewards/dones must be non-NULL");
@@ -268,6 +275,7 @@ int drl_step(const drl_params* p, const drl_state* s, const int32_t* d_actions, 
     a.obs = d_obs;
     a.err = d_err;
     a.og = obs_geom(p, L, d_obs ? obs_k : 1);
+    a.obs_nt = (flags & DRL_STEP_OBS_STREAM) ? 1 : 0;
     hipError_t e = drl::launch_step(a, L.step_group_lanes, stream, drl::kStepMode);
     return e == hipSuccess ? 0 : hip_fail(e, "drl_step launch");
 }

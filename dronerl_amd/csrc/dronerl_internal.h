@@ -94,6 +94,7 @@ struct StepArgs {
     int nchg;       // changed-cell list capacity (entries)
     int obs_k;      // observed drones (0: no observation)
     int obs_wide;   // observation stores: 1 = 16-B via LDS transpose, 0 = 3 x 8-B per cell
+    int obs_nt;     // drl_step: 1 = streaming (non-temporal) observation stores (DRL_STEP_OBS_STREAM)
     int specialize; // 1: use a compile-time-geometry instance when one matches (DRL_SPECIALIZE=0 disables)
     uint32_t max_rounds;
     FastDiv div_side;

@@ -32,10 +32,10 @@ __device__ unsigned long long* g_stamps;
         __builtin_amdgcn_sched_barrier(0);                                               \
         unsigned long long t_;                                                           \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
-        if (lane == 0) g_stamps[(int64_t)blockIdx.x * 16 + (i)] = t_;                    \
-        if (lane == 0 && ((i) == 0 || (i) == 6))                                         \
-            g_stamps[(int64_t)blockIdx.x * 16 + 8 + (i) / 6] =                           \
-                __builtin_amdgcn_s_memrealtime();                                        \
+        const int64_t sw_ = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); \
+        if ((threadIdx.x & 63) == 0) g_stamps[sw_ * 16 + (i)] = t_;                      \
+        if ((threadIdx.x & 63) == 0 && ((i) == 0 || (i) == 6))                           \
+            g_stamps[sw_ * 16 + 8 + (i) / 6] = __builtin_amdgcn_s_memrealtime();         \
         __builtin_amdgcn_sched_barrier(0);                                               \
     } while (0)
 #else
@@ -453,8 +453,8 @@ __device__ __forceinline__ int gshfl(int v, int src, int lane) {
 // rollout of a.steps steps (drl_rollout) with the state kept on chip between
 // them -- ground in LDS, drone records in the scratch area (O order) and the
 // MT index in a register -- and written back once at the end; the actions of
-// step t+1 are loaded during step t.
-template <int P, class GEO, bool ROLL>
+// step t+1 are loaded during step t.  NT: streaming observation stores.
+template <int P, class GEO, bool ROLL, bool NT>
 __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     using GMask = typename GMaskT<P>::type;
     constexpr int GPW = 64 / P;
@@ -807,7 +807,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
 
     DRL_STAMP(4);
 #ifdef DRL_STAMPS
-    if (lane == 0) g_stamps[(int64_t)blockIdx.x * 16 + 7] = __builtin_amdgcn_readfirstlane(rounds_w);
+    if (lane == 0) g_stamps[((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + 7] = __builtin_amdgcn_readfirstlane(rounds_w);
 #endif
     // ---- _pick_packets_after_respawn (env.py:217-224): distinct cells, parallel
     if (active && pos < 0) pos = 0;  // unreachable for valid params (respawn always finds a cell)
@@ -847,7 +847,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         if (active) paint_windows(W.paint + grp * g.lds_paint(), posidx, (int)py, (int)px,
                                   (uint8_t)((c + 1) | (carry << 7)), g);
         wave_sync();
-        write_obs_wave<ROLL>(a.obs + t * a.obs_tstride + wenv0 * (int64_t)(6u * g.env_cells()), nenv_w, g, W,
+        write_obs_wave<NT>(a.obs + t * a.obs_tstride + wenv0 * (int64_t)(6u * g.env_cells()), nenv_w, g, W,
                              a.obs_wide, lane);
     }
     DRL_STAMP(6);
@@ -869,17 +869,18 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
 // One wave per batch of GPW envs.  (Persistent waves looping over 2-4 batches
 // were measured slower at C3/C4/C5: halving the resident waves costs more
 // latency hiding than the longer waves gain in balance.)
-template <int P, class GEO>
+// NT: streaming observation stores (DRL_STEP_OBS_STREAM).
+template <int P, class GEO, bool NT>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : 1, 8)))
 drl_step_kernel(StepArgs a) {
-    step_batch<P, GEO, false>(a, (int64_t)blockIdx.x * (64 / P));
+    step_batch<P, GEO, false, NT>(a, (int64_t)blockIdx.x * (64 / P));
 }
 
 // drl_rollout: a.steps steps per launch, same wave layout.
 template <int P, class GEO>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : 1, 8)))
 drl_rollout_kernel(StepArgs a) {
-    step_batch<P, GEO, true>(a, (int64_t)blockIdx.x * (64 / P));
+    step_batch<P, GEO, true, true>(a, (int64_t)blockIdx.x * (64 / P));
 }
 
 // ------------------------------------------------------------ observation ---
@@ -1506,8 +1507,10 @@ static hipError_t launch_step_t(const StepArgs& a, hipStream_t s, int mode) {
         else return hipErrorInvalidValue;
     } else if (mode == kRolloutMode) {
         hipLaunchKernelGGL((drl_rollout_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
+    } else if (GEO::kObs && a.obs && a.obs_nt) {
+        hipLaunchKernelGGL((drl_step_kernel<P, GEO, GEO::kObs>), grid, block, a.wave_lds, s, a);
     } else {
-        hipLaunchKernelGGL((drl_step_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
+        hipLaunchKernelGGL((drl_step_kernel<P, GEO, false>), grid, block, a.wave_lds, s, a);
     }
     return hipGetLastError();
 }

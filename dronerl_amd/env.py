@@ -17,7 +17,8 @@ from typing import Optional
 
 import torch
 
-from ._native import DRL_ERR_BAD_ACTION, DRL_ERR_NO_FREE_CELL, DRL_MT_WORDS, DroneRLError, DrlState, check, lib
+from ._native import (DRL_ERR_BAD_ACTION, DRL_ERR_NO_FREE_CELL, DRL_MT_WORDS, DRL_STEP_OBS_STREAM, DroneRLError,
+                      DrlState, check, lib)
 from .params import EnvParams
 
 
@@ -109,12 +110,14 @@ class BatchedDeliveryDrones:
         return self.state
 
     def step(self, actions: torch.Tensor, obs_k: int = 0, rewards: Optional[torch.Tensor] = None,
-             dones: Optional[torch.Tensor] = None, obs: Optional[torch.Tensor] = None):
+             dones: Optional[torch.Tensor] = None, obs: Optional[torch.Tensor] = None, obs_stream: bool = False):
         """env.py:112-215 for every env.  actions int32 [E, N] by drone index.
 
         Returns (rewards f32 [E,N], dones bool-as-uint8 [E,N]) and, when
         obs_k > 0, the fused observation f32 [E, obs_k, W, W, 6] of drone
         indices 0..obs_k-1 after the step (train_jax.py:55-56 uses obs_k=1).
+        obs_stream: write the observation with streaming stores
+        (DRL_STEP_OBS_STREAM), for observations no kernel reads right away.
         """
         E, N = self.num_envs, self.n_drones
         actions = self._check(actions, torch.int32, (E, N), "actions")
@@ -126,9 +129,10 @@ class BatchedDeliveryDrones:
             W = self.layout.obs_window
             obs = torch.empty((E, obs_k, W, W, 6), dtype=torch.float32, device=self.device)
         s = self.state.c()
-        check(lib().drl_step(ctypes.byref(self._cp), ctypes.byref(s), _ptr(actions), _ptr(rewards), _ptr(dones),
-                             _ptr(obs) if obs_k else None, int(obs_k), _ptr(self.err), _stream(self.device)),
-              "drl_step")
+        flags = DRL_STEP_OBS_STREAM if obs_stream else 0
+        check(lib().drl_step_ex(ctypes.byref(self._cp), ctypes.byref(s), _ptr(actions), _ptr(rewards), _ptr(dones),
+                                _ptr(obs) if obs_k else None, int(obs_k), _ptr(self.err), flags,
+                                _stream(self.device)), "drl_step")
         if obs_k:
             return rewards, dones, obs
         return rewards, dones

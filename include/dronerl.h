@@ -136,6 +136,16 @@ int drl_reset(const drl_params* p, const drl_state* s, int32_t reseed, uint64_t 
 int drl_step(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
              uint8_t* d_dones, float* d_obs, int32_t obs_k, int32_t* d_err, hipStream_t stream);
 
+/* drl_step with flags (drl_step == drl_step_ex with flags 0).
+ * DRL_STEP_OBS_STREAM: write the observation with streaming (non-temporal)
+ * stores, for observations no kernel reads right away (rollout output).
+ * Without it the stores are cached, so a consumer launched next (the policy's
+ * act) reads them from the caches.  Results are identical either way. */
+#define DRL_STEP_OBS_STREAM 1u
+int drl_step_ex(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
+                uint8_t* d_dones, float* d_obs, int32_t obs_k, int32_t* d_err, uint32_t flags,
+                hipStream_t stream);
+
 /* num_steps steps in one launch (jax_impl run_steps, env/env.py:252-272, with
  * the rewards, dones and observation of every step): identical results to
  * num_steps drl_step calls.  Step t reads d_actions + t * act_step_stride and

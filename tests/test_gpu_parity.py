@@ -237,6 +237,24 @@ def test_ragged_num_envs(E, k):
     np.testing.assert_array_equal(env.get_obs(k).cpu().numpy(), o.obs(3, k))
 
 
+@pytest.mark.parametrize("cfg,E", [(dict(n_drones=8, grid_size=16), 4096), (dict(n_drones=8, grid_size=16), 65),
+                                   (dict(n_drones=16, grid_size=32), 300), (dict(n_drones=6, grid_size=11), 129)])
+def test_streaming_obs_stores(cfg, E):
+    """drl_step_ex(DRL_STEP_OBS_STREAM): identical observation, rewards and
+    state to the cached-store step, step after step."""
+    p = EnvParams(**cfg)
+    envs = [Env(p, E), Env(p, E)]
+    for env in envs:
+        env.reset(seed=21)
+    for t in range(1, 31):
+        a = envs[0].synth_actions(seed=8, step=t)
+        out = [env.step(a, obs_k=1, obs_stream=s) for env, s in zip(envs, (False, True))]
+        for x, y in zip(out[0], out[1]):
+            assert torch.equal(x, y), f"step {t}"
+    assert_state(gpu_state(envs[1]), gpu_state(envs[0]), "streaming vs cached")
+    envs[1].check_errors()
+
+
 @pytest.mark.parametrize("radius", [1, 2, 3, 4, 5, 8])
 @pytest.mark.parametrize("k", [1, 3, 8])
 def test_obs_variants(radius, k):

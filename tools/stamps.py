@@ -21,11 +21,11 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 
-def build_stamps_lib():
+def build_stamps_lib(flags=(), tag=""):
     from dronerl_amd import build as b
-    out = os.path.join(REPO, "dronerl_amd", "libdronerl_stamps.so")
+    out = os.path.join(REPO, "dronerl_amd", f"libdronerl_stamps{tag}.so")
     cmd = [b.hipcc(), f"--offload-arch={b.ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DDRL_STAMPS",
-           "-I", os.path.join(REPO, "include"), "-o", out] + b.SOURCES
+           "-I", os.path.join(REPO, "include"), "-o", out] + list(flags) + b.SOURCES
     subprocess.run(cmd, check=True)
     return out
 
@@ -36,8 +36,19 @@ def main():
     ap.add_argument("--envs", type=int, default=0)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--obs", type=int, default=1)
+    ap.add_argument("--flags", default="", help="extra compile flags, comma separated")
+    ap.add_argument("--tag", default="", help="library name suffix")
+    ap.add_argument("--build-only", action="store_true", help="build the stamps library here and exit")
+    ap.add_argument("--prebuilt", action="store_true", help="use the library --build-only made")
     args = ap.parse_args()
-    path = build_stamps_lib()
+    flags = [f for f in args.flags.split(",") if f]
+    if args.prebuilt:
+        path = os.path.join(REPO, "dronerl_amd", f"libdronerl_stamps{args.tag}.so")
+    else:
+        path = build_stamps_lib(flags, args.tag)
+    if args.build_only:
+        print(path)
+        return
     import dronerl_amd._native as nat
     nat.LIB_PATH = path
     L = nat.lib()
