@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdronerl.so")
+# DRL_LIB: an alternative build of the same library (tools/variants.py A/B runs)
+LIB_PATH = os.environ.get("DRL_LIB") or os.path.join(_HERE, "libdronerl.so")
 
 DRL_MT_WORDS = 640
 DRL_MAX_DRONES = 64

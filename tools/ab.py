@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--lib", default="", help="alternative library (tools/variants.py build)")
     ap.add_argument("--variants", default="spec1,spec0,spec1_noobs,spec0_noobs",
-                    help="comma list; each: specN[_noobs][_wide0|_wide1]")
+                    help="comma list; each: specN[_noobs][_wide0|_wide1][_nt1]")
     args = ap.parse_args()
     if args.lib:
         import dronerl_amd._native as nat
@@ -64,8 +64,9 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
             e0.record()
+            flags = 1 if "nt1" in parts else 0  # DRL_STEP_OBS_STREAM
             for t in range(T):
-                L.drl_step(cp, sp, ap_[t], rp, dp, o, k, None, s)
+                L.drl_step_ex(cp, sp, ap_[t], rp, dp, o, k, None, flags, s)
             e1.record()
             torch.cuda.synchronize()
             if r:
