@@ -234,47 +234,101 @@ def rollout_bench(env, actions, K, warmup_steps, steps, chunk: int, R: int, Wb: 
                                  "read and written once per launch, so HBM traffic per step is lower"}}
 
 
-def train_loop_bench(env, reps: int, seg: int = 100):
-    """SURVEY.md §8 D2 (C5 shape: "multi-step loop, hipGraph of step+obs+act")
-    and train_jax.py:38-113 minus the learner: per step, synthetic actions for
-    every drone, epsilon-greedy DQN action for drone 0 (dense 294->128->64->5),
-    step + obs(K=1), replay add_many of the drone-0 transition; after `seg`
-    steps a reset of every env (reset_env_every, train_jax.py:101-113) and its
-    first observation.  One segment is captured once as a HIP graph (no host
-    work per step) and replayed.  Counters (action stream step, epsilon draws,
-    replay cursor) are baked into the capture, so replays repeat them: the
-    work per step is the same, the action stream repeats every segment."""
-    from dronerl_amd.dqn import QNetwork, ReplayBuffer
-    E, N, dev = env.num_envs, env.n_drones, env.device
-    W = env.layout.obs_window
-    D = W * W * 6
-    net = QNetwork(D, (128, 64), device=dev, generator=torch.Generator().manual_seed(0))
-    rb = ReplayBuffer(10000, D, dev)
-    acts = torch.empty((E, N), dtype=torch.int32, device=dev)
-    rewards = torch.empty((E, N), dtype=torch.float32, device=dev)
-    dones = torch.empty((E, N), dtype=torch.uint8, device=dev)
-    bufs = [torch.empty((E, 1, W, W, 6), dtype=torch.float32, device=dev) for _ in range(2)]
-    env.get_obs(1, out=bufs[0])
+class TrainSegment:
+    """One segment of the train_jax.py:38-113 loop minus the learner (SURVEY.md
+    §8 D2; C5: "multi-step loop, hipGraph of step+obs+act"): per step,
+    synthetic actions for every drone, the epsilon-greedy DQN action for drone
+    0 (dense 294->128->64->5), step + obs(K=1), replay add_many of the drone-0
+    transition; after `seg` steps a reset of every env (reset_env_every,
+    train_jax.py:101-113) and its first observation.
 
-    def segment():
-        for t in range(seg):
-            cur, nxt = bufs[t & 1], bufs[(t + 1) & 1]
-            env.synth_actions(seed=2024, step=t, out=acts)
-            net.act(cur.reshape(E, -1), 0.1, seed=7, step=t, actions=acts)
-            env.step(acts, obs_k=1, rewards=rewards, dones=dones, obs=nxt)
-            rb.add_many(cur, acts, rewards, nxt, dones)
-        env.reset(seed=None)
-        env.get_obs(1, out=bufs[seg & 1])
+    parallel=True: the synthetic actions and the replay add run on two side
+    streams, joined to the act -> step chain by events.  Observations, actions,
+    rewards and dones rotate through 3 buffers, so step t only waits for the
+    replay add of step t-2 and the actions of step t are drawn while step t-1
+    runs.  parallel=False issues the same calls in the same order on one
+    stream; both leave identical state and replay contents
+    (tests/test_gpu_parity.py::test_train_segment_parallel_matches_serial)."""
 
+    NB = 3
+
+    def __init__(self, env, seg: int, parallel: bool = False, net=None, rb=None):
+        from dronerl_amd.dqn import QNetwork, ReplayBuffer
+        E, N, dev = env.num_envs, env.n_drones, env.device
+        W = env.layout.obs_window
+        D = W * W * 6
+        self.env, self.seg, self.parallel, self.E = env, seg, parallel, E
+        self.net = net or QNetwork(D, (128, 64), device=dev, generator=torch.Generator().manual_seed(0))
+        self.rb = rb or ReplayBuffer(10000, D, dev)
+        self.acts = [torch.empty((E, N), dtype=torch.int32, device=dev) for _ in range(self.NB)]
+        self.rewards = [torch.empty((E, N), dtype=torch.float32, device=dev) for _ in range(self.NB)]
+        self.dones = [torch.empty((E, N), dtype=torch.uint8, device=dev) for _ in range(self.NB)]
+        self.obs = [torch.empty((E, 1, W, W, 6), dtype=torch.float32, device=dev) for _ in range(self.NB)]
+        env.get_obs(1, out=self.obs[0])
+        self.s_syn, self.s_rep = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def _synth(self, t):
+        self.env.synth_actions(seed=2024, step=t, out=self.acts[t % self.NB])
+
+    def _act_step(self, t):
+        b, nb = t % self.NB, (t + 1) % self.NB
+        self.net.act(self.obs[b].reshape(self.E, -1), 0.1, seed=7, step=t, actions=self.acts[b])
+        self.env.step(self.acts[b], obs_k=1, rewards=self.rewards[b], dones=self.dones[b], obs=self.obs[nb])
+
+    def _replay(self, t):
+        b, nb = t % self.NB, (t + 1) % self.NB
+        self.rb.add_many(self.obs[b], self.acts[b], self.rewards[b], self.obs[nb], self.dones[b])
+
+    def run(self):
+        main = torch.cuda.current_stream(self.env.device)
+        if not self.parallel:
+            for t in range(self.seg):
+                self._synth(t)
+                self._act_step(t)
+                self._replay(t)
+        else:
+            ev_syn = [torch.cuda.Event() for _ in range(self.seg)]
+            ev_step = [torch.cuda.Event() for _ in range(self.seg)]
+            ev_rep = [torch.cuda.Event() for _ in range(self.seg)]
+            self.s_syn.wait_stream(main)
+            self.s_rep.wait_stream(main)
+            for t in range(self.seg):
+                with torch.cuda.stream(self.s_syn):
+                    if t >= self.NB:  # acts[t % 3] was last read by the replay add of step t-3
+                        self.s_syn.wait_event(ev_rep[t - self.NB])
+                    self._synth(t)
+                    ev_syn[t].record(self.s_syn)
+                main.wait_event(ev_syn[t])
+                if t >= 2:  # step t overwrites obs[(t+1) % 3], read by the replay add of step t-2
+                    main.wait_event(ev_rep[t - 2])
+                self._act_step(t)
+                ev_step[t].record(main)
+                with torch.cuda.stream(self.s_rep):
+                    self.s_rep.wait_event(ev_step[t])
+                    self._replay(t)
+                    ev_rep[t].record(self.s_rep)
+            main.wait_stream(self.s_syn)
+            main.wait_stream(self.s_rep)
+        self.env.reset(seed=None)
+        self.env.get_obs(1, out=self.obs[0])
+
+
+def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False):
+    """TrainSegment captured once as a HIP graph (no host work per step) and
+    replayed.  Counters (action stream step, epsilon draws, replay cursor) are
+    baked into the capture, so replays repeat them: the work per step is the
+    same, the action stream repeats every segment."""
+    dev = env.device
+    loop = TrainSegment(env, seg, parallel=parallel)
     side = torch.cuda.Stream(dev)
     side.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(side):
-        segment()  # eager warm-up on the capture stream
+        loop.run()  # eager warm-up on the capture stream
     torch.cuda.current_stream(dev).wait_stream(side)
     torch.cuda.synchronize(dev)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-        segment()
+        loop.run()
     g.replay()
     torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -285,10 +339,13 @@ def train_loop_bench(env, reps: int, seg: int = 100):
     torch.cuda.synchronize(dev)
     env.check_errors()
     dt = e0.elapsed_time(e1) / 1e3
+    E = env.num_envs
+    branches = ("synthetic actions and replay add_many on parallel graph branches, 3 rotating buffers"
+                if parallel else "one stream")
     return {"env_steps_per_s": E * seg * reps / dt, "us_per_step": dt / (seg * reps) * 1e6,
             "segments": reps, "steps_per_segment": seg,
             "loop": f"hipGraph of {seg} x [synth actions -> qnet act (drone 0) -> step + obs(K=1) -> "
-                    f"replay add_many] + reset + obs, replayed {reps}x (learner not included)"}
+                    f"replay add_many] + reset + obs, replayed {reps}x ({branches}; learner not included)"}
 
 
 def main():
@@ -306,6 +363,9 @@ def main():
                     help="steps per drl_rollout launch for the rollout measurement (0 = skip)")
     ap.add_argument("--loop-segments", type=int, default=3,
                     help="train-loop graph replays (100 steps + reset each; 0 = skip)")
+    ap.add_argument("--parallel-loop", action="store_true",
+                    help="train loop with synth / replay on parallel graph branches (measured slower: the step "
+                         "kernel fills every CU in one generation, and co-running kernels delay its waves)")
     ap.add_argument("--obs-cached", action="store_true",
                     help="write the per-step observation with cached stores (default: streaming, DRL_STEP_OBS_STREAM)")
     ap.add_argument("--obs-k", type=int, default=-1,
@@ -418,7 +478,7 @@ def main():
 
     loop = None
     if args.loop_segments > 0 and not args.no_dqn and K >= 1:
-        loop = train_loop_bench(env, args.loop_segments)
+        loop = train_loop_bench(env, args.loop_segments, parallel=args.parallel_loop)
         loop["env_steps_per_s"] = min_over_ranks(loop["env_steps_per_s"], world) * world
         loop["n_gpus"] = world
 

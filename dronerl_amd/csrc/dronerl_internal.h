@@ -40,13 +40,17 @@ constexpr int nchg(int n_drones) { return 6 * n_drones + 2; }                  /
 constexpr int chg_bytes(int n_drones) { return r16(2 * nchg(n_drones)); }
 constexpr int bit_length(int v) { return v ? 1 + bit_length(v >> 1) : 0; }
 #ifndef DRL_QN_RING
-#define DRL_QN_RING 5
+#define DRL_QN_RING 2
 #endif
 #ifndef DRL_QN_WAVES
 #define DRL_QN_WAVES 8
 #endif
 constexpr int qn_ring = DRL_QN_RING;    // act kernel: K-slices in flight per wave (layer-0 slices padded to a multiple)
 constexpr int qn_waves = DRL_QN_WAVES;  // act kernel: waves per workgroup (one workgroup per CU)
+#ifndef DRL_QN_TILES
+#define DRL_QN_TILES 2
+#endif
+constexpr int qn_tiles = DRL_QN_TILES;  // act kernel: 16-env tiles per pass sharing each weight fragment
 constexpr int fy_buckets = 256;                                   // reset: j-hash buckets (x2 hashes)
 constexpr int fy_table_bytes = (2 * fy_buckets + 64) * 4;        // ... + the 64 i slots, u32 each
 }  // namespace lay

@@ -81,6 +81,7 @@ __global__ void drl_qnet_pack_kernel(QnetPack p) {
 constexpr int QN_WAVES = lay::qn_waves;
 constexpr int QN_MAXT = 8;    // 16-unit tiles per hidden layer (hidden <= 128)
 constexpr int QN_RING = lay::qn_ring;  // K-slices in flight per wave
+constexpr int QN_TILES = lay::qn_tiles;  // env tiles per pass sharing each weight fragment
 
 __device__ __forceinline__ bf16x8 lds_frag(const uint4* base, int frag, int lane) {
     const uint4 v = base[frag * 64 + lane];
@@ -89,17 +90,21 @@ __device__ __forceinline__ bf16x8 lds_frag(const uint4* base, int frag, int lane
     return f;
 }
 
+// TP env tiles per pass share every weight fragment read from LDS (TP MFMAs per
+// fragment): a wave's pass covers TP*16 envs.
 template <int NT0>
 __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_kernel(QnetArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint4 wl[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int c = lane & 15, g = lane >> 4;
     constexpr int nt0 = NT0;  // first-layer tiles (compile time: no branches around its MFMAs)
+    constexpr int TP = QN_TILES;
     const int64_t ntiles = (a.E + 15) / 16;
-    const int64_t tstride = (int64_t)gridDim.x * QN_WAVES;
+    const int64_t ngroups = (ntiles + TP - 1) / TP;
+    const int64_t gstride = (int64_t)gridDim.x * QN_WAVES;
     const int KP = a.kt0;                 // padded to a multiple of QN_RING
     const int rounds = KP / QN_RING;
-    float raw[QN_RING][8];
+    float raw[TP][QN_RING][8];
     // slice t (features 32t + frag_k(g, 0..7)) of the env row at byte offset
     // `rowb` from obs: two 16-B loads; the four lanes of the env cover 64
     // contiguous bytes per load (rows are 8-B aligned at 294 floats: gfx950
@@ -126,12 +131,16 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_kernel(QnetArgs a)
         const int64_t env = t * 16 + c;
         return (uint32_t)((env < a.E ? env : a.E - 1) * a.obs_stride * 4);
     };
-    int64_t tile = (int64_t)blockIdx.x * QN_WAVES + wave;
-    uint32_t row = row_of(tile < ntiles ? tile : 0);
+    int64_t grp = (int64_t)blockIdx.x * QN_WAVES + wave;
+    uint32_t row[TP];
+#pragma unroll
+    for (int h = 0; h < TP; ++h) row[h] = row_of(TP * (grp < ngroups ? grp : 0) + h);
     // ---- the first ring of slices, then the packed net by LDS-DMA (no
     // registers; every 16-B piece in flight at once)
 #pragma unroll
-    for (int i = 0; i < QN_RING; ++i) load_slice(row, i, raw[i]);
+    for (int i = 0; i < QN_RING; ++i)
+#pragma unroll
+        for (int h = 0; h < TP; ++h) load_slice(row[h], i, raw[h][i]);
     for (int v0 = wave * 64; v0 < a.lds_vec; v0 += 64 * QN_WAVES)
         if (v0 + lane < a.lds_vec)
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(a.packed + v0 + lane),
@@ -141,66 +150,85 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_kernel(QnetArgs a)
     const float* bias = reinterpret_cast<const float*>(wl + a.frag_total);
     const uint4* W0 = wl + a.frag_off[0];
 
-    for (; tile < ntiles; tile += tstride) {
-        const int64_t ntile = tile + tstride;
-        const uint32_t nrow = row_of(ntile < ntiles ? ntile : tile);
-        f32x4 acc[QN_MAXT];
+    for (; grp < ngroups; grp += gstride) {
+        const int64_t ngrp = grp + gstride;
+        uint32_t nrow[TP];
 #pragma unroll
-        for (int m = 0; m < QN_MAXT; ++m) acc[m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int h = 0; h < TP; ++h) nrow[h] = row_of(TP * (ngrp < ngroups ? ngrp : grp) + h);
+        f32x4 acc[TP][QN_MAXT];
+#pragma unroll
+        for (int h = 0; h < TP; ++h)
+#pragma unroll
+            for (int m = 0; m < QN_MAXT; ++m) acc[h][m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         // ---- layer 0 over the ring.  Refill mode per round (compile time):
-        // 0 = slice t + RING of this tile (all rounds but the last), 1 = of the
-        // next tile, 2 = none (this wave's last tile)
+        // 0 = slice t + RING of this group (all rounds but the last), 1 = of
+        // the next group, 2 = none (this wave's last group)
         auto round = [&](int rd, auto mode) {
             constexpr int MODE = decltype(mode)::value;
 #pragma unroll
             for (int i = 0; i < QN_RING; ++i) {
                 const int t = rd * QN_RING + i;
-                bf16x8 b;
+                bf16x8 b[TP];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) b[j] = (__bf16)raw[i][j];
-                if constexpr (MODE == 0) load_slice(row, t + QN_RING, raw[i]);
-                else if constexpr (MODE == 1) load_slice(nrow, t + QN_RING - KP, raw[i]);
+                for (int h = 0; h < TP; ++h) {
 #pragma unroll
-                for (int m = 0; m < nt0; ++m)
-                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_frag(W0, m * KP + t, lane), b, acc[m], 0, 0, 0);
+                    for (int j = 0; j < 8; ++j) b[h][j] = (__bf16)raw[h][i][j];
+                    if constexpr (MODE == 0) load_slice(row[h], t + QN_RING, raw[h][i]);
+                    else if constexpr (MODE == 1) load_slice(nrow[h], t + QN_RING - KP, raw[h][i]);
+                }
+#pragma unroll
+                for (int m = 0; m < nt0; ++m) {
+                    const bf16x8 w = lds_frag(W0, m * KP + t, lane);
+#pragma unroll
+                    for (int h = 0; h < TP; ++h) acc[h][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, b[h], acc[h][m], 0, 0, 0);
+                }
                 __builtin_amdgcn_sched_barrier(0);  // A reads next to their MFMAs (register pressure)
             }
         };
         for (int rd = 0; rd + 1 < rounds; ++rd) round(rd, std::integral_constant<int, 0>{});
-        if (ntile < ntiles) round(rounds - 1, std::integral_constant<int, 1>{});
+        if (ngrp < ngroups) round(rounds - 1, std::integral_constant<int, 1>{});
         else round(rounds - 1, std::integral_constant<int, 2>{});
-        const int64_t env = tile * 16 + c;
-        row = nrow;
+#pragma unroll
+        for (int h = 0; h < TP; ++h) row[h] = nrow[h];
         // ---- hidden layers 1..n_hidden-1 and the output layer: B operands in registers
         int nt_prev = nt0;
         const float* bprev = bias + a.bias_off[0];
         for (int l = 1; l <= a.n_hidden; ++l) {
             // activation (bias + ReLU) of the previous layer as bf16 B fragments:
             // K-slice s = registers of tiles 2s (j < 4) and 2s + 1 (j >= 4)
-            bf16x8 bf[QN_MAXT / 2];
+            bf16x8 bf[TP][QN_MAXT / 2];
 #pragma unroll
-            for (int s = 0; s < QN_MAXT / 2; ++s) {
-                if (2 * s < nt_prev) {
+            for (int h = 0; h < TP; ++h) {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const int m = 2 * s + (j >> 2), i = j & 3;
-                        bf[s][j] = (__bf16)fmaxf(acc[m][i] + bprev[16 * m + 4 * g + i], 0.0f);
+                for (int s2 = 0; s2 < QN_MAXT / 2; ++s2) {
+                    if (2 * s2 < nt_prev) {
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const int m = 2 * s2 + (j >> 2), i = j & 3;
+                            bf[h][s2][j] = (__bf16)fmaxf(acc[h][m][i] + bprev[16 * m + 4 * g + i], 0.0f);
+                        }
                     }
                 }
             }
             const int nt_l = (l < a.n_hidden) ? a.nt[l] : 1;  // output layer: one tile (<= 16 actions)
             const int kt = nt_prev / 2;
 #pragma unroll
-            for (int m = 0; m < QN_MAXT; ++m) acc[m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            for (int h = 0; h < TP; ++h)
+#pragma unroll
+                for (int m = 0; m < QN_MAXT; ++m) acc[h][m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
             const uint4* Wl = wl + a.frag_off[l];
 #pragma unroll
             for (int t = 0; t < QN_MAXT / 2; ++t) {
                 if (t < kt) {
 #pragma unroll
-                    for (int m = 0; m < QN_MAXT; ++m)
-                        if (m < nt_l)
-                            acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_frag(Wl, m * kt + t, lane), bf[t],
-                                                                            acc[m], 0, 0, 0);
+                    for (int m = 0; m < QN_MAXT; ++m) {
+                        if (m < nt_l) {
+                            const bf16x8 w = lds_frag(Wl, m * kt + t, lane);
+#pragma unroll
+                            for (int h = 0; h < TP; ++h)
+                                acc[h][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, bf[h][t], acc[h][m], 0, 0, 0);
+                        }
+                    }
                 }
             }
             nt_prev = nt_l;
@@ -208,24 +236,28 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_kernel(QnetArgs a)
         }
         // ---- Q values: actions 0..3 in registers 0..3 of the g = 0 lanes,
         // 4..7 in those of the g = 1 lanes (column = env)
-        float q[8];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float own = acc[0][i] + bprev[4 * g + i];
-            const float hi = __shfl(own, c + 16);  // g = 1 lane of this env
-            q[i] = own;
-            q[i + 4] = hi;
-        }
-        if (g == 0 && env < a.E) {
-            int best = 0;  // jnp.argmax: first maximum
-            for (int i = 1; i < a.n_actions; ++i) best = q[i] > q[best] ? i : best;
-            const uint64_t ge = (uint64_t)(a.env_offset + env);
-            const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (ge << 8) ^ 0xa5ull));
-            const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
-            const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
-            a.actions[env * a.action_stride] = (u < a.epsilon) ? rnd : best;
-            if (a.q)
-                for (int i = 0; i < a.n_actions; ++i) a.q[env * a.n_actions + i] = q[i];
+        for (int h = 0; h < TP; ++h) {
+            float q[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float own = acc[h][0][i] + bprev[4 * g + i];
+                const float hi = __shfl(own, c + 16);  // g = 1 lane of this env
+                q[i] = own;
+                q[i + 4] = hi;
+            }
+            const int64_t env = (TP * grp + h) * 16 + c;
+            if (g == 0 && env < a.E) {
+                int best = 0;  // jnp.argmax: first maximum
+                for (int i = 1; i < a.n_actions; ++i) best = q[i] > q[best] ? i : best;
+                const uint64_t ge = (uint64_t)(a.env_offset + env);
+                const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (ge << 8) ^ 0xa5ull));
+                const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
+                const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
+                a.actions[env * a.action_stride] = (u < a.epsilon) ? rnd : best;
+                if (a.q)
+                    for (int i = 0; i < a.n_actions; ++i) a.q[env * a.n_actions + i] = q[i];
+            }
         }
     }
 }
@@ -283,8 +315,8 @@ hipError_t launch_qnet_pack(const QnetPack& p, hipStream_t s) {
 }
 
 hipError_t launch_qnet_act(const QnetArgs& a, int num_cus, hipStream_t s) {
-    const int64_t ntiles = (a.E + 15) / 16;
-    int64_t blocks = (ntiles + QN_WAVES - 1) / QN_WAVES;
+    const int64_t ngroups = ((a.E + 15) / 16 + QN_TILES - 1) / QN_TILES;
+    int64_t blocks = (ngroups + QN_WAVES - 1) / QN_WAVES;
     if (blocks > num_cus) blocks = num_cus;
     const dim3 grid((unsigned)blocks), block(64 * QN_WAVES);
     const size_t lds = (size_t)a.lds_vec * 16;

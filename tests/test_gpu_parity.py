@@ -670,3 +670,28 @@ def test_rollout_last_step_outputs_and_oracle():
     np.testing.assert_array_equal(d.cpu().numpy().astype(bool), do)
     np.testing.assert_array_equal(ob.cpu().numpy(), o.obs(3, 1))
     assert_state(gpu_state(env), o.state(), "rollout final")
+
+
+def test_train_segment_parallel_matches_serial():
+    """bench.TrainSegment: synthetic actions and replay add_many on parallel
+    stream branches (3 rotating buffers) leave the same env state, replay
+    buffer and next observation as the same calls on one stream."""
+    from bench import TrainSegment
+    p = EnvParams(n_drones=8, grid_size=16)
+    E, seg = 3000, 13
+    runs = []
+    for parallel in (False, True):
+        env = Env(p, E)
+        env.reset(seed=5)
+        loop = TrainSegment(env, seg, parallel=parallel)
+        loop.run()
+        loop.run()
+        torch.cuda.synchronize()
+        env.check_errors()
+        runs.append((gpu_state(env), loop))
+    (g0, l0), (g1, l1) = runs
+    assert_state(g1, g0, "parallel vs serial segments")
+    for k in ("obs", "next_obs", "actions", "rewards", "dones"):
+        assert torch.equal(getattr(l0.rb, k), getattr(l1.rb, k)), k
+    assert l0.rb.cursor == l1.rb.cursor
+    assert torch.equal(l0.obs[0], l1.obs[0])
