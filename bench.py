@@ -247,10 +247,8 @@ class TrainSegment:
     rewards and dones rotate through 3 buffers, so step t only waits for the
     replay add of step t-2 and the actions of step t are drawn while step t-1
     runs.  parallel=False issues the same calls in the same order on one
-    stream; both leave identical state and replay contents
+    stream with 2 buffers; both leave identical state and replay contents
     (tests/test_gpu_parity.py::test_train_segment_parallel_matches_serial)."""
-
-    NB = 3
 
     def __init__(self, env, seg: int, parallel: bool = False, net=None, rb=None):
         from dronerl_amd.dqn import QNetwork, ReplayBuffer
@@ -258,6 +256,10 @@ class TrainSegment:
         W = env.layout.obs_window
         D = W * W * 6
         self.env, self.seg, self.parallel, self.E = env, seg, parallel, E
+        # parallel branches need 3 rotating buffers (see above); on one stream 2
+        # suffice, and the third 77 MB observation buffer costs MALL hits (C3
+        # loop 79.4 vs 74.4 us per step)
+        self.NB = 3 if parallel else 2
         self.net = net or QNetwork(D, (128, 64), device=dev, generator=torch.Generator().manual_seed(0))
         self.rb = rb or ReplayBuffer(10000, D, dev)
         self.acts = [torch.empty((E, N), dtype=torch.int32, device=dev) for _ in range(self.NB)]
