@@ -10,6 +10,10 @@ namespace drl {
 constexpr int MT_N = 624;
 constexpr int MT_M = 397;
 constexpr int MT_WORDS = DRL_MT_WORDS;
+// DRL_DPP8: P = 8 / 16 claim and crash-order scans by DPP lane swaps instead of ds_bpermute
+#ifndef DRL_DPP8
+#define DRL_DPP8 1
+#endif
 // respawn rounds: D draws per lane (D*P MT outputs per round); the first
 // round's words (>= 16) are prefetched into LDS with the step's other loads
 // (tuning knobs for tools/ab.py builds: DRL_DRAWS_P<P> overrides one width)

@@ -443,6 +443,33 @@ __device__ __forceinline__ int gshfl(int v, int src, int lane) {
 #endif
 }
 
+// Value of lane (lane ^ K) within each 8-lane group, K = 1..7, by DPP (no LDS
+// round trip): quad_perm for K = 1, 2, 3, row_half_mirror (lane i <- 7 - i =
+// i ^ 7) for K = 7, and half_mirror after quad_perm(K ^ 7) for K = 4, 5, 6.
+template <int K>
+__device__ __forceinline__ int xor_lane8(int v) {
+    if constexpr (K == 1) return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);       // [1,0,3,2]
+    else if constexpr (K == 2) return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false);  // [2,3,0,1]
+    else if constexpr (K == 3) return __builtin_amdgcn_update_dpp(0, v, 0x1B, 0xf, 0xf, false);  // [3,2,1,0]
+    else if constexpr (K == 7) return __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false);
+    else return __builtin_amdgcn_update_dpp(0, xor_lane8<K ^ 7>(v), 0x141, 0xf, 0xf, false);
+}
+// ... within each 16-lane row, K = 1..15: row_mirror (lane i <- 15 - i = i ^ 15)
+// after xor_lane8<K ^ 15> for K >= 8.
+template <int K>
+__device__ __forceinline__ int xor_lane16(int v) {
+    if constexpr (K < 8) return xor_lane8<K>(v);
+    else return __builtin_amdgcn_update_dpp(0, xor_lane8<K ^ 15>(v), 0x140, 0xf, 0xf, false);
+}
+// f(value of lane j ^ k, k) for k = 1..P-1 within P-lane groups (P = 8 or 16)
+template <int P, int K = 1, class F>
+__device__ __forceinline__ void for_other_lanes(int v, F&& f) {
+    if constexpr (K < P) {
+        f(P == 8 ? xor_lane8<K>(v) : xor_lane16<K>(v), K);
+        for_other_lanes<P, K + 1>(v, f);
+    }
+}
+
 // ------------------------------------------------------------------ step ---
 // One wave per block.  P <= 8 (small grids, LDS <= 5 KB/wave): cap registers
 // at 64 so 8 waves fit a SIMD and every wave of a 65536-env C3 launch is
@@ -572,6 +599,14 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     // later ones crash (list A) and record the cell; OOB crashes (list A).
     bool earlier = false;
     int later_min = P;
+    if constexpr ((P == 8 || P == 16) && DRL_DPP8) {  // the group's other targets by DPP
+        for_other_lanes<P>(tcell, [&](int o, int k) {
+            const int s = j ^ k;
+            const bool same = o == tcell;
+            earlier |= same && s < j;
+            later_min = (same && s > j && s < later_min) ? s : later_min;
+        });
+    } else {
 #pragma unroll
     for (int s0 = 0; s0 < P; s0 += CH) {
         int ts[CH];
@@ -584,6 +619,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
             earlier |= same && s < j;
             later_min = (same && s > j && s < later_min) ? s : later_min;
         }
+    }
     }
     const bool claimer = inb && !earlier;
     const bool crashA = active && !claimer;
@@ -636,6 +672,9 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     int rankB = 0;
     if (__ballot(crashB)) {
         const int bkey = crashB ? (collided ? later_min : P + j) : 4 * P;
+        if constexpr ((P == 8 || P == 16) && DRL_DPP8) {
+            for_other_lanes<P>(bkey, [&](int o, int) { rankB += o < bkey; });
+        } else
 #pragma unroll
         for (int s0 = 0; s0 < P; s0 += CH) {
             int ks[CH];
