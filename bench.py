@@ -517,7 +517,11 @@ def main():
                          "algorithmic_read_bytes_per_env_step": R,
                          "algorithmic_write_bytes_per_env_step": Wb,
                          "achieved_read_plus_write": achieved_rw,
-                         "frac_read_plus_write": achieved_rw / PEAK_HBM_GBS},
+                         "frac_read_plus_write": achieved_rw / PEAK_HBM_GBS,
+                         "note": "frac counts SURVEY.md §8 D3's read bytes R only; its write bytes count a full "
+                                 "ground write-back, but the kernel writes only the changed cells, so the "
+                                 "read+write figure can exceed the peak at large grids (C5); measured HBM bytes "
+                                 "per launch are in traffic"},
             "cpu_baseline": cpu,
             "resets_per_s": resets_per_s,
             "dqn_consumer": dqn,
