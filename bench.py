@@ -46,6 +46,12 @@ def algorithmic_bytes(G: int, N: int, K: int, W: int = 7):
     return R, Wb
 
 
+# DRL_DIST_BACKEND=gloo rehearses the multi-rank path where there are fewer
+# GPUs than ranks (ranks share devices round-robin; the max-over-ranks
+# reductions then run on host tensors).  The driver's runs use nccl (RCCL).
+DIST_BACKEND = os.environ.get("DRL_DIST_BACKEND", "nccl")
+
+
 def dist_init():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -53,8 +59,13 @@ def dist_init():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if DIST_BACKEND == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            local = local % torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group(DIST_BACKEND)
     else:
         torch.cuda.set_device(local)
     return rank, world, local
@@ -70,7 +81,7 @@ def max_over_ranks(v: float, world: int) -> float:
     if world == 1:
         return v
     import torch.distributed as dist
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    t = torch.tensor([v], dtype=torch.float64, device="cuda" if DIST_BACKEND == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
