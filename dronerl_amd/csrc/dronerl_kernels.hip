@@ -5,17 +5,21 @@
 // design: DESIGN.md.  Summary:
 //
 //  drl_step_kernel<P>  one wavefront lane per (env, drone slot); an env owns a
-//      group of P lanes (P = pow2 >= n_drones), 64/P envs per wave, 4 waves
+//      group of P lanes (P = pow2 >= n_drones), 64/P envs per wave, one wave
 //      per block.  Slots are kept in dict order O, so "earlier in O" is "lower
-//      lane".  The env's ground is staged into LDS with 16-B vector copies,
-//      first-comer claims / crash ordering are resolved with __shfl/__ballot,
-//      and the serial respawn section (env.py:186-210) draws P MT outputs per
-//      round in parallel and picks the first accepted (y, x) pair with ballots.
-//      The observation window is written from LDS with 16-B stores.
+//      lane".  The env's ground is staged into LDS by LDS-DMA, first-comer
+//      claims / crash ordering are resolved with DPP lane swaps (8/16-lane
+//      groups) or __shfl, and __ballot, and the serial respawn section
+//      (env.py:186-210) draws D*P MT outputs per round in parallel and places
+//      items from the accepted (y, x) pairs with ballots.  The observation
+//      window is written from LDS with 16-B stores (streaming on request).
+//  drl_rollout_kernel<P>  the same per step, several steps per launch with
+//      the state on chip.
 //  drl_obs_kernel<P>   the same geometry, observation only.
-//  drl_reset_kernel    one lane per env (64-lane blocks): the reset is a long
-//      serial shuffle/sample chain per env (env.py:68-101); the shuffle list
-//      lives in LDS, MT twists are done cooperatively by the whole wave.
+//  drl_reset_wave_kernel  one wavefront per env: MT state in registers,
+//      batched Fisher-Yates shuffles (64 draws per step) over an LDS list.
+//  drl_reset_kernel    one lane per env (the A/B alternative): the shuffle
+//      list lives in LDS, MT twists are done cooperatively by the whole wave.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
