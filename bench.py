@@ -529,10 +529,12 @@ def main():
                          "algorithmic_write_bytes_per_env_step": Wb,
                          "achieved_read_plus_write": achieved_rw,
                          "frac_read_plus_write": achieved_rw / PEAK_HBM_GBS,
-                         "note": "frac counts SURVEY.md §8 D3's read bytes R only; its write bytes count a full "
-                                 "ground write-back, but the kernel writes only the changed cells, so the "
-                                 "read+write figure can exceed the peak at large grids (C5); measured HBM bytes "
-                                 "per launch are in traffic"},
+                         "frac_ceiling": R / (R + Wb),
+                         "note": "frac counts SURVEY.md §8 D3's read bytes R only: moving all R + W "
+                                 "algorithmic bytes at the HBM peak would score frac_ceiling = R / (R + W). W counts "
+                                 "a full ground write-back but the kernel writes only the changed cells, so the "
+                                 "read+write figure can exceed the peak at large grids (C5). Measured HBM bytes "
+                                 "per launch: traffic"},
             "cpu_baseline": cpu,
             "resets_per_s": resets_per_s,
             "dqn_consumer": dqn,
