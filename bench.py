@@ -253,6 +253,10 @@ class TrainSegment:
     transition; after `seg` steps a reset of every env (reset_env_every,
     train_jax.py:101-113) and its first observation.
 
+    fused=True (one stream only): the synthetic actions of drones 1..N-1 are
+    written by the act launch itself (drl_qnet_act_synth), one kernel fewer
+    per step with the same action rows.
+
     parallel=True: the synthetic actions and the replay add run on two side
     streams, joined to the act -> step chain by events.  Observations, actions,
     rewards and dones rotate through 3 buffers, so step t only waits for the
@@ -261,12 +265,13 @@ class TrainSegment:
     stream with 2 buffers; both leave identical state and replay contents
     (tests/test_gpu_parity.py::test_train_segment_parallel_matches_serial)."""
 
-    def __init__(self, env, seg: int, parallel: bool = False, net=None, rb=None):
+    def __init__(self, env, seg: int, parallel: bool = False, net=None, rb=None, fused: bool = True):
         from dronerl_amd.dqn import QNetwork, ReplayBuffer
         E, N, dev = env.num_envs, env.n_drones, env.device
         W = env.layout.obs_window
         D = W * W * 6
         self.env, self.seg, self.parallel, self.E = env, seg, parallel, E
+        self.fused = fused and not parallel
         # parallel branches need 3 rotating buffers (see above); on one stream 2
         # suffice, and the third 77 MB observation buffer costs MALL hits (C3
         # loop 79.4 vs 74.4 us per step)
@@ -285,7 +290,8 @@ class TrainSegment:
 
     def _act_step(self, t):
         b, nb = t % self.NB, (t + 1) % self.NB
-        self.net.act(self.obs[b].reshape(self.E, -1), 0.1, seed=7, step=t, actions=self.acts[b])
+        self.net.act(self.obs[b].reshape(self.E, -1), 0.1, seed=7, step=t, env_offset=self.env.env_offset,
+                     actions=self.acts[b], synth=(2024, t) if self.fused else None)
         self.env.step(self.acts[b], obs_k=1, rewards=self.rewards[b], dones=self.dones[b], obs=self.obs[nb])
 
     def _replay(self, t):
@@ -296,7 +302,8 @@ class TrainSegment:
         main = torch.cuda.current_stream(self.env.device)
         if not self.parallel:
             for t in range(self.seg):
-                self._synth(t)
+                if not self.fused:
+                    self._synth(t)
                 self._act_step(t)
                 self._replay(t)
         else:
@@ -326,13 +333,13 @@ class TrainSegment:
         self.env.get_obs(1, out=self.obs[0])
 
 
-def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False):
+def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fused: bool = True):
     """TrainSegment captured once as a HIP graph (no host work per step) and
     replayed.  Counters (action stream step, epsilon draws, replay cursor) are
     baked into the capture, so replays repeat them: the work per step is the
     same, the action stream repeats every segment."""
     dev = env.device
-    loop = TrainSegment(env, seg, parallel=parallel)
+    loop = TrainSegment(env, seg, parallel=parallel, fused=fused)
     side = torch.cuda.Stream(dev)
     side.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(side):
@@ -354,7 +361,7 @@ def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False):
     dt = e0.elapsed_time(e1) / 1e3
     E = env.num_envs
     branches = ("synthetic actions and replay add_many on parallel graph branches, 3 rotating buffers"
-                if parallel else "one stream")
+                if parallel else "one stream" + ("; synthetic actions inside the act launch" if fused else ""))
     return {"env_steps_per_s": E * seg * reps / dt, "us_per_step": dt / (seg * reps) * 1e6,
             "segments": reps, "steps_per_segment": seg,
             "loop": f"hipGraph of {seg} x [synth actions -> qnet act (drone 0) -> step + obs(K=1) -> "
@@ -376,6 +383,8 @@ def main():
                     help="steps per drl_rollout launch for the rollout measurement (0 = skip)")
     ap.add_argument("--loop-segments", type=int, default=3,
                     help="train-loop graph replays (100 steps + reset each; 0 = skip)")
+    ap.add_argument("--unfused-act", action="store_true",
+                    help="train loop: synthetic actions as their own launch instead of inside the act launch")
     ap.add_argument("--parallel-loop", action="store_true",
                     help="train loop with synth / replay on parallel graph branches (measured slower: the step "
                          "kernel fills every CU in one generation, and co-running kernels delay its waves)")
@@ -491,7 +500,7 @@ def main():
 
     loop = None
     if args.loop_segments > 0 and not args.no_dqn and K >= 1:
-        loop = train_loop_bench(env, args.loop_segments, parallel=args.parallel_loop)
+        loop = train_loop_bench(env, args.loop_segments, parallel=args.parallel_loop, fused=not args.unfused_act)
         loop["env_steps_per_s"] = min_over_ranks(loop["env_steps_per_s"], world) * world
         loop["n_gpus"] = world
 

@@ -29,7 +29,7 @@ EXPORTS = ["drl_abi_version", "drl_last_error", "drl_side_from_density", "drl_la
            "drl_env_step_obs", "drl_env_obs", "drl_env_grid_obs", "drl_env_get_state", "drl_env_set_state", "drl_env_state",
            "drl_env_errors",
            # DQN consumer
-           "drl_qnet_packed_bytes", "drl_qnet_pack", "drl_qnet_act", "drl_replay_add"]
+           "drl_qnet_packed_bytes", "drl_qnet_pack", "drl_qnet_act", "drl_qnet_act_synth", "drl_replay_add"]
 
 
 class DrlParams(ctypes.Structure):

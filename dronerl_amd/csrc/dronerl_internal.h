@@ -171,6 +171,8 @@ struct QnetArgs {
     int32_t* actions;
     int64_t action_stride;
     float* q;
+    int synth_n;                    // > 1: also write drl_synth_actions' columns 1..synth_n-1
+    uint64_t synth_seed, synth_step;
 };
 
 struct ReplayArgs {

@@ -131,7 +131,8 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_kernel(QnetArgs a)
         const int64_t env = t * 16 + c;
         return (uint32_t)((env < a.E ? env : a.E - 1) * a.obs_stride * 4);
     };
-    int64_t grp = (int64_t)blockIdx.x * QN_WAVES + wave;
+    const int64_t grp0 = (int64_t)blockIdx.x * QN_WAVES + wave;
+    int64_t grp = grp0;
     uint32_t row[TP];
 #pragma unroll
     for (int h = 0; h < TP; ++h) row[h] = row_of(TP * (grp < ngroups ? grp : 0) + h);
@@ -257,6 +258,25 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_kernel(QnetArgs a)
                 a.actions[env * a.action_stride] = (u < a.epsilon) ? rnd : best;
                 if (a.q)
                     for (int i = 0; i < a.n_actions; ++i) a.q[env * a.n_actions + i] = q[i];
+            }
+        }
+    }
+    if (a.synth_n > 1) {
+        // drl_synth_actions' columns 1..N-1 of this wave's envs, last: stores
+        // issued before the net's LDS-DMA wait (vmcnt counts them) would delay
+        // the first group
+        const uint32_t nd = (uint32_t)a.synth_n - 1u;
+        const uint32_t per = (uint32_t)(TP * 16) * nd;
+        for (int64_t gg = grp0; gg < ngroups; gg += gstride) {
+            for (uint32_t k = (uint32_t)lane; k < per; k += 64u) {
+                const uint32_t el = k / nd;
+                const int64_t env = TP * 16 * gg + el;
+                const uint64_t drone = 1u + (k - el * nd);
+                if (env < a.E) {
+                    const uint64_t ctr = (a.synth_step << 40) ^ ((uint64_t)(a.env_offset + env) << 8) ^ drone;
+                    const uint64_t h = qn_splitmix64(a.synth_seed ^ qn_splitmix64(ctr));
+                    a.actions[env * a.action_stride + (int64_t)drone] = (int32_t)(((h >> 32) * 5ull) >> 32);
+                }
             }
         }
     }

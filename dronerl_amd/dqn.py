@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import ctypes
 from dataclasses import dataclass
-from typing import Optional, Sequence
+from typing import Optional, Sequence, Tuple
 
 import torch
 
@@ -47,6 +47,7 @@ def _bind(L):
         "drl_qnet_packed_bytes": [D, ctypes.POINTER(i64)],
         "drl_qnet_pack": [D, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp, _vp],
         "drl_qnet_act": [D, _vp, _vp, i64, i64, f32, u64, u64, i64, _vp, i64, _vp, _vp],
+        "drl_qnet_act_synth": [D, _vp, _vp, i64, i64, f32, u64, u64, i64, _vp, i32, u64, u64, _vp, _vp],
         "drl_replay_add": [ctypes.POINTER(DrlReplay), i64, i64, _vp, i64, _vp, i64, _vp, i64, _vp, i64, _vp, i64, _vp],
     }
     for name, args in sig.items():
@@ -120,10 +121,13 @@ class QNetwork:
         return x
 
     def act(self, obs: torch.Tensor, epsilon: float, seed: int = 0, step: int = 0, env_offset: int = 0,
-            actions: Optional[torch.Tensor] = None, q_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+            actions: Optional[torch.Tensor] = None, q_out: Optional[torch.Tensor] = None,
+            synth: Optional[Tuple[int, int]] = None) -> torch.Tensor:
         """Epsilon-greedy action for each row of obs [E, ..., in_features].
         `actions` may be an [E, n_drones] int32 tensor: column 0 is written (the
-        other drones keep their actions, train_jax.py:47-49)."""
+        other drones keep their actions, train_jax.py:47-49).  synth=(seed,
+        step): the other columns get BatchedDeliveryDrones.synth_actions(seed,
+        step)'s values in the same launch (drl_qnet_act_synth)."""
         E = obs.shape[0]
         flat = obs.reshape(E, -1)
         if flat.shape[1] < self.in_features or flat.dtype != torch.float32:
@@ -133,6 +137,13 @@ class QNetwork:
         if actions.dtype != torch.int32 or actions.shape[0] != E or not actions.is_contiguous():
             raise ValueError("actions must be a contiguous int32 [E, n] tensor")
         stride_a = actions.shape[1] if actions.dim() == 2 else 1
+        if synth is not None:
+            _check(self.L, self.L.drl_qnet_act_synth(
+                ctypes.byref(self.desc), _vp(self.packed.data_ptr()), _vp(flat.data_ptr()), E, flat.stride(0),
+                float(epsilon), seed & (2**64 - 1), step, env_offset, _vp(actions.data_ptr()), stride_a,
+                synth[0] & (2**64 - 1), synth[1], None if q_out is None else _vp(q_out.data_ptr()),
+                _stream(self.device)))
+            return actions
         _check(self.L, self.L.drl_qnet_act(ctypes.byref(self.desc), _vp(self.packed.data_ptr()), _vp(flat.data_ptr()),
                                            E, flat.stride(0), float(epsilon), seed & (2**64 - 1), step, env_offset,
                                            _vp(actions.data_ptr()), stride_a,

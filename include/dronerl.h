@@ -272,6 +272,15 @@ int drl_qnet_pack(const drl_qnet_desc* d, const float* const* d_weights, const f
 int drl_qnet_act(const drl_qnet_desc* d, const void* d_packed, const float* d_obs, int64_t num_envs,
                  int64_t obs_stride, float epsilon, uint64_t seed, uint64_t step, int64_t env_offset,
                  int32_t* d_actions, int64_t action_stride, float* d_q, hipStream_t stream);
+/* drl_qnet_act for column 0 of d_actions [num_envs][n_drones] (contiguous
+ * rows), fused with drl_synth_actions(synth_seed, synth_step, env_offset,
+ * num_envs, n_drones) for columns 1..n_drones-1: one launch for the
+ * train_jax.py:42-49 action row (drone 0 from the agent, the others from the
+ * synthetic stream), identical to the two calls in sequence.  n_drones >= 1. */
+int drl_qnet_act_synth(const drl_qnet_desc* d, const void* d_packed, const float* d_obs, int64_t num_envs,
+                       int64_t obs_stride, float epsilon, uint64_t seed, uint64_t step, int64_t env_offset,
+                       int32_t* d_actions, int32_t n_drones, uint64_t synth_seed, uint64_t synth_step, float* d_q,
+                       hipStream_t stream);
 
 /* Replay ring buffer storage (device, caller-owned): obs/next_obs f32
  * [capacity][obs_floats], actions i32, rewards f32, dones u8 [capacity]. */

@@ -128,6 +128,26 @@ def test_qnet_exploration_stream_and_column_write():
 
 
 @gpu
+@pytest.mark.parametrize("E,N,off", [(777, 8, 5000), (31, 3, 0), (4096, 32, 123), (100, 1, 7), (65536, 8, 0)])
+def test_qnet_act_synth_equals_synth_then_act(E, N, off):
+    """drl_qnet_act_synth == drl_synth_actions followed by drl_qnet_act (the
+    fused launch of bench.TrainSegment), Q included."""
+    from dronerl_amd import _native
+    from dronerl_amd.dqn import QNetwork
+    obs, env = _obs_batch(E)
+    net = QNetwork(obs.shape[1], (128, 64), generator=torch.Generator().manual_seed(11))
+    ref = torch.empty((E, N), dtype=torch.int32, device="cuda")
+    assert _native.lib().drl_synth_actions(2024, 9, off, E, N, ref.data_ptr(),
+                                           torch.cuda.current_stream().cuda_stream) == 0
+    q0, q1 = torch.empty((E, 5), device="cuda"), torch.empty((E, 5), device="cuda")
+    net.act(obs, epsilon=0.25, seed=7, step=3, env_offset=off, actions=ref, q_out=q0)
+    got = torch.full((E, N), -1, dtype=torch.int32, device="cuda")
+    net.act(obs, epsilon=0.25, seed=7, step=3, env_offset=off, actions=got, q_out=q1, synth=(2024, 9))
+    assert torch.equal(got, ref)
+    assert torch.equal(q0, q1)
+
+
+@gpu
 def test_qnet_load_repacks():
     from dronerl_amd.dqn import QNetwork
     obs, _ = _obs_batch(256)

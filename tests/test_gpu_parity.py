@@ -674,24 +674,26 @@ def test_rollout_last_step_outputs_and_oracle():
 
 def test_train_segment_parallel_matches_serial():
     """bench.TrainSegment: synthetic actions and replay add_many on parallel
-    stream branches (3 rotating buffers) leave the same env state, replay
-    buffer and next observation as the same calls on one stream."""
+    stream branches (3 rotating buffers), and the one-stream loop with the
+    synthetic actions fused into the act launch, leave the same env state,
+    replay buffer and next observation as the plain calls on one stream."""
     from bench import TrainSegment
     p = EnvParams(n_drones=8, grid_size=16)
     E, seg = 3000, 13
     runs = []
-    for parallel in (False, True):
+    for parallel, fused in ((False, False), (True, False), (False, True)):
         env = Env(p, E)
         env.reset(seed=5)
-        loop = TrainSegment(env, seg, parallel=parallel)
+        loop = TrainSegment(env, seg, parallel=parallel, fused=fused)
         loop.run()
         loop.run()
         torch.cuda.synchronize()
         env.check_errors()
         runs.append((gpu_state(env), loop))
-    (g0, l0), (g1, l1) = runs
-    assert_state(g1, g0, "parallel vs serial segments")
-    for k in ("obs", "next_obs", "actions", "rewards", "dones"):
-        assert torch.equal(getattr(l0.rb, k), getattr(l1.rb, k)), k
-    assert l0.rb.cursor == l1.rb.cursor
-    assert torch.equal(l0.obs[0], l1.obs[0])
+    g0, l0 = runs[0]
+    for name, (g1, l1) in zip(("parallel", "fused"), runs[1:]):
+        assert_state(g1, g0, f"{name} vs serial segments")
+        for k in ("obs", "next_obs", "actions", "rewards", "dones"):
+            assert torch.equal(getattr(l0.rb, k), getattr(l1.rb, k)), (name, k)
+        assert l0.rb.cursor == l1.rb.cursor
+        assert torch.equal(l0.obs[0], l1.obs[0]), name
