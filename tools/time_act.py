@@ -15,6 +15,7 @@ def main():
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--hidden", default="128,64")
     ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--stride", type=int, default=294, help="obs row stride in floats (296: 16-B aligned rows)")
     args = ap.parse_args()
     if args.lib:
         import dronerl_amd._native as nat
@@ -25,6 +26,10 @@ def main():
     net = QNetwork(294, tuple(int(x) for x in args.hidden.split(",")), generator=torch.Generator().manual_seed(0))
     a = torch.zeros((E, 8), dtype=torch.int32, device="cuda")
     flat = obs.reshape(E, -1)
+    if args.stride != 294:
+        big = torch.zeros((E, args.stride), device="cuda")
+        big[:, :294] = flat
+        flat = big[:, :294]
     for _ in range(20):
         net.act(flat, 0.1, actions=a)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -36,7 +41,7 @@ def main():
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / args.iters
     print(f"{os.path.basename(args.lib) or 'libdronerl.so'} E={E} hidden={args.hidden}: {us:.2f} us/launch, "
-          f"{E * 1176 / us / 1e3:.0f} GB/s obs read")
+          f"{E * 1176 / us / 1e3:.0f} GB/s obs read (row stride {flat.stride(0)} floats)")
 
 
 if __name__ == "__main__":
