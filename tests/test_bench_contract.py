@@ -1,0 +1,60 @@
+"""CPU checks of bench.py's measurement pieces (no GPU): the survey's
+algorithmic bytes per env-step, the committed PMC traffic
+bench.py reports, the CPU-baseline record and the command-line contract."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import bench  # noqa: E402
+
+
+@pytest.mark.parametrize("cfg,R,W", [("c2", 296, 1504), ("c3", 296, 1504), ("c4", 1104, 2344),
+                                     ("c5", 4256, 5560)])
+def test_algorithmic_bytes_match_survey_d3(cfg, R, W):
+    G, N, _, K = bench.CONFIGS[cfg]
+    assert bench.algorithmic_bytes(G, N, K) == (R, W)
+
+
+def test_headline_config_is_c3():
+    assert bench.CONFIGS["c3"] == (16, 8, 65536, 1)
+    assert bench.CONFIGS["c5"][2] * 8 == 2 ** 20  # north star: 2^20 envs over 8 GPUs
+
+
+@pytest.mark.parametrize("cfg", ["c3", "c4", "c5"])
+def test_committed_traffic_is_read_plus_doubled_fetch(cfg):
+    path = os.path.join(REPO, "profiles", f"pmc_{cfg}.json")
+    if not os.path.exists(path):
+        pytest.skip(f"no {path}")
+    with open(path) as f:
+        d = json.load(f)
+    pmc = d["pmc_mean_per_launch"]
+    # MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE counts half the bytes (KiB units)
+    expect = (2 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024
+    assert abs(d["hbm_bytes_per_launch"] - expect) <= 1e-6 * expect
+    assert bench.load_traffic(cfg) == d["hbm_bytes_per_launch"]
+    G, N, E, K = bench.CONFIGS[cfg]
+    R, W = bench.algorithmic_bytes(G, N, K)
+    # measured traffic per env-step within a factor of 2 of the algorithmic bytes
+    per = d["hbm_bytes_per_launch"] / E
+    assert 0.5 * (R + W) < per < 2.0 * (R + W)
+
+
+def test_cpu_baseline_record():
+    rec = bench.cpu_baseline(8, 4, 1, seconds=0.4)
+    assert rec["kind"] == "port" and rec["unit"] == "env-steps/s"
+    assert rec["value"] > 0 and rec["single_thread_value"] > 0
+    assert 1 <= rec["cores"] <= 16
+    assert "envs x" in rec["sample"]
+
+
+def test_cli_help_lists_contract_flags():
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--help"], capture_output=True,
+                         text=True, timeout=120, check=True).stdout
+    for flag in ("--gpus", "--steps", "--warmup", "--config"):
+        assert flag in out
