@@ -10,6 +10,10 @@ namespace drl {
 constexpr int MT_N = 624;
 constexpr int MT_M = 397;
 constexpr int MT_WORDS = DRL_MT_WORDS;
+// DRL_ROLL_ACT_LDS: drl_rollout loads the next step's actions by LDS-DMA at the end of each step
+#ifndef DRL_ROLL_ACT_LDS
+#define DRL_ROLL_ACT_LDS 1
+#endif
 // DRL_DPP8: P = 8 / 16 claim and crash-order scans by DPP lane swaps instead of ds_bpermute
 #ifndef DRL_DPP8
 #define DRL_DPP8 1

@@ -206,6 +206,7 @@ struct Geo {
         else return fdiv(n, a.og.div_w);
     }
     static constexpr bool kObs = KC != 0;  // KC == 0: instance for steps without observation
+    static constexpr int kN = NC;
     static constexpr int kGstride = GC > 0 ? lay::gstride(GC) : 0;
 };
 using GeoRT = Geo<0, 0, 0, -1>;
@@ -542,6 +543,21 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     uint32_t* const stash = W.mtw;  // ROLL: records between steps ([GPW][P], O order)
     int act_next = 4;
     const int T = ROLL ? a.steps : 1;
+#if DRL_ROLL_ACT_LDS
+    // rollout: the next step's actions go straight to LDS (LDS-DMA into the
+    // change-list area, unused by rollouts) at the end of each step, so no
+    // register carries them across the observation phase
+    // (only where the 64-VGPR cap made the rollout spill: P <= 8 with the observation)
+    constexpr bool kActLds =
+        ROLL && P <= 8 && GEO::kObs && GEO::kN > 0 && GPW * lay::chg_bytes(GEO::kN > 0 ? GEO::kN : 1) >= 256;
+#else
+    constexpr bool kActLds = false;
+#endif
+    uint32_t* const actb = reinterpret_cast<uint32_t*>(W.chg);
+    if constexpr (kActLds) {  // lane i's action (index li) at actb[i], as the LDS-DMA leaves it
+        actb[lane0] = (uint32_t)act_ld;
+        wave_sync();
+    }
     for (int t = 0; t < T; ++t) {
     // per-lane indices and LDS pointers, re-derived every step from an opaque
     // copy of the lane id: in a rollout under the 64-VGPR cap (P <= 8),
@@ -561,13 +577,15 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     if constexpr (ROLL) {
         if (t > 0) {  // the previous step left its records in the stash
             rec = active ? stash[lane] : 0u;
-            my_action = active ? act_next : 4;
+            if constexpr (kActLds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the actions' LDS-DMA
+            else my_action = active ? act_next : 4;
             wave_sync();
             lds_zero(W.bm, GPW * g.lds_bm(), lane);
             if (GEO::kObs && a.obs) lds_zero(W.paint, GPW * g.lds_paint(), lane);
             wave_sync();
         }
-        if (t + 1 < T) act_next = a.actions[(t + 1) * a.act_tstride + wenv0 * N + li];
+        if constexpr (!kActLds)
+            if (t + 1 < T) act_next = a.actions[(t + 1) * a.act_tstride + wenv0 * N + li];
     }
 
     DRL_STAMP(1);
@@ -575,7 +593,9 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     const int idx = ((int)(rec >> 25) < N) ? (int)(rec >> 25) : j;  // corrupt records never index out of bounds
     int c = (rec >> 16) & 255u;
     int carry = (rec >> 24) & 1u;
-    int act = gshfl<P>(my_action, idx, lane);  // actions are by drone index (env.py:125)
+    int act;  // actions are by drone index (env.py:125)
+    if constexpr (kActLds) act = (int)actb[grp * P + idx];  // lane grp*P + idx holds index grp*N + idx
+    else act = gshfl<P>(my_action, idx, lane);
     // MT-word prefetch: issued once the records have landed (LDS-DMA makes the
     // compiler wait for every outstanding load before the first record use),
     // so its latency overlaps the claim / effect / ordering phases
@@ -897,6 +917,12 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     if constexpr (ROLL) {  // records to the stash (the observation stage aliased it until here)
         wave_sync();
         if (active) stash[grp * P + newslot] = rec_out;
+        if constexpr (kActLds) {
+            if (t + 1 < T)  // after the last LDS write of the step (LDS writes after an LDS-DMA wait for it)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(a.actions + (t + 1) * a.act_tstride + wenv0 * N + li),
+                    (__attribute__((address_space(3))) void*)actb, 4, 0, 0);
+        }
     }
     }  // steps
     if constexpr (ROLL) {  // write the state back once: records, MT index, whole grounds

@@ -11,7 +11,7 @@ if [ -n "${VARLIB:-}" ]; then
   rc=$?; echo "variant rollout tests ($VARLIB) rc=$rc"; tail -1 gpurun_out/pytest_var.log
   [ $rc -le 1 ] || exit $rc
 fi
-for r in 1 2; do
+for r in $(seq 1 ${ROUNDS:-2}); do
   for v in $VARS; do
     DRL_LIB=tools/var_$v.so timeout -k 10 200 python bench.py --config ${CFG:-c3} --steps 500 --warmup 100 --no-cpu-baseline \
       --no-reset-bench --no-dqn --loop-segments 0 > gpurun_out/roll_$v.json 2>/dev/null || exit 1
