@@ -22,7 +22,7 @@ constexpr int MT_WORDS = DRL_MT_WORDS;
 // round's words (>= 16) are prefetched into LDS with the step's other loads
 // (tuning knobs for tools/ab.py builds: DRL_DRAWS_P<P> overrides one width)
 #ifndef DRL_DRAWS_P8
-#define DRL_DRAWS_P8 1
+#define DRL_DRAWS_P8 2
 #endif
 #ifndef DRL_DRAWS_P16
 #define DRL_DRAWS_P16 2
@@ -33,7 +33,17 @@ constexpr int MT_WORDS = DRL_MT_WORDS;
 constexpr int step_draws(int P) {
     return P == 8 ? DRL_DRAWS_P8 : P == 16 ? DRL_DRAWS_P16 : P == 32 ? DRL_DRAWS_P32 : 1;
 }
-constexpr int step_pf(int P) { return step_draws(P) * P < 16 ? 16 : step_draws(P) * P; }
+// drl_rollout keeps one draw per lane at P = 8: two spill under its 64-VGPR cap
+#ifndef DRL_ROLL_DRAWS_P8
+#define DRL_ROLL_DRAWS_P8 1
+#endif
+constexpr int roll_draws(int P) { return P == 8 ? DRL_ROLL_DRAWS_P8 : step_draws(P); }
+// prefetched MT words per env: one round's worth for either kernel, >= 16
+constexpr int step_pf(int P) {
+    return (step_draws(P) > roll_draws(P) ? step_draws(P) : roll_draws(P)) * P < 16
+               ? 16
+               : (step_draws(P) > roll_draws(P) ? step_draws(P) : roll_draws(P)) * P;
+}
 constexpr int OBS_U = 1;        // observation cells per lane per pass (stage: OBS_U*1536 B per wave)
 
 // Per-env LDS layout of drl_step (WaveLds in dronerl_kernels.hip).  Shared by
