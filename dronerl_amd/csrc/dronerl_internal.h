@@ -38,11 +38,18 @@ constexpr int step_draws(int P) {
 #define DRL_ROLL_DRAWS_P8 1
 #endif
 constexpr int roll_draws(int P) { return P == 8 ? DRL_ROLL_DRAWS_P8 : step_draws(P); }
-// prefetched MT words per env: one round's worth for either kernel, >= 16
+// MT words prefetched per env with the step's first loads: at least one
+// round's worth and 16; drl_step at P = 8 takes two rounds' (DRL_PF_P8), the
+// rollout one.  step_pf sizes the LDS area for both kernels.
+#ifndef DRL_PF_P8
+#define DRL_PF_P8 32
+#endif
+constexpr int pf_for(int D, int P, int floor) { return D * P < floor ? floor : D * P; }
+constexpr int roll_pf(int P) { return pf_for(roll_draws(P), P, 16); }
 constexpr int step_pf(int P) {
-    return (step_draws(P) > roll_draws(P) ? step_draws(P) : roll_draws(P)) * P < 16
-               ? 16
-               : (step_draws(P) > roll_draws(P) ? step_draws(P) : roll_draws(P)) * P;
+    return pf_for(step_draws(P), P, P == 8 ? DRL_PF_P8 : 16) > roll_pf(P)
+               ? pf_for(step_draws(P), P, P == 8 ? DRL_PF_P8 : 16)
+               : roll_pf(P);
 }
 constexpr int OBS_U = 1;        // observation cells per lane per pass (stage: OBS_U*1536 B per wave)
 

@@ -491,7 +491,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     using GMask = typename GMaskT<P>::type;
     constexpr int GPW = 64 / P;
     constexpr int D = ROLL ? roll_draws(P) : step_draws(P);  // draws per lane per respawn round
-    constexpr int PF = step_pf(P);               // prefetched MT words per env
+    constexpr int PF = ROLL ? roll_pf(P) : step_pf(P);  // prefetched MT words per env
     constexpr int PFR = (PF + P - 1) / P;        // prefetched MT words per lane
     using CM = typename GMaskT<(P * D <= 32 ? 32 : 64)>::type;  // round-position masks
     constexpr int CH = P < 16 ? P : 16;        // shuffle batch
