@@ -47,11 +47,14 @@ constexpr int roll_draws(int P) { return P == 8 ? DRL_ROLL_DRAWS_P8 : step_draws
 #ifndef DRL_PF_P16
 #define DRL_PF_P16 16
 #endif
+#ifndef DRL_PF_P32
+#define DRL_PF_P32 16
+#endif
 constexpr int pf_for(int D, int P, int floor) { return D * P < floor ? floor : D * P; }
 constexpr int roll_pf(int P) { return pf_for(roll_draws(P), P, 16); }
 constexpr int step_pf(int P) {
-    return pf_for(step_draws(P), P, P == 8 ? DRL_PF_P8 : P == 16 ? DRL_PF_P16 : 16) > roll_pf(P)
-               ? pf_for(step_draws(P), P, P == 8 ? DRL_PF_P8 : P == 16 ? DRL_PF_P16 : 16)
+    return pf_for(step_draws(P), P, P == 8 ? DRL_PF_P8 : P == 16 ? DRL_PF_P16 : P == 32 ? DRL_PF_P32 : 16) > roll_pf(P)
+               ? pf_for(step_draws(P), P, P == 8 ? DRL_PF_P8 : P == 16 ? DRL_PF_P16 : P == 32 ? DRL_PF_P32 : 16)
                : roll_pf(P);
 }
 constexpr int OBS_U = 1;        // observation cells per lane per pass (stage: OBS_U*1536 B per wave)
