@@ -19,6 +19,7 @@ DRL_MAX_SIDE = 128
 DRL_MAX_RADIUS = 8
 DRL_ERR_BAD_ACTION = 1
 DRL_ERR_NO_FREE_CELL = 2
+DRL_ERR_BAD_STATE = 4
 DRL_STEP_OBS_STREAM = 1  # drl_step_ex flag: streaming (non-temporal) observation stores
 
 # Every symbol include/dronerl.h declares (tests check the .so exports them all).
@@ -81,6 +82,12 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise DroneRLError(f"{LIB_PATH} is missing: build the HIP extension with `python -m dronerl_amd.build` "
                            "(there is no CPU fallback)")
+    if not os.environ.get("DRL_LIB"):
+        # the in-tree library must have been built from the sources beside it
+        from . import build as _b
+        if not _b.up_to_date():
+            raise DroneRLError(f"{LIB_PATH} was not built from the current sources (digest mismatch with "
+                               f"{_b.HASH}): rebuild with `python -m dronerl_amd.build`")
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
     P = ctypes.POINTER(DrlParams)

@@ -2,6 +2,7 @@
 
 python -m dronerl_amd.build   (or dronerl_amd.build.build())
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -10,6 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdronerl.so")
+HASH = LIB + ".srchash"
 SOURCES = [os.path.join(CSRC, "dronerl_kernels.hip"), os.path.join(CSRC, "dronerl_api.cpp"),
            os.path.join(CSRC, "dronerl_env.cpp"), os.path.join(CSRC, "dronerl_qnet.hip"),
            os.path.join(CSRC, "dronerl_qnet_api.cpp")]
@@ -24,22 +26,44 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+def compile_cmd(out: str):
+    return [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+            "-Wno-unused-function", "-I", os.path.join(REPO, "include"), "-o", out] + SOURCES
+
+
+def source_digest() -> str:
+    """sha256 over every source/header the library is built from and the
+    target arch: the key a built library is checked against."""
+    h = hashlib.sha256(ARCH.encode())
+    for d in DEPS:
+        h.update(os.path.basename(d).encode())
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def up_to_date() -> bool:
-    if not os.path.exists(LIB):
+    try:
+        with open(HASH) as f:
+            return os.path.exists(LIB) and f.read().strip() == source_digest()
+    except OSError:
         return False
-    t = os.path.getmtime(LIB)
-    return all(os.path.getmtime(d) <= t for d in DEPS)
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Rebuild unless the library on disk was built from exactly these sources
+    (its sidecar LIB.srchash holds their digest; _native refuses to load a
+    library whose digest does not match the sources beside it)."""
     if not force and up_to_date():
         return LIB
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-I", os.path.join(REPO, "include"), "-o", LIB + ".tmp"] + SOURCES
+    cmd = compile_cmd(LIB + ".tmp")
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
+    digest = source_digest()
     subprocess.run(cmd, check=True)
     os.replace(LIB + ".tmp", LIB)
+    with open(HASH, "w") as f:
+        f.write(digest + "\n")
     return LIB
 
 

@@ -124,17 +124,29 @@ def load_qnetwork(path: str) -> TorchQNetwork:
     return TorchQNetwork(read_checkpoint(path)).eval()
 
 
-def save_checkpoint(path: str, net: TorchQNetwork, conv_layers=(), dense_layers=None):
-    """torch-format checkpoint (dqn.py:330-345 metadata keys)."""
+def _conv_meta(m: nn.Conv2d) -> dict:
+    """A Conv2d as the reference's conv_layers entry (dqn.py:336-341); square
+    kernels/strides/paddings are written as ints, as the factories take them."""
+    one = lambda v: v[0] if isinstance(v, tuple) and len(set(v)) == 1 else v  # noqa: E731
+    return {"out_channels": m.out_channels, "kernel_size": one(m.kernel_size), "stride": one(m.stride),
+            "padding": one(m.padding)}
+
+
+def save_checkpoint(path: str, net: TorchQNetwork, conv_layers=None, dense_layers=None):
+    """torch-format checkpoint (dqn.py:330-345 metadata keys).  Layer metadata
+    not given is read off the network's own Linear / Conv2d modules."""
     from safetensors.numpy import save_file
     sd = {k: v.detach().cpu().numpy() for k, v in net.state_dict().items()}
+    lin = [m for m in net.network.children() if isinstance(m, nn.Linear)]
+    if not lin:
+        raise ValueError("network has no Linear layer")
     if dense_layers is None:
-        lin = [m for n, m in net.network.named_children() if n.startswith("dense_")]
         dense_layers = tuple(m.out_features for m in lin[:-1])
-    md = {"network_type": net.kind, "obs_shape": str(net.obs_shape),
-          "action_shape": str((sd[sorted(k for k in sd if k.endswith("weight"))[-1]].shape[0],)),
-          "dense_layers": str(tuple(dense_layers))}
+    md = {"network_type": net.kind, "obs_shape": str(tuple(net.obs_shape)),
+          "action_shape": str((lin[-1].out_features,)), "dense_layers": str(tuple(dense_layers))}
     if net.kind == "conv":
+        if conv_layers is None:
+            conv_layers = tuple(_conv_meta(m) for m in net.network.children() if isinstance(m, nn.Conv2d))
         md["conv_layers"] = str(tuple(conv_layers))
     save_file(sd, path, metadata=md)
 

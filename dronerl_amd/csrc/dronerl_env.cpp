@@ -11,7 +11,7 @@
 #include <stdio.h>
 #include <string.h>
 
-#include "../../include/dronerl.h"
+#include "dronerl_internal.h"
 
 struct drl_env {
     drl_params p;
@@ -202,7 +202,8 @@ int drl_env_set_state(drl_env* env, const drl_state_view* v, hipStream_t stream)
                                        hipMemcpyDeviceToDevice, stream),
                       "mt copy") ||
             hip_check(hipMemcpy2DAsync(env->s.mt_index, 4, v->mt + 624, 625 * 4, 4, E, hipMemcpyDeviceToDevice, stream),
-                      "mt index copy"))
+                      "mt index copy") ||
+            hip_check(drl::launch_mt_index_check(env->s.mt_index, (int64_t)E, env->err, stream), "mt index check"))
             return -1;
         env->seeded = 1;
         return 0;

@@ -235,6 +235,7 @@ hipError_t launch_grid_obs(const uint8_t* ground, const uint32_t* drones, int64_
                            float* out, hipStream_t s);
 hipError_t launch_encode(uint32_t* drones, int64_t E, int N, const int32_t* order, const int32_t* y,
                          const int32_t* x, const int32_t* c, const uint8_t* k, hipStream_t s);
+hipError_t launch_mt_index_check(uint32_t* mt_index, int64_t E, int32_t* err, hipStream_t s);
 hipError_t launch_synth(uint64_t seed, uint64_t step, int64_t env_offset, int64_t E, int N, int32_t* out,
                         hipStream_t s);
 

@@ -1540,6 +1540,17 @@ __global__ void drl_encode_kernel(uint32_t* __restrict__ drones, int64_t total, 
     drones[t] = pack_drone(yv[o], xv[o], cv[o], kv[o] ? 1 : 0, idx);
 }
 
+// CPython's setstate rejects an index outside [0, 624]; the step kernel's MT
+// reads assume that range, so set_state clamps and flags instead.
+__global__ void drl_mt_index_check_kernel(uint32_t* __restrict__ mt_index, int64_t E, int32_t* err) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    if (mt_index[e] > (uint32_t)MT_N) {
+        mt_index[e] = (uint32_t)MT_N;
+        if (err) atomicOr(err, DRL_ERR_BAD_STATE);
+    }
+}
+
 // ------------------------------------------------------- synthetic actions ---
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
     z += 0x9e3779b97f4a7c15ull;
@@ -1652,6 +1663,11 @@ hipError_t launch_encode(uint32_t* drones, int64_t E, int N, const int32_t* orde
     const int64_t total = E * N;
     hipLaunchKernelGGL(drl_encode_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, drones, total, N,
                        order, y, x, c, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_mt_index_check(uint32_t* mt_index, int64_t E, int32_t* err, hipStream_t s) {
+    hipLaunchKernelGGL(drl_mt_index_check_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, mt_index, E, err);
     return hipGetLastError();
 }
 

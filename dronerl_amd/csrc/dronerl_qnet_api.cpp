@@ -186,6 +186,9 @@ int drl_replay_add(const drl_replay* r, int64_t cursor, int64_t n, const float* 
     if ((uintptr_t)d_obs % 8 || (uintptr_t)d_next_obs % 8 || (uintptr_t)r->obs % 8 || (uintptr_t)r->next_obs % 8 ||
         obs_stride % 2 || next_obs_stride % 2)
         return fail("observation rows must be 8-byte aligned");
+    if (obs_stride < r->obs_floats || next_obs_stride < r->obs_floats)
+        return fail("obs_stride / next_obs_stride < obs_floats");
+    if (action_stride < 1 || reward_stride < 1 || done_stride < 1) return fail("action/reward/done strides must be >= 1");
     drl::ReplayArgs a;
     memset(&a, 0, sizeof a);
     a.n = n;

@@ -63,6 +63,12 @@ def _check(L, rc):
         raise DroneRLError(L.drl_last_error().decode())
 
 
+def _on(t, device, dtype, name):
+    """The kernels read and write raw device pointers: no conversion, no copies."""
+    if not isinstance(t, torch.Tensor) or t.device != torch.device(device) or t.dtype != dtype:
+        raise ValueError(f"{name} must be a {dtype} tensor on {device}")
+
+
 def _stream(device):
     return _vp(torch.cuda.current_stream(device).cuda_stream)
 
@@ -129,13 +135,19 @@ class QNetwork:
         step): the other columns get BatchedDeliveryDrones.synth_actions(seed,
         step)'s values in the same launch (drl_qnet_act_synth)."""
         E = obs.shape[0]
+        _on(obs, self.device, torch.float32, "obs")
         flat = obs.reshape(E, -1)
-        if flat.shape[1] < self.in_features or flat.dtype != torch.float32:
-            raise ValueError("obs must be float32 with at least in_features values per env")
+        if flat.shape[1] < self.in_features or flat.stride(1) != 1:
+            raise ValueError("obs must hold at least in_features contiguous float32 values per env")
         if actions is None:
             actions = torch.empty((E, 1), dtype=torch.int32, device=self.device)
-        if actions.dtype != torch.int32 or actions.shape[0] != E or not actions.is_contiguous():
-            raise ValueError("actions must be a contiguous int32 [E, n] tensor")
+        _on(actions, self.device, torch.int32, "actions")
+        if actions.shape[0] != E or actions.dim() > 2 or not actions.is_contiguous():
+            raise ValueError("actions must be a contiguous int32 [E] or [E, n] tensor")
+        if q_out is not None:
+            _on(q_out, self.device, torch.float32, "q_out")
+            if tuple(q_out.shape) != (E, self.n_actions) or not q_out.is_contiguous():
+                raise ValueError(f"q_out must be a contiguous float32 [{E}, {self.n_actions}] tensor")
         stride_a = actions.shape[1] if actions.dim() == 2 else 1
         if synth is not None:
             _check(self.L, self.L.drl_qnet_act_synth(
@@ -176,7 +188,18 @@ class ReplayBuffer:
         """buffers.py:57-80.  obs/next_obs [E, >= obs_floats] f32 rows; actions
         i32, rewards f32, dones u8 as [E] or [E, n_drones] (column 0 taken)."""
         E = obs.shape[0]
+        dev = self.obs.device
+        for t, dt, name in ((obs, torch.float32, "obs"), (next_obs, torch.float32, "next_obs"),
+                            (actions, torch.int32, "actions"), (rewards, torch.float32, "rewards"),
+                            (dones, torch.uint8, "dones")):
+            _on(t, dev, dt, name)
+            if t.shape[0] != E or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous [{E}, ...] tensor")
+            if name in ("actions", "rewards", "dones") and t.dim() > 2:
+                raise ValueError(f"{name} must be [E] or [E, n_drones]")
         o, no = obs.reshape(E, -1), next_obs.reshape(E, -1)
+        if o.shape[1] < self.obs_floats or no.shape[1] < self.obs_floats:
+            raise ValueError(f"obs rows must hold at least obs_floats={self.obs_floats} values")
         col = lambda t: t.shape[1] if t.dim() == 2 else 1  # noqa: E731
         _check(self.L, self.L.drl_replay_add(ctypes.byref(self._c), self.cursor, E, _vp(o.data_ptr()), o.stride(0),
                                              _vp(no.data_ptr()), no.stride(0), _vp(actions.data_ptr()), col(actions),

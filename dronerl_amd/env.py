@@ -17,7 +17,7 @@ from typing import Optional
 
 import torch
 
-from ._native import (DRL_ERR_BAD_ACTION, DRL_ERR_NO_FREE_CELL, DRL_MT_WORDS, DRL_STEP_OBS_STREAM, DroneRLError,
+from ._native import (DRL_ERR_BAD_ACTION, DRL_ERR_BAD_STATE, DRL_ERR_NO_FREE_CELL, DRL_MT_WORDS, DRL_STEP_OBS_STREAM, DroneRLError,
                       DrlState, check, lib)
 from .params import EnvParams
 
@@ -103,7 +103,14 @@ class BatchedDeliveryDrones:
         if env_mask is not None:
             env_mask = self._check(env_mask, torch.uint8, (self.num_envs,), "env_mask")
         reseed = seed is not None
-        seed_base = (int(seed) + self.env_offset) if reseed else 0
+        seed_base = 0
+        if reseed:
+            # Env g is seeded random.seed(seed + g) with a one-word (u64) key;
+            # outside [0, 2**64) CPython's key differs (abs(), longer keys).
+            seed_base = int(seed) + self.env_offset
+            if seed_base < 0 or seed_base + self.num_envs > 2**64:
+                raise ValueError(f"seed + env index must lie in [0, 2**64) for every env; got seed={seed}, "
+                                 f"env_offset={self.env_offset}, num_envs={self.num_envs}")
         s = self.state.c()
         check(lib().drl_reset(ctypes.byref(self._cp), ctypes.byref(s), int(reseed), seed_base, _ptr(env_mask),
                               _stream(self.device)), "drl_reset")
@@ -125,9 +132,13 @@ class BatchedDeliveryDrones:
             rewards = torch.empty((E, N), dtype=torch.float32, device=self.device)
         if dones is None:
             dones = torch.empty((E, N), dtype=torch.uint8, device=self.device)
+        W = self.layout.obs_window
         if obs_k and obs is None:
-            W = self.layout.obs_window
             obs = torch.empty((E, obs_k, W, W, 6), dtype=torch.float32, device=self.device)
+        self._check_out(rewards, torch.float32, (E, N), "rewards")
+        self._check_out(dones, torch.uint8, (E, N), "dones")
+        if obs_k:
+            self._check_out(obs, torch.float32, (E, obs_k, W, W, 6), "obs")
         s = self.state.c()
         flags = DRL_STEP_OBS_STREAM if obs_stream else 0
         check(lib().drl_step_ex(ctypes.byref(self._cp), ctypes.byref(s), _ptr(actions), _ptr(rewards), _ptr(dones),
@@ -246,6 +257,8 @@ class BatchedDeliveryDrones:
         w = torch.where(w >= 2**31, w - 2**32, w).to(torch.int32)
         if w.shape[0] == 1:
             w = w.expand(self.num_envs, 625)
+        if ((w[:, 624] < 0) | (w[:, 624] > 624)).any():
+            raise ValueError("MT index must lie in [0, 624] (CPython setstate)")
         w = w.to(self.device)
         self.state.mt[:, :624].copy_(w[:, :624])
         self.state.mt_index.copy_(w[:, 624])
@@ -265,6 +278,8 @@ class BatchedDeliveryDrones:
                 msgs.append("action index out of range (IndexError in the reference)")
             if e & DRL_ERR_NO_FREE_CELL:
                 msgs.append("respawn found no free cell")
+            if e & DRL_ERR_BAD_STATE:
+                msgs.append("MT index outside [0, 624] in a set state (clamped to 624)")
             raise DroneRLError("; ".join(msgs))
 
     # ------------------------------------------------------------- helpers --

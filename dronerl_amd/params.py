@@ -71,6 +71,14 @@ class EnvParams:
         return replace(self, **kw)
 
     def to_c(self) -> DrlParams:
+        # The kernels do charge / factor arithmetic on integers (the reference
+        # does it on Python numbers, env.py:79-82,152-155): refuse fractions
+        # instead of truncating them.
+        for name in ("charge", "discharge", "packets_factor", "dropzones_factor", "stations_factor",
+                     "skyscrapers_factor", "n_drones", "window_radius"):
+            v = getattr(self, name)
+            if isinstance(v, bool) or float(v) != int(v):
+                raise ValueError(f"{name}={v!r}: the C ABI supports integer values only")
         return DrlParams(self.side, self.n_drones, int(self.charge), int(self.discharge), int(self.packets_factor),
                          int(self.dropzones_factor), int(self.stations_factor), int(self.skyscrapers_factor),
                          int(self.window_radius), float(self.pickup_reward), float(self.delivery_reward),

@@ -62,6 +62,8 @@ typedef struct ihipStream_t* hipStream_t;
 /* error bits written to drl_step's optional err word */
 #define DRL_ERR_BAD_ACTION 1   /* action outside [-5, 4] (IndexError in the reference) */
 #define DRL_ERR_NO_FREE_CELL 2 /* respawn found no free cell (the reference loops forever) */
+#define DRL_ERR_BAD_STATE 4    /* drl_env_set_state: MT index outside [0, 624] (CPython setstate's ValueError);
+                                  clamped to 624 */
 
 /* Env parameters: torch_impl DEFAULT_CONFIG (env.py:28-42) / jax DroneEnvParams
  * (jax env.py:11-26).  `side` is explicit; torch_impl derives it as
@@ -233,7 +235,9 @@ int drl_env_obs(drl_env* env, int32_t k, float* d_obs, hipStream_t stream);
 int drl_env_grid_obs(drl_env* env, float* d_grid, hipStream_t stream);
 /* Copy the state out to / in from a caller-owned SoA view (NULL fields are
  * skipped by get_state; set_state needs all of them and trusts their
- * validity: positions on the grid, distinct cells, charge in [0, 100]). */
+ * validity: positions on the grid, distinct cells, charge in [0, 100]; an MT
+ * index outside [0, 624] is clamped to 624 and raises DRL_ERR_BAD_STATE in
+ * the handle's error word). */
 int drl_env_get_state(drl_env* env, const drl_state_view* v, hipStream_t stream);
 int drl_env_set_state(drl_env* env, const drl_state_view* v, hipStream_t stream);
 /* The handle's raw buffers, params and layout (any output may be NULL). */

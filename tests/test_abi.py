@@ -95,3 +95,28 @@ def test_env_handle_without_device_fails_cleanly():
     from dronerl_amd.params import EnvParams
     with pytest.raises(DroneRLError, match="device"):
         DrlEnvHandle(EnvParams(n_drones=4, grid_size=8), 4)
+
+
+@pytest.mark.parametrize("field,value", [("charge", 7.5), ("discharge", 2.5), ("packets_factor", 1.5),
+                                         ("skyscrapers_factor", 0.5)])
+def test_fractional_integer_params_rejected(field, value):
+    """The C ABI does charge / factor arithmetic on integers: a fraction is an
+    error, not a silent truncation (env.py:79-82 uses Python numbers)."""
+    p = EnvParams(n_drones=4, grid_size=8).replace(**{field: value})
+    with pytest.raises(ValueError, match="integer"):
+        p.to_c()
+    EnvParams(n_drones=4, grid_size=8).replace(**{field: float(int(value) + 1)}).to_c()  # integral floats are fine
+
+
+def test_replay_add_rejects_short_rows():
+    """drl_replay_add validates before any device work (no GPU needed)."""
+    from dronerl_amd.dqn import DrlReplay, _bind
+    L = _bind(lib())
+    r = DrlReplay(16, 294, 8, 8, 8, 8, 8)
+    vp = ctypes.c_void_p
+    args = lambda stride: (ctypes.byref(r), 0, 4, vp(8), stride, vp(8), 294, vp(8), 1, vp(8), 1, vp(8), 1, None)  # noqa
+    assert L.drl_replay_add(*args(292)) != 0
+    assert b"obs_floats" in L.drl_last_error()
+    r0 = DrlReplay(16, 294, 8, 8, 8, 8, 8)
+    assert L.drl_replay_add(ctypes.byref(r0), 0, 4, vp(8), 294, vp(8), 294, vp(8), 0, vp(8), 1, vp(8), 1, None) != 0
+    assert b"strides" in L.drl_last_error()

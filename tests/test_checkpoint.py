@@ -80,6 +80,45 @@ def test_save_load_roundtrip(path, tmp_path):
 
 
 @pytest.mark.parametrize("path", MODELS)
+def test_save_load_roundtrip_metadata_from_modules(path, tmp_path):
+    """save_checkpoint(path, net) with no layer metadata: widths, action shape
+    and conv layers are read off the network's modules (dqn.py:330-345)."""
+    ck = read_checkpoint(path)
+    net = TorchQNetwork(ck)
+    out = str(tmp_path / "rt.safetensors")
+    save_checkpoint(out, net)
+    ck2 = read_checkpoint(out)
+    assert (ck2.network_type, ck2.dense_layers, ck2.action_shape) == (ck.network_type, ck.dense_layers,
+                                                                       ck.action_shape)
+    if ck.network_type == "conv":
+        norm = lambda cl: tuple({k: d.get(k, 0) for k in ("out_channels", "kernel_size", "stride", "padding")}
+                                for d in cl)  # noqa: E731
+        assert norm(ck2.conv_layers) == norm(ck.conv_layers)
+    net2 = TorchQNetwork(ck2)
+    x = np.random.default_rng(1).random((8, 7, 7, 6)).astype(np.float32)
+    with torch.no_grad():
+        np.testing.assert_array_equal(net2(x).numpy(), net(x).numpy())
+
+
+def test_save_checkpoint_many_dense_layers(tmp_path):
+    """action_shape comes from the last Linear, not the text-sorted weight
+    names (dense_10 sorts before dense_2)."""
+    ck = read_checkpoint(MODELS[0])
+    widths = (8,) * 10
+    ck = type(ck)("dense", (7, 7, 6), (5,), widths)
+    rng = np.random.default_rng(0)
+    sizes = [294, *widths, 5]
+    for i in range(len(sizes) - 1):
+        ck.tensors[f"network.dense_{i + 1}.weight"] = rng.standard_normal((sizes[i + 1], sizes[i])).astype(np.float32)
+        ck.tensors[f"network.dense_{i + 1}.bias"] = np.zeros(sizes[i + 1], np.float32)
+    net = TorchQNetwork(ck)
+    out = str(tmp_path / "deep.safetensors")
+    save_checkpoint(out, net)
+    ck2 = read_checkpoint(out)
+    assert ck2.action_shape == (5,) and ck2.dense_layers == widths
+
+
+@pytest.mark.parametrize("path", MODELS)
 def test_jax_format_converts_to_torch_layout(path, tmp_path):
     """jax_impl/agents/dqn.py:228-260 naming and kernel layouts."""
     from safetensors.numpy import save_file

@@ -1,0 +1,118 @@
+"""Argument validation on the GPU façades: every buffer a kernel
+writes through a raw pointer is checked before the launch, seeds outside the
+u64 key range the C ABI takes are refused, and an MT index outside CPython's
+setstate range [0, 624] is refused (Python) or clamped and flagged (C ABI)."""
+import random
+
+import pytest
+import torch
+
+from dronerl_amd import BatchedDeliveryDrones, EnvParams
+from dronerl_amd._native import DRL_ERR_BAD_STATE, DroneRLError
+
+pytestmark = pytest.mark.gpu
+
+P = EnvParams(n_drones=4, grid_size=8)
+
+
+@pytest.fixture(scope="module")
+def env():
+    e = BatchedDeliveryDrones(P, 16, device="cuda:0")
+    e.reset(seed=0)
+    return e
+
+
+def test_negative_and_oversized_seeds_rejected(env):
+    with pytest.raises(ValueError, match="seed"):
+        env.reset(seed=-3)
+    with pytest.raises(ValueError, match="seed"):
+        env.reset(seed=2**64 - 8)  # seed + 15 wraps
+    env.reset(seed=2**64 - 16)      # the last representable block is fine
+    env.reset(seed=0)
+
+
+def test_seed_matches_cpython_at_two_word_keys(env):
+    """seed + g up to 2**64 - 1 is a two-word init_by_array key in CPython."""
+    base = 2**64 - 16
+    env.reset(seed=base)
+    w = env.mt_words()
+    for g in (0, 7, 15):
+        random.seed(base + g)
+        st = random.getstate()[1]
+        assert [int(v) for v in w[g].tolist()] == list(st), g
+    env.reset(seed=0)
+
+
+def test_set_mt_words_rejects_bad_index(env):
+    w = env.mt_words()
+    w[:, 624] = 625
+    with pytest.raises(ValueError, match="MT index"):
+        env.set_mt_words(w)
+    w[:, 624] = -1
+    with pytest.raises(ValueError, match="MT index"):
+        env.set_mt_words(w)
+
+
+def test_step_output_buffers_checked(env):
+    E, N = env.num_envs, env.n_drones
+    a = env.synth_actions(seed=1, step=1)
+    with pytest.raises(ValueError, match="rewards"):
+        env.step(a, rewards=torch.empty((E, N), dtype=torch.float64, device="cuda:0"))
+    with pytest.raises(ValueError, match="dones"):
+        env.step(a, dones=torch.empty((E, N + 1), dtype=torch.uint8, device="cuda:0"))
+    with pytest.raises(ValueError, match="obs"):
+        env.step(a, obs_k=1, obs=torch.empty((E, 1, 7, 7, 5), device="cuda:0"))
+    with pytest.raises(ValueError, match="rewards"):
+        env.step(a, rewards=torch.empty((E, N), dtype=torch.float32))  # host tensor
+    with pytest.raises(ValueError, match="obs"):
+        env.step(a, obs_k=1, obs=torch.empty((E, 1, 7, 7, 12), device="cuda:0")[..., ::2])  # non-contiguous
+
+
+def test_handle_set_state_clamps_and_flags_bad_mt_index():
+    from dronerl_amd.handle import DrlEnvHandle
+    h = DrlEnvHandle(P, 4, device=0)
+    h.reset()
+    d = h.get_state()
+    d["mt"][:, 624] = torch.tensor([3, 700, -5, 624], dtype=torch.int32)
+    h.set_state(d)
+    assert h.errors() & DRL_ERR_BAD_STATE
+    assert h.get_state()["mt"][:, 624].tolist() == [3, 624, 624, 624]
+    assert h.errors() == 0
+    h.close()
+
+
+def test_qnet_act_and_replay_checks():
+    from dronerl_amd.dqn import QNetwork, ReplayBuffer
+    net = QNetwork(294, (32, 32), device="cuda:0")
+    obs = torch.zeros((8, 294), device="cuda:0")
+    with pytest.raises(ValueError, match="obs"):
+        net.act(obs.double(), 0.0)
+    with pytest.raises(ValueError, match="obs"):
+        net.act(obs.cpu(), 0.0)
+    with pytest.raises(ValueError, match="q_out"):
+        net.act(obs, 0.0, q_out=torch.empty((8, 4), device="cuda:0"))
+    with pytest.raises(ValueError, match="actions"):
+        net.act(obs, 0.0, actions=torch.empty((8, 2), dtype=torch.int64, device="cuda:0"))
+    rb = ReplayBuffer(16, 294, torch.device("cuda:0"))
+    a = torch.zeros(8, dtype=torch.int32, device="cuda:0")
+    r = torch.zeros(8, device="cuda:0")
+    d = torch.zeros(8, dtype=torch.uint8, device="cuda:0")
+    with pytest.raises(ValueError, match="obs_floats"):
+        rb.add_many(obs[:, :200].contiguous(), a, r, obs, d)
+    with pytest.raises(ValueError, match="rewards"):
+        rb.add_many(obs, a, r.double(), obs, d)
+    with pytest.raises(ValueError, match="dones"):
+        rb.add_many(obs, a, r, obs, d.bool())
+    rb.add_many(obs, a, r, obs, d)
+    torch.cuda.synchronize()
+    assert rb.size == 8
+
+
+def test_bad_action_flag_reported():
+    """An error word raised by a kernel is reported by check_errors, not lost."""
+    e = BatchedDeliveryDrones(P, 2, device="cuda:0")
+    e.reset(seed=0)
+    a = torch.full((2, 4), 9, dtype=torch.int32, device="cuda:0")
+    e.step(a)
+    with pytest.raises(DroneRLError, match="action"):
+        e.check_errors()
