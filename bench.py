@@ -90,6 +90,64 @@ def min_over_ranks(v: float, world: int) -> float:
     return -max_over_ranks(-v, world)
 
 
+def measure_traffic(args):
+    """HBM bytes per drl_step launch from rocprofv3 PMC passes of this same
+    bench command (MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE in
+    separate passes, FETCH_SIZE doubled for gfx950, KiB -> bytes).  Runs as
+    child processes before this process touches the GPU; returns None when
+    rocprofv3 is absent or a pass fails (the caller then reports the committed
+    profile, labelled as such)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3")
+                                         else None)
+    if prof is None:
+        return None
+    child = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", "20", "--warmup", "3",
+             "--no-cpu-baseline", "--no-reset-bench", "--no-dqn", "--rollout-chunk", "0", "--loop-segments", "0",
+             "--no-pmc-traffic", "--cached-steps", "0"]
+    if args.envs:
+        child += ["--envs", str(args.envs)]
+    if args.obs_cached:
+        child.append("--obs-cached")
+    if args.obs_k >= 0:
+        child += ["--obs-k", str(args.obs_k)]
+    vals = {}
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    with tempfile.TemporaryDirectory(prefix="drl_pmc_") as td:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(td, ctr)
+            cmd = [prof, "--pmc", ctr, "--kernel-include-regex", "drl_step_kernel", "-d", d, "-o", "run",
+                   "--output-format", "csv", "--"] + child
+            try:
+                r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=150, env=env,
+                                   cwd=REPO)
+            except subprocess.TimeoutExpired:
+                print(f"pmc pass {ctr}: timed out", file=sys.stderr)
+                return None
+            if r.returncode != 0:
+                print(f"pmc pass {ctr}: rc={r.returncode} {r.stderr.decode(errors='replace')[-300:]}",
+                      file=sys.stderr)
+                return None
+            xs = []
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                for row in csv.DictReader(open(f)):
+                    if "drl_step_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                        xs.append(float(row["Counter_Value"]))
+            if not xs:
+                return None
+            vals[ctr] = sum(xs) / len(xs)
+    read_b = 2 * vals["FETCH_SIZE"] * 1024
+    write_b = vals["WRITE_SIZE"] * 1024
+    return {"bytes_per_launch": read_b + write_b, "read_bytes_per_launch": read_b, "write_bytes_per_launch": write_b,
+            "fetch_size_kib": vals["FETCH_SIZE"], "write_size_kib": vals["WRITE_SIZE"],
+            "source": "measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate child runs "
+                      "of this bench, 20 steps), traffic = 2*FETCH_SIZE + WRITE_SIZE"}
+
+
 def load_traffic(cfg_name: str):
     """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/),
     FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, or None."""
@@ -114,14 +172,40 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def host_cpus():
+    """CPUs this process can actually use: the scheduler affinity, capped by
+    a cgroup CPU quota when one is set (a GPU lease's CPU share: the affinity
+    mask there lists the whole machine, and threads beyond the quota only
+    time-slice)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, period = open(path).read().split()[:2]
+            if q != "max":
+                quota = max(1, -(-int(q) // int(period)))
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, -(-q // period))
+        except (OSError, ValueError):
+            pass
+    n = min(aff, quota) if quota else aff
+    return n, f"affinity {aff} CPUs" + (f", cgroup CPU quota {quota}" if quota else ", no cgroup CPU quota")
+
+
 def cpu_baseline(G, N, K, seconds: float):
     """The oracle (C restatement of torch_impl step + WindowedGridView) on host
     cores, bounded sample; 'port' baseline (the same workload
     with a static env partition over the host threads, plus a 1-thread figure)."""
     from oracle.oracle import Params, rollout
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads, cpu_note = host_cpus()  # every host core this process may use (SURVEY.md §8 D4)
     p = Params(side=G, n_drones=N)
-    E = 4096
+    E = max(4096, 128 * threads)
 
     def timed(envs, steps, nthreads):
         t0 = time.perf_counter()
@@ -147,6 +231,7 @@ def cpu_baseline(G, N, K, seconds: float):
     return {"value": E * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"{E} envs x {steps} steps of reset + step()+obs(K={K}) at {G}x{G}/{N} drones, "
                       f"{threads} host threads (static env partition), {dt:.1f}s wall",
+            "cores_basis": cpu_note,
             "single_thread_value": e1 * s1 / d1,
             "single_thread_sample": f"{e1} envs x {s1} steps, 1 thread, {d1:.1f}s wall",
             "cpu_model": cpu_model()}
@@ -392,7 +477,17 @@ def main():
                     help="write the per-step observation with cached stores (default: streaming, DRL_STEP_OBS_STREAM)")
     ap.add_argument("--obs-k", type=int, default=-1,
                     help="diagnostic: observed drones per step (default: the config's; 0 = step without obs)")
+    ap.add_argument("--cached-steps", type=int, default=200,
+                    help="also time this many steps with cached observation stores (the drop-in env.step() "
+                         "default) and report them under `cached_obs` (0 = skip)")
+    ap.add_argument("--no-pmc-traffic", action="store_true",
+                    help="do not run the rocprofv3 FETCH_SIZE / WRITE_SIZE passes for roofline.traffic")
     args = ap.parse_args()
+
+    traffic_run = None
+    if (not args.no_pmc_traffic and int(os.environ.get("WORLD_SIZE", "1")) == 1
+            and os.environ.get("DRL_BENCH_PMC", "1") != "0"):
+        traffic_run = measure_traffic(args)  # child processes, before this one touches the GPU
 
     rank, world, local = dist_init()
     if world != args.gpus and rank == 0:
@@ -470,6 +565,37 @@ def main():
     achieved = E * R / launch_s / 1e9
     achieved_rw = E * (R + Wb) / launch_s / 1e9
 
+    # the drop-in path: env.step()'s default cached observation stores (a
+    # consumer such as the act kernel reads the observation right away)
+    cached = None
+    if args.cached_steps > 0 and K > 0 and not args.obs_cached:
+        flags_main = flags
+        flags = 0
+        nc = min(args.cached_steps, args.steps)
+        for t in range(min(args.warmup, 20)):
+            run(t)
+        torch.cuda.synchronize()
+        barrier(world)
+        torch.cuda.synchronize()
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        tc = time.perf_counter()
+        c0.record(stream)
+        for t in range(args.warmup, args.warmup + nc):
+            run(t)
+        c1.record(stream)
+        torch.cuda.synchronize()
+        barrier(world)
+        torch.cuda.synchronize()
+        cwall = max_over_ranks(time.perf_counter() - tc, world)
+        env.check_errors()
+        flags = flags_main
+        c_launch = c0.elapsed_time(c1) / 1e3 / nc
+        cached = {"value": E * world * nc / cwall, "unit": "env-steps/s", "steps": nc,
+                  "ms_per_step": cwall / nc * 1e3, "avg_launch_us": c_launch * 1e6,
+                  "frac": E * algorithmic_bytes(G, N, K, W)[0] / c_launch / 1e9 / PEAK_HBM_GBS,
+                  "note": "env.step() / drl_step default (cached observation stores): what a train_jax-style "
+                          "caller whose policy reads the observation next gets"}
+
     # resets (train_jax.py:101-113 resets every 100 steps in C5): timed separately
     resets_per_s = None
     if not args.no_reset_bench:
@@ -508,7 +634,14 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(G, N, K, args.cpu_seconds)
 
-    traffic = load_traffic(args.config)
+    traffic_src = None
+    if traffic_run is not None:
+        traffic, traffic_src = traffic_run["bytes_per_launch"], traffic_run
+    else:
+        traffic = load_traffic(args.config)
+        if traffic is not None:
+            traffic_src = {"source": f"committed profiles/pmc_{args.config}.json (an earlier run; no rocprofv3 pass "
+                                     "in this one)"}
     if rank == 0:
         with open(os.path.join(REPO, "BASELINE.json")) as f:
             metric = json.load(f)["metric"]
@@ -543,7 +676,9 @@ def main():
                                  "algorithmic bytes at the HBM peak would score frac_ceiling = R / (R + W). W counts "
                                  "a full ground write-back but the kernel writes only the changed cells, so the "
                                  "read+write figure can exceed the peak at large grids (C5). Measured HBM bytes "
-                                 "per launch: traffic"},
+                                 "per launch: traffic",
+                         "traffic_detail": traffic_src},
+            "cached_obs": cached,
             "cpu_baseline": cpu,
             "resets_per_s": resets_per_s,
             "dqn_consumer": dqn,

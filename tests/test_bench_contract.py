@@ -49,12 +49,13 @@ def test_cpu_baseline_record():
     rec = bench.cpu_baseline(8, 4, 1, seconds=0.4)
     assert rec["kind"] == "port" and rec["unit"] == "env-steps/s"
     assert rec["value"] > 0 and rec["single_thread_value"] > 0
-    assert 1 <= rec["cores"] <= 16
+    assert rec["cores"] == bench.host_cpus()[0] <= len(os.sched_getaffinity(0))  # the lease's CPUs (§8 D4)
+    assert "affinity" in rec["cores_basis"]
     assert "envs x" in rec["sample"]
 
 
 def test_cli_help_lists_contract_flags():
     out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--help"], capture_output=True,
                          text=True, timeout=120, check=True).stdout
-    for flag in ("--gpus", "--steps", "--warmup", "--config"):
+    for flag in ("--gpus", "--steps", "--warmup", "--config", "--cached-steps", "--no-pmc-traffic"):
         assert flag in out

@@ -1,0 +1,133 @@
+"""Full-size parity against the oracle over EVERY env.
+
+1. C3 / C4 / C5 per-GPU shares (65,536 / 65,536 / 131,072 envs): the HIP
+   path and the threaded oracle rollout (oracle/dronerl_oracle.c
+   orc_rollout: random.seed(123 + g), torch_impl reset, synthetic actions)
+   run the same steps; the final state of every env (ground, dict order,
+   positions, charge, carry, all 625 MT words) is compared bit for bit, with
+   every env's done count and reward sum.  Size-independent invariants are
+   checked over every env as well.
+2. The C5 scan-style train-loop segment (train_jax.py:38-115, reset every
+   100 steps :359): per step, synthetic actions for drones 1..N-1 plus the
+   epsilon-greedy DQN action of drone 0 (one drl_qnet_act_synth launch),
+   step + fused obs(K=1), replay add_many of the drone-0 transition; after
+   100 steps a reset of every env and its observation.  The oracle is driven
+   by the kernel's actions; env state, rewards, dones and the observation are
+   compared every step, and the replay ring at the end against the ring the
+   oracle's transitions give.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.oracle import OracleMulti, Params as OParams, rollout
+from tests.test_gpu_parity import EnvParams, Env, assert_rewards, assert_state, gpu_state, oparams
+
+pytestmark = pytest.mark.gpu
+
+THREADS = max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+@pytest.mark.parametrize("cfg,E,steps", [
+    (dict(n_drones=8, grid_size=16), 65536, 200),       # C3 on one GPU
+    (dict(n_drones=16, grid_size=32), 65536, 100),      # C4 per-GPU share (262144 / 4)
+    (dict(n_drones=32, grid_size=64), 131072, 60),      # C5 per-GPU share (2**20 / 8)
+])
+def test_full_size_every_env_matches_oracle(cfg, E, steps):
+    p = EnvParams(**cfg)
+    N, G = p.n_drones, p.side
+    env = Env(p, E)
+    env.reset(seed=123)
+    rsum = torch.zeros(E, dtype=torch.float64, device=env.device)
+    dsum = torch.zeros(E, dtype=torch.int64, device=env.device)
+    for t in range(steps):
+        r, dn = env.step(env.synth_actions(seed=77, step=t))
+        rsum += r.double().sum(1)
+        dsum += dn.sum(1)
+    torch.cuda.synchronize()
+    env.check_errors()
+    o = rollout(oparams(p), E, steps, seed0=123, action_seed=77, nthreads=THREADS)
+    assert_state(gpu_state(env), o, f"{G}x{G}/{N}, {E} envs x {steps} steps")
+    np.testing.assert_array_equal(dsum.cpu().numpy(), o["done_sum"])
+    assert np.abs(rsum.cpu().numpy() - o["reward_sum"]).max() <= steps * N * 1e-6
+    # size-independent invariants over every env
+    d = env.decode()
+    gr = d["ground"]
+    cnt = lambda v: (gr == v).sum(dim=(1, 2))  # noqa: E731
+    assert torch.all(cnt(2) == 3 * N) and torch.all(cnt(3) == 2 * N) and torch.all(cnt(4) == 2 * N)
+    assert torch.all(cnt(5) + d["carrying"].sum(1) == 3 * N)
+    cells = d["y"].long() * G + d["x"].long()
+    assert torch.all(cells.sort(1).values.diff(dim=1) > 0)  # distinct cells
+    assert not (torch.gather(gr.view(E, -1), 1, cells) == 2).any()
+    assert torch.all((d["charge"] >= 1) & (d["charge"] <= 100))
+    assert torch.all(d["order"].sort(1).values == torch.arange(N, device=env.device))
+    assert torch.all(d["mt_index"] <= 624)
+
+
+@pytest.mark.parametrize("E,seg", [(4096, 100)])
+def test_c5_train_loop_segment_matches_oracle(E, seg):
+    from dronerl_amd.dqn import QNetwork, ReplayBuffer
+    p = EnvParams(n_drones=32, grid_size=64)
+    N = p.n_drones
+    dev = torch.device("cuda:0")
+    env = Env(p, E)
+    env.reset(seed=3)
+    o = OracleMulti(oparams(p), E)
+    o.reset(3 + np.arange(E))
+    W = env.layout.obs_window
+    D = W * W * 6
+    net = QNetwork(D, (128, 64), device=dev, generator=torch.Generator().manual_seed(0))
+    cap = 10000
+    rb = ReplayBuffer(cap, D, dev)
+    obs = [torch.empty((E, 1, W, W, 6), device=dev) for _ in range(2)]
+    acts = torch.empty((E, N), dtype=torch.int32, device=dev)
+    rew = torch.empty((E, N), device=dev)
+    don = torch.empty((E, N), dtype=torch.uint8, device=dev)
+    env.get_obs(1, out=obs[0])
+    np.testing.assert_array_equal(obs[0].cpu().numpy(), o.obs(3, 1), err_msg="first obs")
+    hist = {}  # drone-0 transitions of the steps the ring keeps, from the oracle
+    t_keep = (seg * E - cap) // E
+    o_prev = o.obs(3, 1)
+    for t in range(seg):
+        cur, nxt = obs[t & 1], obs[(t + 1) & 1]
+        net.act(cur.reshape(E, -1), 0.1, seed=7, step=t, actions=acts, synth=(2024, t))
+        env.step(acts, obs_k=1, rewards=rew, dones=don, obs=nxt)
+        rb.add_many(cur, acts, rew, nxt, don)
+        a = acts.cpu().numpy()
+        # drones 1..N-1 follow the synthetic stream; drone 0 the policy
+        np.testing.assert_array_equal(a[:, 1:], env.synth_actions(seed=2024, step=t).cpu().numpy()[:, 1:])
+        assert ((a[:, 0] >= 0) & (a[:, 0] < 5)).all()
+        ro, do = o.step(a, nthreads=THREADS)
+        ctx = f"C5 loop step {t}"
+        assert_rewards(rew.cpu().numpy(), ro, ctx)
+        np.testing.assert_array_equal(don.cpu().numpy().astype(bool), do, err_msg=ctx)
+        o_next = o.obs(3, 1)
+        np.testing.assert_array_equal(nxt.cpu().numpy(), o_next, err_msg=f"{ctx} obs")
+        if t % 10 == 9 or t == seg - 1:
+            assert_state(gpu_state(env), o.state(), ctx)
+        if t >= t_keep:
+            hist[t] = (o_prev.reshape(E, -1), a[:, 0].copy(), ro[:, 0].astype(np.float32), o_next.reshape(E, -1),
+                       do[:, 0])
+        o_prev = o_next
+    env.check_errors()
+    # replay ring (buffers.py:57-80): transition i (step i // E, env i % E) in slot i % cap, later writes win
+    torch.cuda.synchronize()
+    assert rb.cursor == (seg * E) % cap and rb.size == cap
+    first = seg * E - cap
+    slots = np.arange(first, seg * E)
+    tt, ee = slots // E, slots % E
+    want_obs = np.stack([hist[t][0][e] for t, e in zip(tt, ee)])
+    want_next = np.stack([hist[t][3][e] for t, e in zip(tt, ee)])
+    order = slots % cap
+    np.testing.assert_array_equal(rb.obs.cpu().numpy()[order], want_obs)
+    np.testing.assert_array_equal(rb.next_obs.cpu().numpy()[order], want_next)
+    np.testing.assert_array_equal(rb.actions.cpu().numpy()[order], [hist[t][1][e] for t, e in zip(tt, ee)])
+    np.testing.assert_array_equal(rb.rewards.cpu().numpy()[order], [hist[t][2][e] for t, e in zip(tt, ee)])
+    np.testing.assert_array_equal(rb.dones.cpu().numpy()[order].astype(bool), [hist[t][4][e] for t, e in zip(tt, ee)])
+    # reset_env_every: a reset of every env continuing each stream, then its observation
+    env.reset(seed=None)
+    o.reset(None)
+    assert_state(gpu_state(env), o.state(), "C5 loop reset")
+    np.testing.assert_array_equal(env.get_obs(1).cpu().numpy(), o.obs(3, 1), err_msg="C5 loop reset obs")

@@ -2,8 +2,6 @@
 writes through a raw pointer is checked before the launch, seeds outside the
 u64 key range the C ABI takes are refused, and an MT index outside CPython's
 setstate range [0, 624] is refused (Python) or clamped and flagged (C ABI)."""
-import random
-
 import pytest
 import torch
 
@@ -31,15 +29,18 @@ def test_negative_and_oversized_seeds_rejected(env):
     env.reset(seed=0)
 
 
-def test_seed_matches_cpython_at_two_word_keys(env):
-    """seed + g up to 2**64 - 1 is a two-word init_by_array key in CPython."""
+def test_seed_matches_oracle_at_two_word_keys(env):
+    """seed + g near 2**64 is a two-word init_by_array key in CPython; the
+    oracle's MT is pinned there against CPython (test_oracle_golden)."""
+    import numpy as np
+    from oracle.oracle import OracleMulti, Params
     base = 2**64 - 16
     env.reset(seed=base)
-    w = env.mt_words()
-    for g in (0, 7, 15):
-        random.seed(base + g)
-        st = random.getstate()[1]
-        assert [int(v) for v in w[g].tolist()] == list(st), g
+    o = OracleMulti(Params(side=8, n_drones=4), 16)
+    o.reset(np.arange(16, dtype=np.uint64) + np.uint64(base))
+    st = o.state()
+    np.testing.assert_array_equal(env.mt_words().numpy().astype(np.uint32), st["mt"])
+    np.testing.assert_array_equal(env.decode()["ground"].cpu().numpy(), st["ground"])
     env.reset(seed=0)
 
 

@@ -20,7 +20,7 @@ from oracle.oracle import MT, OracleEnv, Params
 from tests._golden import load_ref_tests, load_traj, oracle_params, traj_names
 
 
-@pytest.mark.parametrize("seed", [0, 1, 7, 845, 2**31 - 1, 2**32, 2**40 + 3])
+@pytest.mark.parametrize("seed", [0, 1, 7, 845, 2**31 - 1, 2**32, 2**40 + 3, 2**64 - 16, 2**64 - 1])
 def test_mt_matches_cpython(seed):
     r, m = random.Random(seed), MT(seed)
     assert [r.getrandbits(32) for _ in range(1500)] == [m.genrand() for _ in range(1500)]
