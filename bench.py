@@ -269,6 +269,17 @@ def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream)
     ev[3].record(stream)
     torch.cuda.synchronize()
     env.check_errors()
+    # the same act with the reference's f32 numerics (DRL_QNET_F32)
+    net32 = QNetwork(D, (128, 64), device=env.device, generator=torch.Generator().manual_seed(0), precision="f32")
+    for t in range(warmup):
+        net32.act(flat, 0.1, seed=1, step=t, actions=a0)
+    f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    f0.record(stream)
+    for t in range(steps):
+        net32.act(flat, 0.1, seed=1, step=t, actions=a0)
+    f1.record(stream)
+    torch.cuda.synchronize()
+    act32_s = f0.elapsed_time(f1) / 1e3 / steps
     act_s = ev[0].elapsed_time(ev[1]) / 1e3 / steps
     loop_s = ev[2].elapsed_time(ev[3]) / 1e3 / steps
     read = E * D * 4
@@ -276,6 +287,11 @@ def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream)
             "act_roofline": {"bound": "hbm", "achieved": read / act_s / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": read / act_s / 1e9 / PEAK_HBM_GBS,
                              "algorithmic_bytes_per_env": D * 4 + 4},
+            "act_f32_us": act32_s * 1e6,
+            "act_f32_roofline": {"bound": "hbm", "achieved": read / act32_s / 1e9, "peak": PEAK_HBM_GBS,
+                                 "unit": "GB/s", "frac": read / act32_s / 1e9 / PEAK_HBM_GBS},
+            "act_f32_note": "precision='f32' (DRL_QNET_F32): fp16 hi/lo split operands, 3 MFMAs per product tile, "
+                            "Q to f32 rounding (the reference's f32 nets)",
             "loop_us_per_step": loop_s * 1e6, "loop_env_steps_per_s": E / loop_s,
             "loop": "act(obs_t) -> step + obs(K=1) -> replay add_many(obs_t, a, r, obs_t+1, done), capacity 10000"}
 

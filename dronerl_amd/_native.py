@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # DRL_LIB: an alternative build of the same library (tools/variants.py A/B runs)
 LIB_PATH = os.environ.get("DRL_LIB") or os.path.join(_HERE, "libdronerl.so")
 
+DRL_ABI_VERSION = 3  # include/dronerl.h
 DRL_MT_WORDS = 640
 DRL_MAX_DRONES = 64
 DRL_MAX_SIDE = 128
@@ -109,7 +110,7 @@ def lib():
     for f in ["drl_layout_query", "drl_reset", "drl_step", "drl_step_ex", "drl_rollout", "drl_obs", "drl_grid_obs", "drl_decode", "drl_encode",
               "drl_synth_actions"]:
         getattr(L, f).restype = ctypes.c_int
-    if L.drl_abi_version() != 2:
+    if L.drl_abi_version() != DRL_ABI_VERSION:
         raise DroneRLError("libdronerl.so ABI version mismatch; rebuild it")
     _lib = L
     return L

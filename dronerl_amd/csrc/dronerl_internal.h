@@ -170,7 +170,10 @@ struct QnetLayout {
     int bias_off[QN_MAX_LAYERS];  // float offset of the layer's biases (padded to 16 * nt)
     int frag_total;               // uint4s of fragments
     int n_bias;                   // floats of biases
-    int lds_vec;                  // uint4s of the whole packed net
+    int lds_vec;                  // uint4s of the LDS image (fragments + biases)
+    int precision;                // DRL_QNET_BF16 / DRL_QNET_F32
+    int frag_lo_off[QN_MAX_LAYERS];  // F32: uint4 offset of the layer's lo fragments (after the LDS image)
+    int total_vec;                // uint4s of the whole packed net
 };
 
 struct QnetPack {
@@ -180,15 +183,18 @@ struct QnetPack {
     const float* w[QN_MAX_LAYERS];
     const float* b[QN_MAX_LAYERS];
     int64_t n_wfrag_elems, n_bias;
-    uint16_t* packed_w;  // bf16 bits
+    uint16_t* packed_w;  // bf16 bits (F32: fp16 hi bits)
     float* packed_b;
+    int precision;
+    int frag_lo_off[QN_MAX_LAYERS];  // F32: lo fragments, uint4 offsets from packed_w
 };
 
 struct QnetArgs {
-    int in_features, kt0, n_hidden, n_actions;
+    int in_features, kt0, n_hidden, n_actions, precision;
     int nt[QN_MAX_LAYERS];
     int frag_off[QN_MAX_LAYERS], bias_off[QN_MAX_LAYERS];
     int frag_total, lds_vec, n_bias;
+    int frag_lo_off[QN_MAX_LAYERS];  // F32: lo fragments in global memory (uint4 offsets from packed)
     const uint4* packed;
     const float* obs;
     int64_t obs_stride, E;

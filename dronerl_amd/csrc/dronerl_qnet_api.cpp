@@ -29,7 +29,10 @@ int qnet_layout(const drl_qnet_desc* d, drl::QnetLayout* L) {
         if (d->hidden[i] < 32 || d->hidden[i] > 128 || d->hidden[i] % 32)
             return fail("hidden widths must be multiples of 32 in [32, 128]");
     if (d->n_actions < 1 || d->n_actions > 8) return fail("n_actions must be in [1, 8]");
+    if (d->precision != DRL_QNET_BF16 && d->precision != DRL_QNET_F32)
+        return fail("precision must be DRL_QNET_BF16 or DRL_QNET_F32");
     memset(L, 0, sizeof *L);
+    L->precision = d->precision;
     L->n_layers = d->n_hidden + 1;
     int frag = 0, bias = 0;
     for (int l = 0; l < L->n_layers; ++l) {
@@ -47,6 +50,18 @@ int qnet_layout(const drl_qnet_desc* d, drl::QnetLayout* L) {
     L->frag_total = frag * 64;
     L->n_bias = bias;
     L->lds_vec = L->frag_total + (bias + 3) / 4;
+    if (d->precision == DRL_QNET_F32) {
+        // lo fragments: the hidden and output layers' after the biases (LDS
+        // image), layer 0's after the image (read from global memory / L2)
+        for (int l = 1; l < L->n_layers; ++l) {
+            L->frag_lo_off[l] = L->lds_vec;
+            L->lds_vec += L->nt[l] * L->kt[l] * 64;
+        }
+        L->frag_lo_off[0] = L->lds_vec;
+        L->total_vec = L->lds_vec + L->nt[0] * L->kt[0] * 64;
+    } else {
+        L->total_vec = L->lds_vec;
+    }
     if (L->lds_vec * 16 > kQnetLdsMax) return fail("the packed network does not fit the 160 KB LDS of a CU");
     return 0;
 }
@@ -79,7 +94,7 @@ int drl_qnet_packed_bytes(const drl_qnet_desc* d, int64_t* bytes) {
     drl::QnetLayout L;
     if (qnet_layout(d, &L)) return -1;
     if (!bytes) return fail("bytes is NULL");
-    *bytes = (int64_t)L.lds_vec * 16;
+    *bytes = (int64_t)L.total_vec * 16;
     return 0;
 }
 
@@ -102,6 +117,8 @@ int drl_qnet_pack(const drl_qnet_desc* d, const float* const* d_weights, const f
         p.w[l] = d_weights[l];
         p.b[l] = d_biases[l];
     }
+    p.precision = L.precision;
+    for (int l = 0; l < L.n_layers; ++l) p.frag_lo_off[l] = L.frag_lo_off[l];
     p.n_wfrag_elems = (int64_t)L.frag_total * 8;
     p.n_bias = L.n_bias;
     p.packed_w = static_cast<uint16_t*>(d_packed);
@@ -134,7 +151,9 @@ static int qnet_act_impl(const drl_qnet_desc* d, const void* d_packed, const flo
         a.nt[l] = L.nt[l];
         a.frag_off[l] = L.frag_off[l];
         a.bias_off[l] = L.bias_off[l];
+        a.frag_lo_off[l] = L.frag_lo_off[l];
     }
+    a.precision = L.precision;
     a.frag_total = L.frag_total;
     a.lds_vec = L.lds_vec;
     a.n_bias = L.n_bias;

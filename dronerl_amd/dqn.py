@@ -24,9 +24,13 @@ from ._native import DroneRLError, lib
 NUM_ACTIONS = 5  # common/constants.py Action
 
 
+DRL_QNET_BF16, DRL_QNET_F32 = 0, 1  # include/dronerl.h
+PRECISIONS = {"bf16": DRL_QNET_BF16, "f32": DRL_QNET_F32}
+
+
 class DrlQnetDesc(ctypes.Structure):
     _fields_ = [("in_features", ctypes.c_int32), ("n_hidden", ctypes.c_int32),
-                ("hidden", ctypes.c_int32 * 3), ("n_actions", ctypes.c_int32)]
+                ("hidden", ctypes.c_int32 * 3), ("n_actions", ctypes.c_int32), ("precision", ctypes.c_int32)]
 
 
 class DrlReplay(ctypes.Structure):
@@ -74,12 +78,22 @@ def _stream(device):
 
 
 class QNetwork:
-    """Dense Q-network: in_features -> hidden... (ReLU) -> n_actions."""
+    """Dense Q-network: in_features -> hidden... (ReLU) -> n_actions.
+
+    precision "bf16": bf16 MFMA operands, f32 accumulation (Q to ~1e-2
+    relative).  "f32": the reference's f32 nets (jax dqn.py:47-63, torch
+    dqn.py:44-82): split fp16 hi/lo operands, three MFMAs per product tile,
+    Q to f32 rounding (include/dronerl.h DRL_QNET_F32)."""
 
     def __init__(self, in_features: int, hidden: Sequence[int] = (32, 32), n_actions: int = NUM_ACTIONS,
-                 device=None, generator: Optional[torch.Generator] = None):
+                 device=None, generator: Optional[torch.Generator] = None, precision: str = "bf16"):
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
+        self.precision = precision
         self.L = _bind(lib())
         self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.in_features, self.hidden, self.n_actions = in_features, tuple(hidden), n_actions
         sizes = [in_features, *self.hidden, n_actions]
         self.weights, self.biases = [], []
@@ -91,7 +105,7 @@ class QNetwork:
             self.weights.append(w.to(self.device))
             self.biases.append(torch.zeros(sizes[i + 1], device=self.device))
         self.desc = DrlQnetDesc(in_features, len(self.hidden), (ctypes.c_int32 * 3)(*self.hidden, *[0] * (3 - len(self.hidden))),
-                                n_actions)
+                                n_actions, PRECISIONS[precision])
         nb = ctypes.c_int64()
         _check(self.L, self.L.drl_qnet_packed_bytes(ctypes.byref(self.desc), ctypes.byref(nb)))
         self.packed = torch.empty(nb.value // 4, dtype=torch.int32, device=self.device)  # 16-B aligned
@@ -109,6 +123,10 @@ class QNetwork:
         self.pack()
 
     def pack(self):
+        if self.precision == "f32":  # fp16 hi/lo split range (include/dronerl.h DRL_QNET_F32)
+            for w, b in zip(self.weights, self.biases):
+                if not bool(torch.isfinite(w).all()) or float(w.abs().max()) >= 65504.0:
+                    raise ValueError("f32 precision needs finite weights with |w| < 65504")
         n = len(self.weights)
         wp = (_vp * n)(*[w.data_ptr() for w in self.weights])
         bp = (_vp * n)(*[b.data_ptr() for b in self.biases])

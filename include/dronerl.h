@@ -46,7 +46,7 @@ extern "C" {
 
 typedef struct ihipStream_t* hipStream_t;
 
-#define DRL_ABI_VERSION 2
+#define DRL_ABI_VERSION 3
 #define DRL_MT_WORDS 640     /* per-env MT19937 row: words 0..623 state (row padded to 2560 B) */
 #define DRL_MAX_DRONES 64
 #define DRL_MAX_SIDE 128
@@ -247,20 +247,34 @@ int drl_env_state(const drl_env* env, drl_state* s, drl_params* p, drl_layout* L
 int drl_env_errors(drl_env* env, int32_t* flags, int32_t clear, hipStream_t stream);
 
 /* ------------------------------------------------------------------------
- * DQN consumer of the observation, on MFMA (bf16 operands,
- * f32 accumulate): the dense Q-network of jax_impl/agents/dqn.py:47-63
+ * DQN consumer of the observation, on MFMA: the dense Q-network of jax_impl/agents/dqn.py:47-63
  * (Dense(h) + ReLU per hidden layer, then Dense(n_actions)) and the
  * epsilon-greedy act of dqn.py:132-146 for every env (train_jax.py:42-49:
  * drone 0 follows the agent), plus ReplayBuffer.add_many (buffers.py:57-80).
+ *
+ * Precision (drl_qnet_desc.precision):
+ *   DRL_QNET_BF16: bf16 operands, f32 accumulation (one MFMA per tile and
+ *     K-slice); Q within ~1e-2 relative of the f32 forward.
+ *   DRL_QNET_F32: the reference's f32 nets (jax dqn.py:47-63 / torch
+ *     dqn.py:44-82 run in f32): every operand v is split exactly enough into
+ *     fp16 hi = fp16(v) and lo = fp16((v - hi) * 2^11); products hi*hi go to
+ *     one f32 accumulator and hi*lo + lo*hi to a second, combined as
+ *     acc_hi + 2^-11 * acc_lo (the lo*lo term, <= 2^-22 relative, is
+ *     dropped).  Q matches an f32 forward to f32 rounding (~1e-6 relative).
+ *     Range: |weights|, |inputs| and |hidden activations| < 65504 (fp16).
  * ------------------------------------------------------------------------ */
+#define DRL_QNET_BF16 0
+#define DRL_QNET_F32 1
 typedef struct drl_qnet_desc {
     int32_t in_features;  /* observation floats, W*W*6 (even, <= 512) */
     int32_t n_hidden;     /* 1..3 hidden layers */
     int32_t hidden[3];    /* widths: multiples of 32 in [32, 128] */
     int32_t n_actions;    /* 1..8 (Action.num_actions() = 5) */
+    int32_t precision;    /* DRL_QNET_BF16 or DRL_QNET_F32 */
 } drl_qnet_desc;
 
-/* Bytes of the packed network (bf16 weight fragments + f32 biases). */
+/* Bytes of the packed network (weight fragments + f32 biases; DRL_QNET_F32
+ * packs fp16 hi fragments where bf16 ones go, then the lo fragments). */
 int drl_qnet_packed_bytes(const drl_qnet_desc* d, int64_t* bytes);
 /* Pack the network once per weight update.  d_weights / d_biases: host arrays
  * of n_hidden + 1 device pointers; layer l weights f32 [out][in] row-major

@@ -19,10 +19,10 @@ Q_TOL_BF16 = 2e-2   # |Q - Q_ref(bf16 operands)| <= tol * (1 + |Q_ref|): f32 sum
 Q_TOL_F32 = 8e-2    # vs the plain fp32 forward (bf16 operand rounding)
 
 
-def _desc(in_features, hidden, n_actions=5):
+def _desc(in_features, hidden, n_actions=5, precision=0):
     from dronerl_amd.dqn import DrlQnetDesc
     h = list(hidden) + [0] * (3 - len(hidden))
-    return DrlQnetDesc(in_features, len(hidden), (ctypes.c_int32 * 3)(*h), n_actions)
+    return DrlQnetDesc(in_features, len(hidden), (ctypes.c_int32 * 3)(*h), n_actions, precision)
 
 
 @pytest.mark.parametrize("inf,hidden,ok", [
@@ -50,6 +50,13 @@ def test_qnet_packed_size_formula():
     frags = 8 * 10 + 4 * 4 + 1 * 2          # (16-row tiles x 32-wide K-slices) per layer, 1 KB each
     biases = (128 + 64 + 16) * 4
     assert nb.value == frags * 1024 + biases
+    # DRL_QNET_F32: fp16 hi fragments, biases, the later layers' lo fragments (the LDS image), then layer 0's lo
+    assert L.drl_qnet_packed_bytes(ctypes.byref(_desc(294, (128, 64), precision=1)), ctypes.byref(nb)) == 0
+    assert nb.value == 2 * frags * 1024 + biases
+    assert L.drl_qnet_packed_bytes(ctypes.byref(_desc(294, (128, 64), precision=2)), ctypes.byref(nb)) != 0
+    assert b"precision" in L.drl_last_error()
+    # hi + lo fragments of three 128-wide hidden layers exceed the LDS in f32 mode
+    assert L.drl_qnet_packed_bytes(ctypes.byref(_desc(294, (128, 128, 128), precision=1)), ctypes.byref(nb)) != 0
 
 
 def _hash_explore(seed, step, genv, n_actions, eps):
@@ -104,6 +111,51 @@ def test_qnet_greedy_matches_torch_reference(hidden, E):
     assert torch.equal(a[safe, 0].long(), torch.argmax(ref, dim=1)[safe])
 
 
+# DRL_QNET_F32 (the reference's f32 nets): Q against an f32 forward, relative
+# to the row's scale, and the greedy action against the f32 argmax everywhere.
+Q_TOL_EXACT = 1e-5
+
+
+@gpu
+@pytest.mark.parametrize("hidden,E", [((128, 64), 65536), ((128, 64), 1000), ((32, 32), 4096), ((64,), 31),
+                                      ((96, 32), 4096), ((128, 128), 333), ((64, 64, 32), 4096)])
+def test_qnet_f32_matches_fp32_forward(hidden, E):
+    from dronerl_amd.dqn import QNetwork
+    obs, _ = _obs_batch(E)
+    g = torch.Generator().manual_seed(len(hidden) * 1000 + E)
+    net = QNetwork(obs.shape[1], hidden, generator=g, precision="f32")
+    for b in net.biases:
+        b.normal_(0, 0.1, generator=None)
+    net.pack()
+    q = torch.empty((E, 5), device="cuda")
+    a = net.act(obs, epsilon=0.0, q_out=q)
+    # f32 forward on the host (plain IEEE f32 matmuls) and an f64 one
+    x = obs.cpu()
+    ref32, ref64 = x.clone(), x.double()
+    for i, (w, b) in enumerate(zip(net.weights, net.biases)):
+        ref32 = ref32 @ w.cpu().t() + b.cpu()
+        ref64 = ref64 @ w.cpu().double().t() + b.cpu().double()
+        if i < len(net.weights) - 1:
+            ref32, ref64 = torch.relu(ref32), torch.relu(ref64)
+    qc = q.cpu()
+    scale = 1.0 + ref32.abs().amax(dim=1, keepdim=True)
+    err = ((qc - ref32).abs() / scale).max().item()
+    assert err <= Q_TOL_EXACT, err
+    assert ((qc.double() - ref64).abs() / scale.double()).max().item() <= Q_TOL_EXACT
+    # greedy action == torch.argmax of the f32 reference (first maximum) on every env
+    assert torch.equal(a[:, 0].cpu().long(), torch.argmax(ref32, dim=1))
+
+
+@gpu
+def test_qnet_f32_weight_range_checked():
+    from dronerl_amd.dqn import QNetwork
+    net = QNetwork(294, (32,), precision="f32")
+    w = [t.clone() for t in net.weights]
+    w[0][0, 0] = 70000.0
+    with pytest.raises(ValueError, match="65504"):
+        net.load(w, net.biases)
+
+
 @gpu
 def test_qnet_exploration_stream_and_column_write():
     from dronerl_amd.dqn import QNetwork
@@ -128,14 +180,15 @@ def test_qnet_exploration_stream_and_column_write():
 
 
 @gpu
+@pytest.mark.parametrize("precision", ["bf16", "f32"])
 @pytest.mark.parametrize("E,N,off", [(777, 8, 5000), (31, 3, 0), (4096, 32, 123), (100, 1, 7), (65536, 8, 0)])
-def test_qnet_act_synth_equals_synth_then_act(E, N, off):
+def test_qnet_act_synth_equals_synth_then_act(E, N, off, precision):
     """drl_qnet_act_synth == drl_synth_actions followed by drl_qnet_act (the
     fused launch of bench.TrainSegment), Q included."""
     from dronerl_amd import _native
     from dronerl_amd.dqn import QNetwork
     obs, env = _obs_batch(E)
-    net = QNetwork(obs.shape[1], (128, 64), generator=torch.Generator().manual_seed(11))
+    net = QNetwork(obs.shape[1], (128, 64), generator=torch.Generator().manual_seed(11), precision=precision)
     ref = torch.empty((E, N), dtype=torch.int32, device="cuda")
     assert _native.lib().drl_synth_actions(2024, 9, off, E, N, ref.data_ptr(),
                                            torch.cuda.current_stream().cuda_stream) == 0

@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--hidden", default="128,64")
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--stride", type=int, default=294, help="obs row stride in floats (296: 16-B aligned rows)")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "f32"])
     args = ap.parse_args()
     if args.lib:
         import dronerl_amd._native as nat
@@ -23,7 +24,8 @@ def main():
     from dronerl_amd.dqn import QNetwork
     E = args.envs
     obs = torch.rand((E, 1, 7, 7, 6), device="cuda")
-    net = QNetwork(294, tuple(int(x) for x in args.hidden.split(",")), generator=torch.Generator().manual_seed(0))
+    net = QNetwork(294, tuple(int(x) for x in args.hidden.split(",")), generator=torch.Generator().manual_seed(0),
+                   precision=args.precision)
     a = torch.zeros((E, 8), dtype=torch.int32, device="cuda")
     flat = obs.reshape(E, -1)
     if args.stride != 294:
@@ -40,7 +42,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / args.iters
-    print(f"{os.path.basename(args.lib) or 'libdronerl.so'} E={E} hidden={args.hidden}: {us:.2f} us/launch, "
+    print(f"{os.path.basename(args.lib) or 'libdronerl.so'} E={E} hidden={args.hidden} {args.precision}: {us:.2f} us/launch, "
           f"{E * 1176 / us / 1e3:.0f} GB/s obs read (row stride {flat.stride(0)} floats)")
 
 
