@@ -1,0 +1,127 @@
+"""Multi-rank runs of the HIP env, on the one-GPU box.
+
+Two processes share cuda:0 over a gloo process group (the driver's
+multi-GPU runs use nccl = RCCL, one device per rank; the data path is the
+same: contiguous env shards with env_offset = rank * E / world, train_jax.py
+:196-212, and one all-reduce of the eval table, :270-319).
+
+1. evaluate_sharded with gpu_episode_runner (greedy DQN for drone 0, f32
+   numerics) on 2 ranks == the one-process table, bit for bit.
+2. Sharded stepping: each rank steps its shard; the concatenated final
+   states == one process stepping every env.
+3. bench.py under torch.distributed.run with 2 ranks (DRL_DIST_BACKEND=gloo)
+   prints one whole-job JSON line.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NUM_EVALS, EVAL_STEPS, EVAL_SEED = 9, 60, 845
+STEP_E, STEP_T = 2048, 40
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _params():
+    from dronerl_amd import EnvParams
+    return EnvParams(n_drones=8, grid_size=16)
+
+
+def _policy():
+    from dronerl_amd.dqn import QNetwork
+    net = QNetwork(294, (128, 64), device="cuda:0", generator=torch.Generator().manual_seed(5), precision="f32")
+
+    def act(obs):
+        a = torch.empty((obs.shape[0], 1), dtype=torch.int32, device=obs.device)
+        net.act(obs.contiguous(), 0.0, actions=a)
+        return a[:, 0]
+    return act
+
+
+def _shard_states(rank, world):
+    from dronerl_amd import BatchedDeliveryDrones
+    from dronerl_amd.distributed import shard_envs
+    sh = shard_envs(STEP_E, rank, world)
+    env = BatchedDeliveryDrones(_params(), sh.num_envs, device="cuda:0", env_offset=sh.env_offset)
+    env.reset(seed=11)
+    for t in range(STEP_T):
+        env.step(env.synth_actions(seed=3, step=t))
+    torch.cuda.synchronize()
+    env.check_errors()
+    d = env.decode()
+    return {k: d[k].cpu().numpy() for k in ("ground", "order", "y", "x", "charge", "carrying", "mt_index")}
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+    from dronerl_amd.distributed import evaluate_sharded, gpu_episode_runner
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        runner = gpu_episode_runner(_params(), EVAL_STEPS, EVAL_SEED, policy=_policy(), device="cuda:0")
+        agent, rnd, table = evaluate_sharded(runner, NUM_EVALS, rank=rank, world=world)
+        out[rank] = (agent, rnd, table.cpu().numpy(), _shard_states(rank, world))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_eval_and_shards_match_one_process():
+    from dronerl_amd.distributed import evaluate_sharded, gpu_episode_runner
+    runner = gpu_episode_runner(_params(), EVAL_STEPS, EVAL_SEED, policy=_policy(), device="cuda:0")
+    ref_agent, ref_rnd, ref_table = evaluate_sharded(runner, NUM_EVALS)
+    ref_states = _shard_states(0, 1)
+    ctx = mp.get_context("spawn")
+    with ctx.Manager() as man:
+        out = man.dict()
+        port = _free_port()
+        procs = [ctx.Process(target=_worker, args=(r, 2, port, out)) for r in range(2)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=300)
+            assert p.exitcode == 0, p.exitcode
+        res = dict(out)
+    for r in range(2):
+        agent, rnd, table, _ = res[r]
+        np.testing.assert_array_equal(table, ref_table.cpu().numpy())
+        assert (agent, rnd) == (ref_agent, ref_rnd)
+    for k, v in ref_states.items():
+        np.testing.assert_array_equal(np.concatenate([res[0][3][k], res[1][3][k]]), v, err_msg=k)
+
+
+def test_bench_two_ranks_gloo_whole_job_json():
+    env = dict(os.environ, DRL_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", DRL_BENCH_PMC="0")
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "20", "--warmup", "5", "--envs", "4096", "--no-cpu-baseline", "--no-dqn",
+           "--no-reset-bench", "--rollout-chunk", "0", "--loop-segments", "0", "--cached-steps", "10"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["steps"] == 20
+    assert d["config"]["num_envs_total"] == 2 * 4096 and d["config"]["parallelism"] == "env-shard x2"
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    # value = every rank's env-steps over the slowest rank's wall time
+    assert d["value"] == pytest.approx(2 * 4096 * 20 / (d["ms_per_step"] * 20 / 1e3), rel=1e-6)
+    assert d["cached_obs"]["value"] > 0
