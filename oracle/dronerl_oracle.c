@@ -296,9 +296,12 @@ int orc_reset(orc_env* e) {
     return 0;
 }
 
-/* env.py:226-233.  mask: 1 = blocked.  Returns the cell. */
-static int32_t find_respawn_position(orc_env* e, const uint8_t* mask) {
+/* env.py:226-233.  mask: 1 = blocked; n_blocked: how many cells are.
+ * Returns the cell, or -1 when every cell is blocked: the reference's loop
+ * would spin forever there (the kernel raises DRL_ERR_NO_FREE_CELL). */
+static int32_t find_respawn_position(orc_env* e, const uint8_t* mask, int32_t n_blocked) {
     const uint32_t G = (uint32_t)e->p.side;
+    if (n_blocked >= (int32_t)(G * G)) return -1;
     for (;;) {
         uint32_t y = orc_randbelow(&e->rng, G); /* randint(0, G-1) */
         uint32_t x = orc_randbelow(&e->rng, G);
@@ -308,7 +311,8 @@ static int32_t find_respawn_position(orc_env* e, const uint8_t* mask) {
 }
 
 /* env.py:112-215.  actions[N] by drone index; rewards[N]/dones[N] by drone
- * index.  Returns 0, or -1 on an action index Python would reject. */
+ * index.  Returns 0, -1 on an action index Python would reject, or -2 when a
+ * respawn finds every cell blocked (the reference loops forever there). */
 int orc_step(orc_env* e, const int32_t* actions, double* rewards, uint8_t* dones) {
     const int32_t G = e->p.side, N = e->p.n_drones, GG = G * G;
     int32_t* new_at = e->scratch;               /* [GG] drone+1 claiming a cell (new_drones) */
@@ -400,8 +404,14 @@ int orc_step(orc_env* e, const int32_t* actions, double* rewards, uint8_t* dones
     e->n_order = no;
 
     /* respawn crashed drones (env.py:186-195); mask = drones | skyscrapers */
-    for (int32_t c = 0; c < GG; c++) mask[c] = (e->ground[c] == OBJ_SKYSCRAPER);
-    for (int32_t q = 0; q < e->n_order; q++) mask[e->pos[e->order[q]]] = 1;
+    int32_t n_blocked = 0;
+    for (int32_t c = 0; c < GG; c++) n_blocked += mask[c] = (e->ground[c] == OBJ_SKYSCRAPER);
+    for (int32_t q = 0; q < e->n_order; q++) {
+        int32_t c = e->pos[e->order[q]];
+        n_blocked += !mask[c];
+        mask[c] = 1;
+    }
+    int no_free = 0;
     for (int32_t t = 0; t < n_crashed; t++) {
         int32_t d = crashed[t];
         e->charge[d] = 100;
@@ -411,24 +421,32 @@ int orc_step(orc_env* e, const int32_t* actions, double* rewards, uint8_t* dones
         }
         rewards[d] = e->p.crash_reward;
         dones[d] = 1;
-        int32_t c = find_respawn_position(e, mask);
+        int32_t c = find_respawn_position(e, mask, n_blocked);
+        if (c < 0) { no_free = 1; break; }
         e->pos[d] = c;
         e->order[e->n_order++] = d;
         mask[c] = 1;
+        n_blocked++;
     }
 
     /* respawn used packets and dropzones (env.py:198-210) */
-    for (int32_t c = 0; c < GG; c++) mask[c] = (e->ground[c] != OBJ_EMPTY);
-    for (int32_t t = 0; t < nb_pack; t++) {
-        int32_t c = find_respawn_position(e, mask);
+    n_blocked = 0;
+    for (int32_t c = 0; c < GG; c++) n_blocked += mask[c] = (e->ground[c] != OBJ_EMPTY);
+    for (int32_t t = 0; t < nb_pack && !no_free; t++) {
+        int32_t c = find_respawn_position(e, mask, n_blocked);
+        if (c < 0) { no_free = 1; break; }
         e->ground[c] = OBJ_PACKET;
         mask[c] = 1;
+        n_blocked++;
     }
-    for (int32_t t = 0; t < nb_drop; t++) {
-        int32_t c = find_respawn_position(e, mask);
+    for (int32_t t = 0; t < nb_drop && !no_free; t++) {
+        int32_t c = find_respawn_position(e, mask, n_blocked);
+        if (c < 0) { no_free = 1; break; }
         e->ground[c] = OBJ_DROPZONE;
         mask[c] = 1;
+        n_blocked++;
     }
+    if (no_free) return -2; /* the reference never returns from this step */
 
     pick_packets_after_respawn(e);
     return 0;
@@ -659,7 +677,10 @@ static void* multi_step_worker(void* arg) {
     const int32_t N = j->m->p.n_drones;
     j->status = 0;
     for (int64_t i = j->e0; i < j->e1; i++)
-        if (orc_step(j->m->envs[i], j->actions + i * N, j->rewards + i * N, j->dones + i * N)) j->status = -1;
+        {
+            int r = orc_step(j->m->envs[i], j->actions + i * N, j->rewards + i * N, j->dones + i * N);
+            if (r && (!j->status || r == -2)) j->status = r;
+        }
     return NULL;
 }
 
@@ -681,7 +702,7 @@ int orc_multi_step(orc_multi* m, const int32_t* actions, double* rewards, uint8_
     int st = 0;
     for (int t = 0; t < nthreads; t++) {
         if (nthreads > 1) pthread_join(th[t], NULL);
-        if (jobs[t].status) st = -1;
+        if (jobs[t].status && (!st || jobs[t].status == -2)) st = jobs[t].status;
     }
     return st;
 }

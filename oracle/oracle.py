@@ -16,7 +16,8 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+# DRL_ORACLE_LIB: another build of the same source (the sanitizer build of `make asan`)
+_LIB_PATH = os.environ.get("DRL_ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
 _lib = None
 
 
@@ -43,11 +44,26 @@ class OrcParams(ctypes.Structure):
     ]
 
 
+class NoFreeCell(RuntimeError):
+    """A respawn found every cell blocked: the reference's
+    _find_respawn_position (env.py:226-233) would loop forever."""
+
+
+def _step_status(st: int):
+    if st == -1:
+        raise IndexError("list index out of range")
+    if st == -2:
+        raise NoFreeCell("respawn found no free cell (the reference loops forever)")
+    if st:
+        raise RuntimeError(f"orc_step failed ({st})")
+
+
 def lib():
     global _lib
     if _lib is None:
         src = os.path.join(_HERE, "dronerl_oracle.c")
-        if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        if not os.environ.get("DRL_ORACLE_LIB") and (not os.path.exists(_LIB_PATH)
+                                                     or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src)):
             build()
         L = ctypes.CDLL(_LIB_PATH)
         vp, i32, i64, u32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64
@@ -190,8 +206,7 @@ class OracleEnv:
         assert a.shape == (N,)
         r = np.zeros(N, dtype=np.float64)
         d = np.zeros(N, dtype=np.uint8)
-        if lib().orc_step(self._e, _ptr(a), _ptr(r), _ptr(d)):
-            raise IndexError("list index out of range")
+        _step_status(lib().orc_step(self._e, _ptr(a), _ptr(r), _ptr(d)))
         return r, d.astype(bool)
 
     def obs(self, radius: int = 3, k: int | None = None) -> np.ndarray:
@@ -297,8 +312,7 @@ class OracleMulti:
         a = np.ascontiguousarray(actions, dtype=np.int32).reshape(self.E, N)
         r = np.zeros((self.E, N), dtype=np.float64)
         d = np.zeros((self.E, N), dtype=np.uint8)
-        if lib().orc_multi_step(self._m, _ptr(a), _ptr(r), _ptr(d), nthreads):
-            raise IndexError("list index out of range")
+        _step_status(lib().orc_multi_step(self._m, _ptr(a), _ptr(r), _ptr(d), nthreads))
         return r, d.astype(bool)
 
     def state(self) -> dict:

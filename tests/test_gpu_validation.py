@@ -117,3 +117,17 @@ def test_bad_action_flag_reported():
     e.step(a)
     with pytest.raises(DroneRLError, match="action"):
         e.check_errors()
+
+
+def test_full_grid_respawn_raises_no_free_cell():
+    """The oracle's NoFreeCell state (tests/test_oracle_golden.py) on the GPU:
+    the kernel bounds the respawn rounds and raises DRL_ERR_NO_FREE_CELL
+    instead of spinning like the reference (env.py:226-233)."""
+    from tests.test_oracle_golden import full_grid_delivery_state
+    st, act = full_grid_delivery_state()
+    e = BatchedDeliveryDrones(EnvParams(n_drones=1, grid_size=4), 1, device="cuda:0")
+    e.reset(seed=0)
+    e.set_state(st["ground"][None], [st["order"]], [st["y"]], [st["x"]], [st["charge"]], [st["packet"]])
+    e.step(torch.tensor([act], dtype=torch.int32, device="cuda:0"))
+    with pytest.raises(DroneRLError, match="no free cell"):
+        e.check_errors()

@@ -247,3 +247,24 @@ def test_charge_div_true_division():
     c = np.arange(0, 101)
     ref = (c.astype(np.float64) / 100).astype(np.float32)
     assert (c.astype(np.float32) / np.float32(100) == ref).all()
+
+
+def full_grid_delivery_state(G=4):
+    """A delivery on a grid whose every other cell holds an object: the packet
+    respawn takes the freed dropzone cell, and the dropzone respawn then finds
+    no free cell, where the reference's _find_respawn_position
+    (env.py:226-233) loops forever.  Drone 0 at (0,0) carries a packet and
+    moves RIGHT onto the dropzone at (0,1)."""
+    ground = np.full((G, G), 3, np.uint8)  # stations everywhere
+    ground[0, 1] = 4                       # one dropzone
+    return dict(ground=ground, order=[0], y=[0], x=[0], charge=[50], packet=[1]), [2]
+
+
+def test_full_grid_respawn_detected_not_hung():
+    from oracle.oracle import NoFreeCell
+    st, act = full_grid_delivery_state()
+    env = OracleEnv(Params(side=4, n_drones=1))
+    env.seed(0)
+    env.set_state(st["ground"], st["order"], st["y"], st["x"], st["charge"], st["packet"])
+    with pytest.raises(NoFreeCell):
+        env.step(np.array(act, np.int32))
