@@ -736,7 +736,11 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     for (int r = 0; r < PFR; ++r)
         if (j + P * r < pfn) mtw[j + P * r] = pfw[r];
     int pf_base = pf_base0;
+#ifdef DRL_DIAG_NO_RESPAWN  // timing-only diagnostic build (wrong results): the step without its respawn rounds
+    int w = total, have_y = 0, yv = 0;
+#else
     int w = 0, have_y = 0, yv = 0;
+#endif
     const int shift = 32 - g.kbits();
     const int my_item = crashed ? newslot - nS : -1;  // this drone's respawn item
     uint32_t rounds = 0;
@@ -749,11 +753,17 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         while (need) {
             const int tl = __ffsll((unsigned long long)need) - 1;
             need &= need - 1ull;
+#if !defined(DRL_DIAG_NO_TWIST) && !defined(DRL_DIAG_TWIST_FREE)  // timing-only builds (wrong streams)
             twist_wave(mt_w + (uint32_t)(tl / P) * MT_WORDS, lane);
+#endif
             if (grp == tl / P) {
                 midx = 0;
                 pf_base = 0;
+#ifdef DRL_DIAG_TWIST_FREE  // timing-only: as if the new block's first words were prefetched
+                pfn = PF;
+#else
                 pfn = 0;  // prefetched words are stale now
+#endif
             }
         }
         // ---- one round: D*P consecutive draws of this env's stream; position

@@ -34,7 +34,7 @@ def main():
     args = ap.parse_args()
     if args.lib:
         import dronerl_amd._native as nat
-        nat.LIB_PATH = os.path.abspath(args.lib)
+        nat.LIB_PATH = os.environ["DRL_LIB"] = os.path.abspath(args.lib)
     G, N, E, K = CONFIGS[args.config]
     env = BatchedDeliveryDrones(EnvParams(n_drones=N, grid_size=G), E)
     env.reset(seed=0)

@@ -20,7 +20,7 @@ def main():
     args = ap.parse_args()
     if args.lib:
         import dronerl_amd._native as nat
-        nat.LIB_PATH = os.path.abspath(args.lib)
+        nat.LIB_PATH = os.environ["DRL_LIB"] = os.path.abspath(args.lib)
     from dronerl_amd.dqn import QNetwork
     E = args.envs
     obs = torch.rand((E, 1, 7, 7, 6), device="cuda")
