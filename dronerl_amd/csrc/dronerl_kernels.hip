@@ -42,9 +42,19 @@ __device__ unsigned long long* g_stamps;
             g_stamps[sw_ * 16 + 8 + (i) / 6] = __builtin_amdgcn_s_memrealtime();         \
         __builtin_amdgcn_sched_barrier(0);                                               \
     } while (0)
+// sub-phase clock (accumulated per wave into slots 10..13 of the stamp row)
+#define DRL_SUBT(v)                                                                  \
+    do {                                                                             \
+        __builtin_amdgcn_sched_barrier(0);                                           \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");   \
+        __builtin_amdgcn_sched_barrier(0);                                           \
+    } while (0)
 #else
 #define DRL_STAMP(i) \
     do {             \
+    } while (0)
+#define DRL_SUBT(v) \
+    do {            \
     } while (0)
 #endif
 
@@ -745,10 +755,12 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     const int my_item = crashed ? newslot - nS : -1;  // this drone's respawn item
     uint32_t rounds = 0;
     [[maybe_unused]] uint32_t rounds_w = 0;  // wave-level loop trips (diagnostics)
+    [[maybe_unused]] unsigned long long sub_t0 = 0, sub_t1 = 0, sub_t2 = 0, sub_t3 = 0, sub_acc[4] = {0, 0, 0, 0};
     for (;;) {
         const bool work = env_ok && w < total;
         if (!__ballot(work)) break;
         ++rounds_w;
+        DRL_SUBT(sub_t0);
         uint64_t need = __ballot(work && j == 0 && midx >= MT_N);
         while (need) {
             const int tl = __ffsll((unsigned long long)need) - 1;
@@ -769,6 +781,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         // ---- one round: D*P consecutive draws of this env's stream; position
         // d = q*P + j is lane j's q-th draw (branch-free; groups without work
         // compute and discard)
+        DRL_SUBT(sub_t1);
         const int avail = MT_N - midx;
         int rq[D], ccq[D];
         bool candq[D], accq[D];
@@ -818,11 +831,21 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
             okdc |= CM(okd) << (q * P);
             okgc |= CM(okg) << (q * P);
         }
+        DRL_SUBT(sub_t2);
         // ---- place as many items as this round's candidates allow: a placement
         // ends on a pair's second draw, so the pairing holds for the next item;
         // cells placed this round are removed from the masks by compare-ballots.
         int last = -1;
         bool more = work;
+#ifdef DRL_DIAG_NO_PLACE  // timing-only (wrong results): every item placed at once at the first candidate
+        if (more) {
+            const CM m0 = (w < nR ? okdc : okgc);
+            last = m0 ? lobit(m0) : D * P - 1;
+            pos = (my_item >= 0 && m0) ? ccq[0] : pos;
+            w = m0 ? total : w;
+            more = false;
+        }
+#endif
         while (__ballot(more)) {
             if (more) {
                 const bool isd = w < nR;
@@ -858,6 +881,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
                 }
             }
         }
+        DRL_SUBT(sub_t3);
         if (work) {
             if (w >= total) {
                 midx += last + 1;  // draws after the last placement stay unconsumed
@@ -876,7 +900,22 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
             }
         }
         wave_sync();
+#ifdef DRL_STAMPS
+        {  // twists | candidates (draws, pairing, masks) | placement | round tail
+            unsigned long long t4;
+            DRL_SUBT(t4);
+            sub_acc[3] += t4 - sub_t3;
+        }
+        sub_acc[0] += sub_t1 - sub_t0;
+        sub_acc[1] += sub_t2 - sub_t1;
+        sub_acc[2] += sub_t3 - sub_t2;
+#endif
     }
+#ifdef DRL_STAMPS
+    if (lane == 0)
+        for (int k = 0; k < 4; ++k)
+            g_stamps[((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + 10 + k] = sub_acc[k];
+#endif
 
     DRL_STAMP(4);
 #ifdef DRL_STAMPS

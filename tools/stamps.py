@@ -50,7 +50,7 @@ def main():
         print(path)
         return
     import dronerl_amd._native as nat
-    nat.LIB_PATH = path
+    nat.LIB_PATH = os.environ["DRL_LIB"] = path
     L = nat.lib()
     L.drl_debug_set_stamps.argtypes = [ctypes.c_void_p]
     from bench import CONFIGS
@@ -66,6 +66,7 @@ def main():
     assert L.drl_debug_set_stamps(ctypes.c_void_p(stamps.data_ptr())) == 0
     acc = []
     rounds = []
+    subs = []
     for t in range(args.steps):
         a = env.synth_actions(seed=1, step=t)
         env.step(a, obs_k=K)
@@ -74,6 +75,7 @@ def main():
         if t >= 2:
             acc.append(np.diff(st[:, :7], axis=1))
             rounds.append(st[:, 7].copy())
+            subs.append(st[:, 10:14].copy())
         if t == args.steps - 1:
             # s_memrealtime (100 MHz, chip-wide) at wave start / end
             rs, re_ = st[:, 8], st[:, 9]
@@ -90,6 +92,13 @@ def main():
             print(f"  wave end p10/50/90/99/max {np.percentile(ends, 10):.1f}/{np.percentile(ends, 50):.1f}/"
                   f"{np.percentile(ends, 90):.1f}/{np.percentile(ends, 99):.1f}/{ends.max():.1f} us; "
                   f"lifetime max {life.max():.1f} us")
+            rl = st[:, 7]
+            late = ends >= np.percentile(ends, 99)
+            print("  wave end by respawn trips (trips: n / mean end us / max end us): " + ", ".join(
+                f"{k}: {int((rl == k).sum())}/{ends[rl == k].mean():.1f}/{ends[rl == k].max():.1f}"
+                for k in range(int(rl.max()) + 1) if (rl == k).any()))
+            print(f"  latest 1% of waves: trips mean {rl[late].mean():.2f} (all waves {rl.mean():.2f}), "
+                  f"start mean {starts[late].mean():.1f} us (all {starts.mean():.1f})")
             xcd = np.arange(len(starts)) % 8
             print("  per-XCD (block % 8) mean start / mean end / max end us: " + ", ".join(
                 f"{starts[xcd == i].mean():.1f}/{ends[xcd == i].mean():.1f}/{ends[xcd == i].max():.1f}"
@@ -100,6 +109,9 @@ def main():
     tot = d.sum(1)
     print(f"{args.config} E={E} K={K}: wave lifetime (clk) mean {tot.mean():.0f} median {np.median(tot):.0f} "
           f"p90 {np.percentile(tot, 90):.0f}")
+    sub = np.concatenate(subs)
+    print("  respawn sub-phases, clk per wave (mean over waves): " + ", ".join(
+        f"{n} {sub[:, i].mean():.0f}" for i, n in enumerate(["twists", "candidates", "placement", "round tail"])))
     rr = np.concatenate(rounds)
     print(f"  respawn loop trips per wave: mean {rr.mean():.2f}  median {np.median(rr):.0f}  p90 "
           f"{np.percentile(rr, 90):.0f}  max {rr.max()}  hist {np.bincount(rr, minlength=8)[:10].tolist()}")
