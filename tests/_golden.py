@@ -42,3 +42,20 @@ def oracle_params(d):
                   stations_factor=p["stations_factor"], skyscrapers_factor=p["skyscrapers_factor"],
                   pickup_reward=p["pickup_reward"], delivery_reward=p["delivery_reward"],
                   crash_reward=p["crash_reward"], charge_reward=p["charge_reward"])
+
+
+def load_npz(name):
+    with np.load(os.path.join(GOLDEN, name)) as z:
+        return {k: z[k] for k in z.files}
+
+
+def reset_configs():
+    """Configs of reset_states.npz (oracle/gen_reset_mt_golden.py): name -> (side, n_drones)."""
+    d = load_npz("reset_states.npz")
+    return {k[:-6]: (int(d[k]), int(d[k[:-6] + "__n"])) for k in d if k.endswith("__side")}
+
+
+def mt_sha(words625):
+    """sha256 of the 624 MT state words (little-endian u32), as the fixture stores it."""
+    import hashlib
+    return np.frombuffer(hashlib.sha256(np.asarray(words625[:624], dtype="<u4").tobytes()).digest(), np.uint8)

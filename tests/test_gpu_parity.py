@@ -660,3 +660,28 @@ def test_train_segment_parallel_matches_serial():
             assert torch.equal(getattr(l0.rb, k), getattr(l1.rb, k)), (name, k)
         assert l0.rb.cursor == l1.rb.cursor
         assert torch.equal(l0.obs[0], l1.obs[0]), name
+
+
+@pytest.mark.parametrize("kernel", list(RESET_KERNELS))
+@pytest.mark.parametrize("name", ["c1_g8_n4", "c3_g16_n8", "c4_g32_n16", "c5_g64_n32", "t_g5_n1", "t_g7_n2",
+                                  "t_g11_n6", "t_g13_n8"])
+def test_reset_states_fixture_on_gpu(name, kernel, monkeypatch):
+    """C-3 item 3: random.seed(s); env.reset() of the reference for s = 0..15
+    (tests/golden/reset_states.npz): env g of reset(seed=0) is seeded g."""
+    from tests._golden import load_npz, mt_sha
+    for k, v in RESET_KERNELS[kernel].items():
+        monkeypatch.setenv(k, v)
+    d = load_npz("reset_states.npz")
+    G, N = int(d[f"{name}__side"]), int(d[f"{name}__n"])
+    E = len(d["seeds"])
+    env = Env(EnvParams(n_drones=N, grid_size=G), E)
+    env.reset(seed=0)
+    g = gpu_state(env)
+    np.testing.assert_array_equal(g["ground"], d[f"{name}__ground"])
+    np.testing.assert_array_equal(g["y"], d[f"{name}__y"])
+    np.testing.assert_array_equal(g["x"], d[f"{name}__x"])
+    np.testing.assert_array_equal(g["packet"], d[f"{name}__packet"])
+    np.testing.assert_array_equal(g["order"], np.tile(np.arange(N), (E, 1)))
+    np.testing.assert_array_equal(g["mt"][:, 624], d[f"{name}__mtidx"])
+    for e in range(E):
+        np.testing.assert_array_equal(mt_sha(g["mt"][e]), d[f"{name}__mtsha"][e], err_msg=f"{name} seed {e} MT")

@@ -268,3 +268,43 @@ def test_full_grid_respawn_detected_not_hung():
     env.set_state(st["ground"], st["order"], st["y"], st["x"], st["charge"], st["packet"])
     with pytest.raises(NoFreeCell):
         env.step(np.array(act, np.int32))
+
+
+# ---- C-3 items 3 and 4: committed reset states (seeds 0..15 per config) and
+# MT19937 known answers, both generated from the reference / CPython
+# (oracle/gen_reset_mt_golden.py), so the box-side checks need neither.
+def test_mt_known_answers_fixture():
+    from tests._golden import load_npz
+    k = load_npz("mt_kat.npz")
+    for i, s in enumerate(k["seeds"]):
+        m = MT(int(s))
+        assert [m.genrand() for _ in range(16)] == k["first16"][i].tolist()
+        m = MT(int(s))
+        assert [m.getrandbits(b) for b in range(1, 9)] == k["bits1_8"][i].tolist()
+        for gi, G in enumerate(k["sides"]):
+            m = MT(int(s))
+            assert [m.randint(0, int(G) - 1) for _ in range(16)] == k["randint"][i, gi].tolist()
+        assert MT(int(s)).shuffle(list(range(100))) == k["shuffle100"][i].tolist()
+        assert MT(int(s)).sample(list(range(300)), 8) == k["sample_set_300_8"][i].tolist()
+        assert MT(int(s)).sample(list(range(13)), 4) == k["sample_pool_13_4"][i].tolist()
+
+
+@pytest.mark.parametrize("name", ["c1_g8_n4", "c3_g16_n8", "c4_g32_n16", "c5_g64_n32", "t_g5_n1", "t_g7_n2",
+                                  "t_g11_n6", "t_g13_n8"])
+def test_reset_states_fixture(name):
+    from oracle.oracle import OracleMulti
+    from tests._golden import load_npz, mt_sha
+    d = load_npz("reset_states.npz")
+    G, N = int(d[f"{name}__side"]), int(d[f"{name}__n"])
+    seeds = d["seeds"]
+    o = OracleMulti(Params(side=G, n_drones=N), len(seeds))
+    o.reset(seeds)
+    st = o.state()
+    np.testing.assert_array_equal(st["ground"], d[f"{name}__ground"])
+    np.testing.assert_array_equal(st["y"], d[f"{name}__y"])
+    np.testing.assert_array_equal(st["x"], d[f"{name}__x"])
+    np.testing.assert_array_equal(st["packet"], d[f"{name}__packet"])
+    np.testing.assert_array_equal(st["order"], np.tile(np.arange(N), (len(seeds), 1)))
+    np.testing.assert_array_equal(st["mt"][:, 624], d[f"{name}__mtidx"])
+    for e in range(len(seeds)):
+        np.testing.assert_array_equal(mt_sha(st["mt"][e]), d[f"{name}__mtsha"][e])
