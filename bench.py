@@ -550,10 +550,26 @@ def main():
     # stores.
     flags = 0 if args.obs_cached else DRL_STEP_OBS_STREAM
 
-    def run(t):
+    # the respawn-candidate rings are topped up every refill_every steps (what
+    # env.step() does), as a separate drl_refill launch bracketed by its own
+    # events, so the step kernel's average duration can be separated from it
+    refill_every = env.refill_every
+    refill_ev = []  # (start, end) event pairs of the timed region's refills
+
+    def run(t, timed=False):
         rc = L.drl_step_ex(cp, sp, a_ptrs[t], r_p, d_p, o_p, K, e_p, flags, s_p)
         if rc:
             raise RuntimeError(L.drl_last_error().decode())
+        if refill_every > 0 and (t + 1) % refill_every == 0:
+            if timed:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record(stream)
+            rc = L.drl_refill(cp, sp, s_p)
+            if rc:
+                raise RuntimeError(L.drl_last_error().decode())
+            if timed:
+                ev[1].record(stream)
+                refill_ev.append(ev)
 
     for t in range(args.warmup):
         run(t)
@@ -564,7 +580,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     for t in range(args.warmup, T):
-        run(t)
+        run(t, timed=True)
     ev1.record(stream)
     torch.cuda.synchronize()
     barrier(world)
@@ -576,7 +592,13 @@ def main():
 
     total_env_steps = E * world * args.steps
     value = total_env_steps / wall_max
-    launch_s = ev_ms / 1e3 / args.steps      # average drl_step duration on this stream
+    refill_ms = sum(a.elapsed_time(b) for a, b in refill_ev)
+    launch_s = (ev_ms - refill_ms) / 1e3 / args.steps  # average drl_step duration on this stream
+    refill = {"every": refill_every, "launches": len(refill_ev),
+              "avg_launch_us": refill_ms / max(len(refill_ev), 1) * 1e3,
+              "per_step_us": refill_ms / args.steps * 1e3,
+              "note": "drl_refill (respawn-candidate rings) launches inside the timed region: in value and "
+                      "ms_per_step, not in roofline.avg_launch_us (the drl_step kernel alone)"}
     R, Wb = algorithmic_bytes(G, N, K, W)
     achieved = E * R / launch_s / 1e9
     achieved_rw = E * (R + Wb) / launch_s / 1e9
@@ -605,7 +627,7 @@ def main():
         cwall = max_over_ranks(time.perf_counter() - tc, world)
         env.check_errors()
         flags = flags_main
-        c_launch = c0.elapsed_time(c1) / 1e3 / nc
+        c_launch = c0.elapsed_time(c1) / 1e3 / nc  # (refill share included)
         cached = {"value": E * world * nc / cwall, "unit": "env-steps/s", "steps": nc,
                   "ms_per_step": cwall / nc * 1e3, "avg_launch_us": c_launch * 1e6,
                   "frac": E * algorithmic_bytes(G, N, K, W)[0] / c_launch / 1e9 / PEAK_HBM_GBS,
@@ -694,6 +716,7 @@ def main():
                                  "read+write figure can exceed the peak at large grids (C5). Measured HBM bytes "
                                  "per launch: traffic",
                          "traffic_detail": traffic_src},
+            "refill": refill,
             "cached_obs": cached,
             "cpu_baseline": cpu,
             "resets_per_s": resets_per_s,

@@ -13,8 +13,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # DRL_LIB: an alternative build of the same library (tools/variants.py A/B runs)
 LIB_PATH = os.environ.get("DRL_LIB") or os.path.join(_HERE, "libdronerl.so")
 
-DRL_ABI_VERSION = 3  # include/dronerl.h
-DRL_MT_WORDS = 640
+DRL_ABI_VERSION = 4  # include/dronerl.h
+DRL_MT_WORDS = 1344  # per-env RNG row: two MT blocks + the respawn-candidate ring
+DRL_CAND_SLOTS = 64
 DRL_MAX_DRONES = 64
 DRL_MAX_SIDE = 128
 DRL_MAX_RADIUS = 8
@@ -22,10 +23,11 @@ DRL_ERR_BAD_ACTION = 1
 DRL_ERR_NO_FREE_CELL = 2
 DRL_ERR_BAD_STATE = 4
 DRL_STEP_OBS_STREAM = 1  # drl_step_ex flag: streaming (non-temporal) observation stores
+DRL_STEP_REFILL = 2      # drl_step_ex flag: top up the respawn-candidate rings after the step
 
 # Every symbol include/dronerl.h declares (tests check the .so exports them all).
 EXPORTS = ["drl_abi_version", "drl_last_error", "drl_side_from_density", "drl_layout_query", "drl_reset",
-           "drl_step", "drl_step_ex", "drl_rollout", "drl_obs", "drl_grid_obs", "drl_decode", "drl_encode", "drl_synth_actions",
+           "drl_step", "drl_step_ex", "drl_rollout", "drl_refill", "drl_mt_get", "drl_mt_set", "drl_obs", "drl_grid_obs", "drl_decode", "drl_encode", "drl_synth_actions",
            # library-owned env handles
            "drl_env_create", "drl_env_destroy", "drl_env_seed", "drl_env_reset", "drl_env_step",
            "drl_env_step_obs", "drl_env_obs", "drl_env_grid_obs", "drl_env_get_state", "drl_env_set_state", "drl_env_state",
@@ -55,7 +57,7 @@ class DrlParams(ctypes.Structure):
 class DrlLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in [
         "side", "n_drones", "cells", "ground_stride", "drone_stride", "mt_stride", "obs_window", "obs_floats",
-        "step_group_lanes", "step_lds_bytes"]]
+        "step_group_lanes", "step_lds_bytes", "cand_slots", "refill_every"]]
 
 
 class DrlState(ctypes.Structure):
@@ -102,12 +104,15 @@ def lib():
     L.drl_step.argtypes = [P, S, vp, vp, vp, vp, i32, vp, vp]
     L.drl_step_ex.argtypes = [P, S, vp, vp, vp, vp, i32, vp, ctypes.c_uint32, vp]
     L.drl_rollout.argtypes = [P, S, i32, vp, i64, vp, vp, i64, vp, i32, i64, vp, vp]
+    L.drl_refill.argtypes = [P, S, vp]
+    L.drl_mt_get.argtypes = [P, S, vp, vp]
+    L.drl_mt_set.argtypes = [P, S, vp, vp, vp]
     L.drl_obs.argtypes = [P, S, i32, vp, vp]
     L.drl_grid_obs.argtypes = [P, S, vp, vp]
     L.drl_decode.argtypes = [P, S, vp, vp, vp, vp, vp, vp]
     L.drl_encode.argtypes = [P, S, vp, vp, vp, vp, vp, vp]
     L.drl_synth_actions.argtypes = [u64, u64, i64, i64, i32, vp, vp]
-    for f in ["drl_layout_query", "drl_reset", "drl_step", "drl_step_ex", "drl_rollout", "drl_obs", "drl_grid_obs", "drl_decode", "drl_encode",
+    for f in ["drl_layout_query", "drl_reset", "drl_step", "drl_step_ex", "drl_rollout", "drl_refill", "drl_mt_get", "drl_mt_set", "drl_obs", "drl_grid_obs", "drl_decode", "drl_encode",
               "drl_synth_actions"]:
         getattr(L, f).restype = ctypes.c_int
     if L.drl_abi_version() != DRL_ABI_VERSION:

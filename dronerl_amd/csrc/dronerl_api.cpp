@@ -83,6 +83,17 @@ int step_group_lanes(int n_drones, int gstride, int cells, int window) {
     return P;
 }
 
+// Steps between refills: a step consumes about 0.19 N candidates at the
+// benchmark shapes (respawns per env-step 1.23 / 1.94 / 3.50 at N = 8 / 16 /
+// 32, SURVEY.md §8 A7, plus rejected and ground-item draws), so a third of the
+// ring lasts about CAND_Q / (0.6 N) steps: 13 at C3, 6 at C4, 3 at C5.
+// DRL_REFILL_EVERY overrides it (A/B runs).
+int refill_cadence(int n_drones) {
+    if (const char* v = getenv("DRL_REFILL_EVERY")) return atoi(v) > 0 ? atoi(v) : 1;
+    const int r = (int)(DRL_CAND_SLOTS / (0.6 * n_drones));
+    return r < 1 ? 1 : (r > 16 ? 16 : r);
+}
+
 int validate(const drl_params* p, drl_layout* L) {
     if (!p) return fail("params is NULL");
     if (p->side < 2 || p->side > DRL_MAX_SIDE) return fail("side %d outside [2, %d]", p->side, DRL_MAX_SIDE);
@@ -115,6 +126,8 @@ int validate(const drl_params* p, drl_layout* L) {
             wave_lds_bytes(64 / L->step_group_lanes,
                            env_lds(L->ground_stride, GG, N, 1, L->obs_window, L->step_group_lanes), true);
         if (L->step_lds_bytes > kLdsMax) return fail("side %d needs %d B of LDS per block", p->side, L->step_lds_bytes);
+        L->cand_slots = DRL_CAND_SLOTS;
+        L->refill_every = refill_cadence(N);
     }
     return 0;
 }
@@ -179,6 +192,17 @@ drl::StepArgs step_args(const drl_params* p, const drl_state* s, const drl_layou
     a.max_rounds = 1u << 20;
     a.div_side = drl::make_fastdiv((uint32_t)p->side);
     return a;
+}
+
+int launch_refill(const drl_params* p, const drl_state* s, hipStream_t stream) {
+    drl::RefillArgs a;
+    a.side = p->side;
+    a.kbits = bit_length((uint32_t)p->side);
+    a.E = s->num_envs;
+    a.mt = s->mt;
+    a.mt_index = s->mt_index;
+    hipError_t e = drl::launch_refill(a, stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_refill launch");
 }
 
 }  // namespace
@@ -249,7 +273,34 @@ int drl_reset(const drl_params* p, const drl_state* s, int32_t reseed, uint64_t 
     }
     a.div_side = drl::make_fastdiv((uint32_t)p->side);
     hipError_t e = drl::launch_reset(a, stream);
-    return e == hipSuccess ? 0 : hip_fail(e, "drl_reset launch");
+    if (e != hipSuccess) return hip_fail(e, "drl_reset launch");
+    return launch_refill(p, s, stream);
+}
+
+int drl_refill(const drl_params* p, const drl_state* s, hipStream_t stream) {
+    drl_layout L;
+    if (validate(p, &L) || check_state(s, L)) return -1;
+    if (s->num_envs == 0) return 0;
+    return launch_refill(p, s, stream);
+}
+
+int drl_mt_get(const drl_params* p, const drl_state* s, uint32_t* d_words, hipStream_t stream) {
+    drl_layout L;
+    if (validate(p, &L) || check_state(s, L)) return -1;
+    if (s->num_envs == 0) return 0;
+    if (!d_words) return fail("words is NULL");
+    hipError_t e = drl::launch_mt_get(s->mt, s->mt_index, s->num_envs, d_words, stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_mt_get launch");
+}
+
+int drl_mt_set(const drl_params* p, const drl_state* s, const uint32_t* d_words, int32_t* d_err, hipStream_t stream) {
+    drl_layout L;
+    if (validate(p, &L) || check_state(s, L)) return -1;
+    if (s->num_envs == 0) return 0;
+    if (!d_words) return fail("words is NULL");
+    hipError_t e = drl::launch_mt_set(s->mt, s->mt_index, s->num_envs, d_words, d_err, stream);
+    if (e != hipSuccess) return hip_fail(e, "drl_mt_set launch");
+    return launch_refill(p, s, stream);
 }
 
 int drl_step(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards, uint8_t* d_dones,
@@ -261,7 +312,7 @@ int drl_step_ex(const drl_params* p, const drl_state* s, const int32_t* d_action
                 uint8_t* d_dones, float* d_obs, int32_t obs_k, int32_t* d_err, uint32_t flags,
                 hipStream_t stream) {
     drl_layout L;
-    if (flags & ~DRL_STEP_OBS_STREAM) return fail("unknown drl_step flags 0x%x", flags);
+    if (flags & ~(DRL_STEP_OBS_STREAM | DRL_STEP_REFILL)) return fail("unknown drl_step flags 0x%x", flags);
     if (validate(p, &L) || check_state(s, L)) return -1;
     if (s->num_envs == 0) return 0;
     if (!d_actions || !d_rewards || !d_dones) return fail("actions/rewards/dones must be non-NULL");
@@ -277,7 +328,8 @@ int drl_step_ex(const drl_params* p, const drl_state* s, const int32_t* d_action
     a.og = obs_geom(p, L, d_obs ? obs_k : 1);
     a.obs_nt = (flags & DRL_STEP_OBS_STREAM) ? 1 : 0;
     hipError_t e = drl::launch_step(a, L.step_group_lanes, stream, drl::kStepMode);
-    return e == hipSuccess ? 0 : hip_fail(e, "drl_step launch");
+    if (e != hipSuccess) return hip_fail(e, "drl_step launch");
+    return (flags & DRL_STEP_REFILL) ? launch_refill(p, s, stream) : 0;
 }
 
 int drl_rollout(const drl_params* p, const drl_state* s, int32_t num_steps, const int32_t* d_actions,
@@ -311,8 +363,11 @@ int drl_rollout(const drl_params* p, const drl_state* s, int32_t num_steps, cons
     a.act_tstride = act_step_stride;
     a.out_tstride = out_step_stride;
     a.obs_tstride = d_obs ? obs_step_stride : 0;
-    hipError_t e = drl::launch_step(a, L.step_group_lanes, stream, drl::kRolloutMode);
-    return e == hipSuccess ? 0 : hip_fail(e, "drl_rollout launch");
+    hipError_t e = drl::launch_mt_block0(s->mt, s->mt_index, s->num_envs, stream);  // the stream into block 0
+    if (e != hipSuccess) return hip_fail(e, "drl_rollout launch");
+    e = drl::launch_step(a, L.step_group_lanes, stream, drl::kRolloutMode);
+    if (e != hipSuccess) return hip_fail(e, "drl_rollout launch");
+    return launch_refill(p, s, stream);  // the rollout left the rings empty
 }
 
 int drl_obs(const drl_params* p, const drl_state* s, int32_t k, float* d_obs, hipStream_t stream) {

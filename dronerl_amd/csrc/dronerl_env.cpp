@@ -21,6 +21,7 @@ struct drl_env {
     int64_t env_offset;
     uint64_t base_seed;
     int seeded;  // 0: the next reset re-seeds every env (random.seed(base_seed + env_offset + e))
+    int32_t since_refill;  // steps since the candidate rings were last topped up (drl_refill)
     drl_state s;
     int32_t* err;
 };
@@ -130,16 +131,25 @@ int drl_env_reset(drl_env* env, const uint8_t* d_env_mask, hipStream_t stream) {
             return drl_internal_fail("the first reset after create/seed must cover every env (mask must be NULL)");
         const int reseed = env->seeded ? 0 : 1;
         if (drl_reset(&env->p, &env->s, reseed, env->base_seed + (uint64_t)env->env_offset, d_env_mask, stream))
-            return -1;
+            return -1;  // (drl_reset ends with a refill)
         env->seeded = 1;
+        env->since_refill = 0;
         return 0;
     });
+}
+
+// DRL_STEP_REFILL every layout.refill_every steps
+static uint32_t refill_flag(drl_env* env) {
+    if (++env->since_refill < env->L.refill_every) return 0u;
+    env->since_refill = 0;
+    return DRL_STEP_REFILL;
 }
 
 int drl_env_step(drl_env* env, const int32_t* d_actions, float* d_rewards, uint8_t* d_dones, hipStream_t stream) {
     return on_device(env, [&]() -> int {
         if (!env->seeded) return drl_internal_fail("step before the first reset");
-        return drl_step(&env->p, &env->s, d_actions, d_rewards, d_dones, nullptr, 0, env->err, stream);
+        return drl_step_ex(&env->p, &env->s, d_actions, d_rewards, d_dones, nullptr, 0, env->err, refill_flag(env),
+                           stream);
     });
 }
 
@@ -148,7 +158,8 @@ int drl_env_step_obs(drl_env* env, const int32_t* d_actions, float* d_rewards, u
     return on_device(env, [&]() -> int {
         if (!env->seeded) return drl_internal_fail("step before the first reset");
         if (!d_obs) return drl_internal_fail("obs is NULL");
-        return drl_step(&env->p, &env->s, d_actions, d_rewards, d_dones, d_obs, k, env->err, stream);
+        return drl_step_ex(&env->p, &env->s, d_actions, d_rewards, d_dones, d_obs, k, env->err, refill_flag(env),
+                           stream);
     });
 }
 
@@ -175,15 +186,7 @@ int drl_env_get_state(drl_env* env, const drl_state_view* v, hipStream_t stream)
                                    "ground copy"))
             return -1;
         if (drl_decode(&env->p, &env->s, v->order, v->y, v->x, v->charge, v->carry, stream)) return -1;
-        if (v->mt) {
-            if (hip_check(hipMemcpy2DAsync(v->mt, 625 * 4, env->s.mt, DRL_MT_WORDS * 4, 624 * 4, E,
-                                           hipMemcpyDeviceToDevice, stream),
-                          "mt copy") ||
-                hip_check(hipMemcpy2DAsync(v->mt + 624, 625 * 4, env->s.mt_index, 4, 4, E, hipMemcpyDeviceToDevice,
-                                           stream),
-                          "mt index copy"))
-                return -1;
-        }
+        if (v->mt && drl_mt_get(&env->p, &env->s, v->mt, stream)) return -1;
         return 0;
     });
 }
@@ -198,14 +201,9 @@ int drl_env_set_state(drl_env* env, const drl_state_view* v, hipStream_t stream)
                       "ground copy"))
             return -1;
         if (drl_encode(&env->p, &env->s, v->order, v->y, v->x, v->charge, v->carry, stream)) return -1;
-        if (hip_check(hipMemcpy2DAsync(env->s.mt, DRL_MT_WORDS * 4, v->mt, 625 * 4, 624 * 4, E,
-                                       hipMemcpyDeviceToDevice, stream),
-                      "mt copy") ||
-            hip_check(hipMemcpy2DAsync(env->s.mt_index, 4, v->mt + 624, 625 * 4, 4, E, hipMemcpyDeviceToDevice, stream),
-                      "mt index copy") ||
-            hip_check(drl::launch_mt_index_check(env->s.mt_index, (int64_t)E, env->err, stream), "mt index check"))
-            return -1;
+        if (drl_mt_set(&env->p, &env->s, v->mt, env->err, stream)) return -1;  // (then a refill)
         env->seeded = 1;
+        env->since_refill = 0;
         return 0;
     });
 }

@@ -10,6 +10,31 @@ namespace drl {
 constexpr int MT_N = 624;
 constexpr int MT_M = 397;
 constexpr int MT_WORDS = DRL_MT_WORDS;
+constexpr int MT_ALT = DRL_MT_BLOCK1;  // word offset of MT block 1 in an env's row
+constexpr int MT_RING = DRL_MT_RING;   // word offset of the respawn-candidate ring
+constexpr int CAND_Q = DRL_CAND_SLOTS; // ring entries (power of two)
+static_assert((CAND_Q & (CAND_Q - 1)) == 0 && CAND_Q <= 64, "ring size");
+
+// mt_index word (include/dronerl.h): index | par << 10 | head << 16 | count << 24
+__host__ __device__ constexpr int mi_idx(uint32_t w) { return (int)(w & 0x3ffu); }
+__host__ __device__ constexpr int mi_par(uint32_t w) { return (int)((w >> 10) & 1u); }
+__host__ __device__ constexpr int mi_head(uint32_t w) { return (int)((w >> 16) & (uint32_t)(CAND_Q - 1)); }
+__host__ __device__ constexpr int mi_cnt(uint32_t w) {
+    return (int)((w >> 24) & 127u) < CAND_Q ? (int)((w >> 24) & 127u) : CAND_Q;
+}
+__host__ __device__ constexpr uint32_t mi_pack(int idx, int par, int head, int cnt) {
+    return (uint32_t)idx | ((uint32_t)par << 10) | ((uint32_t)head << 16) | ((uint32_t)cnt << 24);
+}
+// candidate ring entry: cell | MT index after the pair << 16 | that index's block << 26
+__host__ __device__ constexpr int ce_cell(uint32_t e) { return (int)(e & 0x3fffu); }
+__host__ __device__ constexpr int ce_idx(uint32_t e) { return (int)((e >> 16) & 0x3ffu); }
+__host__ __device__ constexpr int ce_par(uint32_t e) { return (int)((e >> 26) & 1u); }
+__host__ __device__ constexpr uint32_t ce_pack(int cell, int idx, int par) {
+    return (uint32_t)cell | ((uint32_t)idx << 16) | ((uint32_t)par << 26);
+}
+// ring entries each drl_step lane holds (P lanes per env: P * step_cq(P) candidates per step
+// without a second memory round trip; more come from the stream itself)
+constexpr int step_cq(int P) { return P <= 16 ? 2 : 1; }
 // DRL_ROLL_ACT_LDS: drl_rollout loads the next step's actions by LDS-DMA at the end of each step
 #ifndef DRL_ROLL_ACT_LDS
 #define DRL_ROLL_ACT_LDS 1
@@ -140,6 +165,13 @@ struct StepArgs {
     int64_t act_tstride, out_tstride, obs_tstride;
 };
 
+struct RefillArgs {
+    int side, kbits;
+    int64_t E;
+    uint32_t* mt;
+    uint32_t* mt_index;
+};
+
 struct ResetArgs {
     int side, n_drones, cells, gstride;
     int n_sky, n_pack, n_drop, n_stat;
@@ -241,7 +273,10 @@ hipError_t launch_grid_obs(const uint8_t* ground, const uint32_t* drones, int64_
                            float* out, hipStream_t s);
 hipError_t launch_encode(uint32_t* drones, int64_t E, int N, const int32_t* order, const int32_t* y,
                          const int32_t* x, const int32_t* c, const uint8_t* k, hipStream_t s);
-hipError_t launch_mt_index_check(uint32_t* mt_index, int64_t E, int32_t* err, hipStream_t s);
+hipError_t launch_refill(const RefillArgs& a, hipStream_t s);
+hipError_t launch_mt_get(const uint32_t* mt, const uint32_t* mt_index, int64_t E, uint32_t* out, hipStream_t s);
+hipError_t launch_mt_block0(uint32_t* mt, uint32_t* mt_index, int64_t E, hipStream_t s);
+hipError_t launch_mt_set(uint32_t* mt, uint32_t* mt_index, int64_t E, const uint32_t* in, int32_t* err, hipStream_t s);
 hipError_t launch_synth(uint64_t seed, uint64_t step, int64_t env_offset, int64_t E, int N, int32_t* out,
                         hipStream_t s);
 

@@ -502,7 +502,8 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     constexpr int GPW = 64 / P;
     constexpr int D = ROLL ? roll_draws(P) : step_draws(P);  // draws per lane per respawn round
     constexpr int PF = ROLL ? roll_pf(P) : step_pf(P);  // prefetched MT words per env
-    constexpr int PFR = (PF + P - 1) / P;        // prefetched MT words per lane
+    constexpr int PFR = (PF + P - 1) / P;        // prefetched MT words per lane (rollout)
+    constexpr int QL = step_cq(P);               // ring entries per lane (step)
     using CM = typename GMaskT<(P * D <= 32 ? 32 : 64)>::type;  // round-position masks
     constexpr int CH = P < 16 ? P : 16;        // shuffle batch
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -544,12 +545,17 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     if constexpr (GEO::kGstride > 0) stage_ground_dma_n<GPW * GEO::kGstride / 16>(ground_w, nenv_w * gstride, W.gl, lane0);
     else stage_ground_dma(ground_w, nenv_w * gstride, W.gl, lane0);
     __builtin_amdgcn_sched_barrier(0);  // issue every load above before waiting for the MT index
-    int midx = (int)mi[0];
+    uint32_t mword = mi[0];  // the env's mt_index word: index, block, ring head / count
 #pragma unroll
-    for (int e = 1; e < GPW; ++e) midx = (grp0 >= e) ? (int)mi[e] : midx;
+    for (int e = 1; e < GPW; ++e) mword = (grp0 >= e) ? mi[e] : mword;
     uint32_t rec = active0 ? rec_ld : 0u;
     int my_action = active0 ? act_ld : 4;
-    if (!env_ok0) midx = MT_N;
+    if (!env_ok0) mword = (uint32_t)MT_N;
+    // the stream position: drl_rollout reads it now (its stream is in block 0:
+    // drl_rollout launches drl_mt_block0_kernel first); drl_step only after
+    // the ring's entries, which carry it along, so nothing holds it across
+    // the claim phase
+    int midx = ROLL ? min(mi_idx(mword), MT_N) : 0;
     uint32_t* const stash = W.mtw;  // ROLL: records between steps ([GPW][P], O order)
     int act_next = 4;
     const int T = ROLL ? a.steps : 1;
@@ -583,7 +589,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     uint32_t* bm = W.bm + grp * (g.lds_bm() / 4);
     uint32_t* mtw = W.mtw + grp * PF;
     uint16_t* posidx = W.posidx + grp * g.np();
-    const uint32_t* mrow = mt_w + (uint32_t)(env_ok ? grp : 0) * MT_WORDS;
+    const uint32_t* mrow = mt_w + (uint32_t)(env_ok ? grp : 0) * MT_WORDS;  // drl_step: set after the ring
     if constexpr (ROLL) {
         if (t > 0) {  // the previous step left its records in the stash
             rec = active ? stash[lane] : 0u;
@@ -609,12 +615,22 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     // MT-word prefetch: issued once the records have landed (LDS-DMA makes the
     // compiler wait for every outstanding load before the first record use),
     // so its latency overlaps the claim / effect / ordering phases
+    // drl_step: the env's next P*QL ring entries (drl_refill drew them ahead)
+    // instead; the MT words are read only if the ring runs dry.
     __builtin_amdgcn_sched_barrier(0);
     const int pf_base0 = midx;
-    int pfn = min(PF, MT_N - midx);
-    uint32_t pfw[PFR];  // next MT words of the stream (addresses clamped: no per-word branch)
+    int pfn = ROLL ? min(PF, MT_N - midx) : 0;
+    uint32_t pfw[ROLL ? PFR : 1];  // next MT words of the stream (addresses clamped: no per-word branch)
+    uint32_t cq[ROLL ? 1 : QL];    // ring entries head + j + P*r
+    if constexpr (ROLL) {
 #pragma unroll
-    for (int r = 0; r < PFR; ++r) pfw[r] = mrow[min(midx + j + P * r, MT_N - 1)];
+        for (int r = 0; r < PFR; ++r) pfw[r] = mrow[min(midx + j + P * r, MT_N - 1)];
+    } else {
+        const uint32_t* ring = mt_w + (uint32_t)(env_ok ? grp : 0) * MT_WORDS + MT_RING;
+        const int qhead = mi_head(mword);
+#pragma unroll
+        for (int r = 0; r < QL; ++r) cq[r] = ring[(qhead + j + P * r) & (CAND_Q - 1)];
+    }
     __builtin_amdgcn_sched_barrier(0);
     if (active) {
         if (act < 0) act += 5;  // Python negative list index
@@ -742,10 +758,11 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     // every item: the round's candidate cells are read from LDS once and
     // several items are placed per round, later items seeing the cells placed
     // earlier in the round through register compares.
+    if constexpr (ROLL) {
 #pragma unroll
-    for (int r = 0; r < PFR; ++r)
-        if (j + P * r < pfn) mtw[j + P * r] = pfw[r];
-    int pf_base = pf_base0;
+        for (int r = 0; r < PFR; ++r)
+            if (j + P * r < pfn) mtw[j + P * r] = pfw[r];
+    }
 #ifdef DRL_DIAG_NO_RESPAWN  // timing-only diagnostic build (wrong results): the step without its respawn rounds
     int w = total, have_y = 0, yv = 0;
 #else
@@ -753,6 +770,99 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
 #endif
     const int shift = 32 - g.kbits();
     const int my_item = crashed ? newslot - nS : -1;  // this drone's respawn item
+    if constexpr (!ROLL) {
+        // ---- fast path (drl_step): the ring's candidate cells, i.e. the
+        // stream's next accepted (y, x) pairs, P per batch, one per lane.  An
+        // item takes the first candidate after the previous item's that is free
+        // under its mask, so the items of one class (drones: drones |
+        // skyscrapers; packets, then dropzones: any ground object) are the
+        // class's first free candidates that do not repeat an earlier candidate
+        // of the class (a repeat is either occupied or the cell an earlier item
+        // took).  One ballot and a rank place a whole class; the next class
+        // starts after its last item.  Earlier batches' placements are in the
+        // bitmap / ground.
+        const int qcnt = env_ok ? mi_cnt(mword) : 0;
+        const int GGc = G * G;
+        int start = 0;  // ring entries consumed (group-uniform)
+#pragma unroll
+        for (int r = 0; r < QL; ++r) {
+            if (!__ballot(env_ok && w < total)) break;
+            const int cell = ce_cell(cq[r]);
+            const bool valid = env_ok && P * r + j < qcnt && cell < GGc;
+            const int ccell = valid ? cell : 0;
+            const int tg = valid ? cell : -1 - j;  // unique negatives never match
+            int prev = -1;                        // nearest earlier lane of the batch with the same cell
+            if constexpr ((P == 8 || P == 16) && DRL_DPP8) {
+                for_other_lanes<P>(tg, [&](int o, int k) {
+                    const int s2 = j ^ k;
+                    prev = (o == tg && s2 < j && s2 > prev) ? s2 : prev;
+                });
+            } else {
+#pragma unroll
+                for (int s0 = 0; s0 < P; s0 += CH) {
+                    int ts[CH];
+#pragma unroll
+                    for (int t2 = 0; t2 < CH; ++t2) ts[t2] = gshfl<P>(tg, s0 + t2, lane);
+#pragma unroll
+                    for (int t2 = 0; t2 < CH; ++t2) prev = (ts[t2] == tg && s0 + t2 < j) ? s0 + t2 : prev;
+                }
+            }
+            const int gobj = gl[ccell];
+            const bool occ = bm_test(bm, ccell);
+#pragma unroll
+            for (int cs = 0; cs < 3; ++cs) {  // class steps: drones, packets, dropzones
+                const bool act = env_ok && w < total && start < P * (r + 1);
+                if (!__ballot(act)) break;
+                const bool isd = w < nR;
+                const int cls_end = isd ? nR : (w < nR + n_pack ? nR + n_pack : total);
+                const int need = cls_end - w;
+                const int gnow = cs == 0 ? gobj : (int)gl[ccell];  // packets placed by the previous step
+                const bool fresh = valid && P * r + j >= start && (prev < 0 || P * r + prev < start);
+                const bool ok = act && fresh && (isd ? (!occ && gnow != OBJ_SKYSCRAPER) : gnow == OBJ_EMPTY);
+                const GMask M = gballot<P>(ok, gshift);
+                const int k = min(popc(M), need);
+                const int rank = popc(M & ((GMask(1) << j) - GMask(1)));
+                const bool chosen = ok && rank < k;
+                const GMask C = gballot<P>(chosen, gshift);
+                if (chosen) {
+                    if (isd) {
+                        posidx[w + rank] = (uint16_t)cell;  // item slot (posidx is rewritten at write-back)
+                        bm_set(bm, cell);
+                    } else {
+                        gl[cell] = (w + rank < nR + n_pack) ? OBJ_PACKET : OBJ_DROPZONE;
+                        chg_push(W, grp, nchg, cell);
+                    }
+                }
+                if (act) {
+                    start = (k == need) ? P * r + hibit(C) + 1 : P * (r + 1);
+                    w += k;
+                }
+                wave_sync();
+            }
+        }
+        if (crashed && my_item < w) pos = posidx[my_item];
+        // stream position after the consumed entries; a dry ring continues from
+        // the end of the last entry it held (loaded)
+        const bool dry = env_ok && w < total;
+        const int ncons = dry ? min(qcnt, P * QL) : start;
+        const int ei = ncons > 0 ? ncons - 1 : 0;
+        uint32_t ent = (uint32_t)gshfl<P>((int)cq[0], ei % P, lane);
+#pragma unroll
+        for (int r = 1; r < QL; ++r) {
+            const uint32_t v = (uint32_t)gshfl<P>((int)cq[r], ei % P, lane);
+            ent = (ei / P == r) ? v : ent;
+        }
+        midx = min(ncons > 0 ? ce_idx(ent) : mi_idx(mword), MT_N);
+        const int mpar = ncons > 0 ? ce_par(ent) : mi_par(mword);
+        // the ring served every item: the new word goes out now (a dry ring's
+        // after the draws below, with the block read back from mrow)
+        if (env_ok && j == 0 && !dry)
+            a.mt_index[wenv0 + grp] = mi_pack(midx, mpar, (mi_head(mword) + ncons) & (CAND_Q - 1), qcnt - ncons);
+        mrow += (uint32_t)mpar * MT_ALT;
+        wave_sync();
+    }
+    int pf_base = pf_base0;
+    if constexpr (!ROLL) pf_base = midx;
     uint32_t rounds = 0;
     [[maybe_unused]] uint32_t rounds_w = 0;  // wave-level loop trips (diagnostics)
     [[maybe_unused]] unsigned long long sub_t0 = 0, sub_t1 = 0, sub_t2 = 0, sub_t3 = 0, sub_acc[4] = {0, 0, 0, 0};
@@ -766,7 +876,14 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
             const int tl = __ffsll((unsigned long long)need) - 1;
             need &= need - 1ull;
 #if !defined(DRL_DIAG_NO_TWIST) && !defined(DRL_DIAG_TWIST_FREE)  // timing-only builds (wrong streams)
-            twist_wave(mt_w + (uint32_t)(tl / P) * MT_WORDS, lane);
+            if constexpr (ROLL) {  // the rollout's streams are in block 0
+                twist_wave(mt_w + (uint32_t)(tl / P) * MT_WORDS, lane);
+            } else {  // lane tl's stream block (either)
+                const uint64_t pr = (uint64_t)(uintptr_t)mrow;
+                const uint64_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pr, tl);
+                const uint64_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pr >> 32), tl);
+                twist_wave(reinterpret_cast<uint32_t*>((hi << 32) | lo), lane);
+            }
 #endif
             if (grp == tl / P) {
                 midx = 0;
@@ -940,7 +1057,10 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         a.dones[t * a.out_tstride + wenv0 * N + (rl + idx)] = crashed ? 1 : 0;
         posidx[idx] = (uint16_t)pos;
     }
-    if (!ROLL && env_ok && j == 0) a.mt_index[wenv0 + grp] = (uint32_t)midx;
+    if constexpr (!ROLL) {  // a dry ring: the stream position after the draws, an empty ring
+        if (env_ok && j == 0 && rounds > 0)
+            a.mt_index[wenv0 + grp] = mi_pack(midx, mrow != mt_w + (uint32_t)grp * MT_WORDS ? 1 : 0, 0, 0);
+    }
     wave_sync();
     if (!ROLL && env_ok) {
         const uint32_t nc = W.cnt[grp * 4];
@@ -977,7 +1097,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     if constexpr (ROLL) {  // write the state back once: records, MT index, whole grounds
         wave_sync();
         if (active0) drones_w[rl0 + j0] = stash[lane0];
-        if (env_ok0 && j0 == 0) a.mt_index[wenv0 + grp0] = (uint32_t)midx;
+        if (env_ok0 && j0 == 0) a.mt_index[wenv0 + grp0] = (uint32_t)midx;  // block 0, empty ring (stale now)
         const uint4* src = reinterpret_cast<const uint4*>(W.gl);
         uint4* dst = reinterpret_cast<uint4*>(ground_w);
         for (int v = lane0; v < nenv_w * gstride / 16; v += 64) dst[v] = src[v];
@@ -1145,7 +1265,9 @@ __global__ void __launch_bounds__(64) drl_reset_kernel(ResetArgs a) {
     uint16_t* sel = list + a.list_cap;
     uint16_t* pool = sel + 64;
     const int GG = a.cells, N = a.n_drones;
-    uint32_t* mrow = a.mt + (own ? env : 0) * MT_WORDS;
+    const uint32_t w0 = (own && !a.reseed) ? a.mt_index[env] : 0u;
+    const int par = mi_par(w0);  // the block holding the stream (a reseed writes block 0)
+    uint32_t* mrow = a.mt + (own ? env : 0) * MT_WORDS + par * MT_ALT;
     uint8_t* grow = a.ground + (own ? env : 0) * a.gstride;
 
     if (own) {
@@ -1154,7 +1276,7 @@ __global__ void __launch_bounds__(64) drl_reset_kernel(ResetArgs a) {
         for (int i = 0; i < GG; ++i) list[i] = (uint16_t)i;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    int midx = own ? (a.reseed ? MT_N : (int)a.mt_index[env]) : MT_N;
+    int midx = own ? (a.reseed ? MT_N : min(mi_idx(w0), MT_N)) : MT_N;
     int n = GG;
 
     // Draw one tempered output for every participating lane; twists are
@@ -1167,7 +1289,8 @@ __global__ void __launch_bounds__(64) drl_reset_kernel(ResetArgs a) {
         while (need_) {                                                                   \
             const int tl_ = __ffsll((unsigned long long)need_) - 1;                       \
             need_ &= need_ - 1ull;                                                        \
-            twist_wave(a.mt + ((int64_t)blockIdx.x * a.lanes + tl_) * MT_WORDS, lane);     \
+            twist_wave(a.mt + ((int64_t)blockIdx.x * a.lanes + tl_) * MT_WORDS +             \
+                           __builtin_amdgcn_readlane(par, tl_) * MT_ALT, lane);               \
             if (lane == tl_) midx = 0;                                                    \
         }                                                                                 \
         if (act_) {                                                                       \
@@ -1255,7 +1378,7 @@ __global__ void __launch_bounds__(64) drl_reset_kernel(ResetArgs a) {
             const uint32_t py = fdiv((uint32_t)cell, a.div_side);
             a.drones[env * N + d] = pack_drone((int)py, cell - (int)py * a.side, 100, carry, d);
         }
-        a.mt_index[env] = (uint32_t)midx;
+        a.mt_index[env] = mi_pack(midx, par, 0, 0);  // the candidate ring is stale: empty
     }
 }
 
@@ -1376,13 +1499,15 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
     uint16_t* sel = list + a.list_cap;
     uint16_t* pool = sel + 64;
     const int GG = a.cells, N = a.n_drones;
-    uint32_t* mrow = a.mt + env * MT_WORDS;
+    const uint32_t w0 = a.reseed ? 0u : a.mt_index[env];
+    const int par = mi_par(w0);  // the block holding the stream (a reseed writes block 0)
+    uint32_t* mrow = a.mt + env * MT_WORDS + par * MT_ALT;
     uint8_t* grow = a.ground + env * a.gstride;
     for (int i = lane; i < 2 * kFyBuckets + 64; i += 64) htab[i] = 0u;
 
     // x[k] holds words 64 * ((k + rot) % 10) + lane: the current chunk is
     // always x[0] (moving to the next chunk rotates the array by one register)
-    int midx = a.reseed ? MT_N : (int)a.mt_index[env];
+    int midx = a.reseed ? MT_N : min(mi_idx(w0), MT_N);
     int rot = midx < MT_N ? midx >> 6 : 0;
     uint32_t x[10];
     if (a.reseed) {
@@ -1530,7 +1655,7 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
         const int c = k + rot < 10 ? k + rot : k + rot - 10;
         if (64 * c + lane < MT_N) mrow[64 * c + lane] = x[k];
     }
-    if (lane == 0) a.mt_index[env] = (uint32_t)midx;
+    if (lane == 0) a.mt_index[env] = mi_pack(midx, par, 0, 0);  // the candidate ring is stale: empty
 }
 
 // ------------------------------------------------------------ full grid ---
@@ -1589,15 +1714,270 @@ __global__ void drl_encode_kernel(uint32_t* __restrict__ drones, int64_t total, 
     drones[t] = pack_drone(yv[o], xv[o], cv[o], kv[o] ? 1 : 0, idx);
 }
 
-// CPython's setstate rejects an index outside [0, 624]; the step kernel's MT
-// reads assume that range, so set_state clamps and flags instead.
-__global__ void drl_mt_index_check_kernel(uint32_t* __restrict__ mt_index, int64_t E, int32_t* err) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= E) return;
-    if (mt_index[e] > (uint32_t)MT_N) {
-        mt_index[e] = (uint32_t)MT_N;
-        if (err) atomicOr(err, DRL_ERR_BAD_STATE);
+// random.getstate() / setstate() words of every env: [E][625] = the 624
+// words of the block holding the stream + the index.  CPython's setstate
+// rejects an index outside [0, 624]; the kernels' MT reads assume that range,
+// so set clamps and flags instead.  set writes block 0 and an empty ring.
+__global__ void drl_mt_get_kernel(const uint32_t* __restrict__ mt, const uint32_t* __restrict__ mt_index, int64_t E,
+                                  uint32_t* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= E * 625) return;
+    const int64_t e = t / 625;
+    const int k = (int)(t - e * 625);
+    const uint32_t w = mt_index[e];
+    out[t] = k < MT_N ? mt[e * MT_WORDS + mi_par(w) * MT_ALT + k] : (uint32_t)min(mi_idx(w), MT_N);
+}
+
+__global__ void drl_mt_set_kernel(uint32_t* __restrict__ mt, uint32_t* __restrict__ mt_index, int64_t E,
+                                  const uint32_t* __restrict__ in, int32_t* err) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= E * 625) return;
+    const int64_t e = t / 625;
+    const int k = (int)(t - e * 625);
+    if (k < MT_N) {
+        mt[e * MT_WORDS + k] = in[t];
+    } else {
+        uint32_t idx = in[t];
+        if (idx > (uint32_t)MT_N) {
+            idx = (uint32_t)MT_N;
+            if (err) atomicOr(err, DRL_ERR_BAD_STATE);
+        }
+        mt_index[e] = mi_pack((int)idx, 0, 0, 0);
     }
+}
+
+// drl_rollout draws from block 0 only: move a stream held in block 1 there.
+// (mt_index is left alone: every thread of the env reads its block bit; the
+// rollout writes the word back as block 0 with an empty ring.)
+__global__ void drl_mt_block0_kernel(uint32_t* __restrict__ mt, const uint32_t* __restrict__ mt_index, int64_t E) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= E * MT_N) return;
+    const int64_t e = t / MT_N;
+    const int k = (int)(t - e * MT_N);
+    if (mi_par(mt_index[e])) mt[e * MT_WORDS + k] = mt[e * MT_WORDS + MT_ALT + k];
+}
+
+// ---------------------------------------------------------------- refill ---
+// drl_refill: top up each env's respawn-candidate ring (include/dronerl.h).
+// The candidates are the (y, x) pairs of consecutive accepted randint(0,
+// side-1) draws (_randbelow: the top kbits bits of a tempered word, kept if <
+// side; env.py:226-233 draws y then x), in stream order, starting at the end
+// of the ring's last entry (or at the stream position when it is empty).
+// They depend on the stream alone, so they can be drawn ahead of the steps
+// that consume them.
+//
+// Layout: a wave serves kRefillEnvs envs, one after another, lane l taking
+// the l-th word of a 64-word pass of the env's stream: acceptance is one
+// ballot, a draw's accepted rank one mbcnt, and its pair partner comes back
+// through an LDS slot indexed by rank.  Every load of a pass (the 64 words of
+// each of the wave's envs) is issued before any is used, so a pass costs one
+// round trip; so does the first one (the mt_index words and the whole rings,
+// for the ring's last entry).  Per-env scalars live in lane e of a few VGPRs.
+//
+// Positions are extended: [0, 624) is the block holding the stream (mt_index
+// par), [624, 1248) the next block, kept in the other block's words.  A pass
+// that reaches it first twists the stream's block into them (out of place:
+// the stream's own block stays as the state says), kTwistBatch envs at a time
+// with their blocks loaded together.
+#ifndef DRL_REFILL_ENVS
+#define DRL_REFILL_ENVS 4
+#endif
+#ifndef DRL_TWIST_BATCH
+#define DRL_TWIST_BATCH 2
+#endif
+constexpr int kRefillEnvs = DRL_REFILL_ENVS;
+constexpr int kTwistBatch = DRL_TWIST_BATCH;
+
+__global__ void __launch_bounds__(64) drl_refill_kernel(RefillArgs a) {
+    constexpr int NE = kRefillEnvs;
+    __shared__ uint32_t rank_lds[65];  // a pass's accepted draws by accepted rank (+1: slot 0 = pending y)
+    const int lane = threadIdx.x & 63;
+    const int64_t env0 = (int64_t)blockIdx.x * NE;
+    const int nenv_w = (int)min((int64_t)NE, a.E - env0);
+    if (nenv_w <= 0) return;
+    uint32_t* const wrow = a.mt + env0 * MT_WORDS;  // the wave's rows (scalar base)
+    const int G = a.side, shift = 32 - a.kbits;
+#ifdef DRL_STAMPS  // diagnostic build: per-wave clocks (tools/refill_stamps.py)
+    unsigned long long rs_t0, rs_t1, rs_a, rs_b, rs_tw = 0, rs_ps = 0, rs_ntw = 0, rs_np = 0;
+    DRL_SUBT(rs_t0);
+#endif
+    // ---- round trip 1: every env's mt_index word and ring
+    uint32_t mi[NE], rv[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        mi[e] = a.mt_index[env0 + min(e, nenv_w - 1)];
+        rv[e] = wrow[(uint32_t)min(e, nenv_w - 1) * MT_WORDS + MT_RING + lane];
+    }
+    // per-env state, env e in lane e: count, extended resume position, pending
+    // y (-1: none), next block twisted, done
+    int v_cnt = CAND_Q, v_gext = 0, v_y = -1, v_nval = 0, v_twisted = 0, v_par = 0;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const int cnt = e < nenv_w ? mi_cnt(mi[e]) : CAND_Q;
+        const int head = mi_head(mi[e]), tpar = mi_par(mi[e]);
+        const uint32_t last = (uint32_t)__builtin_amdgcn_readlane((int)rv[e], (head + max(cnt, 1) - 1) & (CAND_Q - 1));
+        const int nval = cnt > 0 && ce_par(last) != tpar;
+        const int gext = cnt > 0 ? min(ce_idx(last), MT_N) + (nval ? MT_N : 0) : min(mi_idx(mi[e]), MT_N);
+        if (lane == e) {
+            v_cnt = cnt;
+            v_gext = gext;
+            v_nval = nval;
+            v_par = tpar;
+        }
+    }
+#ifdef DRL_STAMPS
+    DRL_SUBT(rs_t1);
+#endif
+    for (;;) {
+        const uint64_t work = __ballot(lane < NE && v_cnt < CAND_Q && v_gext < 2 * MT_N);
+        if (!work) break;
+#ifdef DRL_STAMPS
+        DRL_SUBT(rs_a);
+        ++rs_np;
+#endif
+        // ---- twists: envs whose pass reaches the next block.  The block is
+        // loaded, twisted in registers and stored to the other block's words
+        // without waiting for the stores: this pass takes its words from the
+        // registers, and a later pass that reads them from memory first
+        // waits (fence) for them.
+#ifdef DRL_DIAG_REFILL_NO_TWIST  // timing-only (wrong rings): as if every next block were twisted already
+        v_nval = 1;
+#endif
+        if (__ballot(lane < NE && (work >> lane) & 1ull && v_twisted)) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            wave_sync();
+        }
+        uint64_t tw = __ballot(lane < NE && v_cnt < CAND_Q && v_gext < 2 * MT_N && !v_nval && v_gext + 64 > MT_N);
+        v_nval |= (int)((tw >> lane) & 1ull);
+        v_twisted = (int)((tw >> lane) & 1ull);
+        // ---- one pass: 64 words of every env with work, all loads first
+        uint32_t w[NE];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int gext = __builtin_amdgcn_readlane(v_gext, e);
+            const int par = mi_par(mi[e]);
+            const int p = gext + lane;
+            const uint32_t off = (uint32_t)e * MT_WORDS +
+                                 (p < MT_N ? (uint32_t)par * MT_ALT + (uint32_t)p
+                                           : (uint32_t)(1 - par) * MT_ALT + (uint32_t)min(p - MT_N, MT_N - 1));
+            // (the next block may have been written by this wave's previous pass: an L2 load)
+            w[e] = ((work >> e) & 1ull) && !((tw >> e) & 1ull) ? (gext + 64 > MT_N ? load_l2(wrow + off) : wrow[off])
+                                                                : 0u;
+        }
+#ifdef DRL_STAMPS
+        rs_ntw += __popcll(tw);
+#endif
+        while (tw) {
+            int te[kTwistBatch];
+            uint32_t x[kTwistBatch][10];
+#pragma unroll
+            for (int t = 0; t < kTwistBatch; ++t) {
+                te[t] = tw ? __ffsll((unsigned long long)tw) - 1 : -1;
+                if (tw) tw &= tw - 1ull;
+                if (te[t] >= 0) {
+                    // the stream's block: not written by this kernel, plain loads
+                    const uint32_t* src = wrow + (uint32_t)te[t] * MT_WORDS +
+                                          (uint32_t)__builtin_amdgcn_readlane(v_par, te[t]) * MT_ALT;
+#pragma unroll
+                    for (int c = 0; c < 10; ++c) x[t][c] = (64 * c + lane < MT_N) ? src[64 * c + lane] : 0u;
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < kTwistBatch; ++t) {
+                if (te[t] >= 0) {
+                    // the pass's words: positions g0 + lane, old block below 624, new block from 624 (its
+                    // first chunk: g0 <= 624 here)
+                    const int g0 = __builtin_amdgcn_readlane(v_gext, te[t]);
+                    const int c0 = g0 >> 6, sl = (g0 + lane) & 63;
+                    uint32_t xa = 0u, xb = 0u;
+#pragma unroll
+                    for (int c = 0; c < 10; ++c) {
+                        xa = c == c0 ? x[t][c] : xa;
+                        xb = c == c0 + 1 ? x[t][c] : xb;
+                    }
+                    const uint32_t oa = (uint32_t)__shfl((int)xa, sl), ob = (uint32_t)__shfl((int)xb, sl);
+                    const uint32_t wold = (g0 & 63) + lane < 64 ? oa : ob;
+                    twist_regs(x[t], lane);
+                    const uint32_t wnew = (uint32_t)__shfl((int)x[t][0], (g0 + lane - MT_N) & 63);  // new word p - 624
+                    const uint32_t wt = g0 + lane < MT_N ? wold : wnew;
+#pragma unroll
+                    for (int e = 0; e < NE; ++e) w[e] = te[t] == e ? wt : w[e];
+                    uint32_t* dst = wrow + (uint32_t)te[t] * MT_WORDS +
+                                    (uint32_t)(1 - __builtin_amdgcn_readlane(v_par, te[t])) * MT_ALT;
+#pragma unroll
+                    for (int c = 0; c < 10; ++c)
+                        if (64 * c + lane < MT_N) dst[64 * c + lane] = x[t][c];
+                }
+            }
+        }
+#ifdef DRL_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        DRL_SUBT(rs_b);
+        rs_tw += rs_b - rs_a;
+        rs_a = rs_b;
+#endif
+        // the pass's entries are kept in registers and stored after it: a
+        // store between two uses of w[] would make the next use wait for it
+        uint32_t ent[NE];
+        int eslot[NE];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            eslot[e] = -1;
+            ent[e] = 0u;
+            if (!((work >> e) & 1ull)) continue;  // uniform
+            const int gext = __builtin_amdgcn_readlane(v_gext, e);
+            const int cnt = __builtin_amdgcn_readlane(v_cnt, e);
+            const int yv = __builtin_amdgcn_readlane(v_y, e);
+            const int head = mi_head(mi[e]), tpar = mi_par(mi[e]);
+            const int p = gext + lane;
+            const int r = p < 2 * MT_N ? (int)(temper(w[e]) >> shift) : G;
+            const bool acc = r < G;
+            const uint64_t M = __ballot(acc);
+            const int hy = yv >= 0 ? 1 : 0;
+            const int ar = hy + mbcnt64(M);  // accepted draws before this one (+ a pending y)
+            if (lane == 0 && hy) rank_lds[0] = (uint32_t)yv;
+            if (acc) rank_lds[ar] = (uint32_t)r;
+            wave_sync();
+            const int slot = cnt + (ar >> 1);
+            if (acc && (ar & 1) && slot < CAND_Q) {
+                const int ycell = (int)rank_lds[ar - 1];
+                const int end = p + 1;  // extended position after the pair's second draw
+                eslot[e] = (head + slot) & (CAND_Q - 1);
+                ent[e] = ce_pack(ycell * G + r, end <= MT_N ? end : end - MT_N, end <= MT_N ? tpar : 1 - tpar);
+            }
+            const int tot = hy + __popcll(M);
+            const int ny = (tot & 1) ? (int)rank_lds[tot - 1] : -1;
+            wave_sync();
+            if (lane == e) {
+                v_cnt = min(cnt + (tot >> 1), CAND_Q);
+                v_y = ny;
+                v_gext = gext + 64;
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < NE; ++e)
+            if (eslot[e] >= 0) wrow[(uint32_t)e * MT_WORDS + MT_RING + (uint32_t)eslot[e]] = ent[e];
+#ifdef DRL_STAMPS
+        DRL_SUBT(rs_b);
+        rs_ps += rs_b - rs_a;
+#endif
+    }
+#ifdef DRL_STAMPS
+    {
+        unsigned long long t_end;
+        DRL_SUBT(t_end);
+        if (lane == 0) {
+            unsigned long long* r = g_stamps + (int64_t)blockIdx.x * 16;
+            r[0] = rs_t0; r[1] = rs_t1 - rs_t0; r[2] = rs_tw; r[3] = rs_ps; r[4] = t_end - rs_t0; r[5] = rs_ntw;
+            r[6] = rs_np; r[7] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+#endif
+    // (a pending y at the end is dropped: the next refill re-reads it)
+    uint32_t wout = mi[0];
+#pragma unroll
+    for (int e = 1; e < NE; ++e) wout = lane == e ? mi[e] : wout;
+    if (lane < nenv_w) a.mt_index[env0 + lane] = (wout & ~(127u << 24)) | ((uint32_t)v_cnt << 24);
 }
 
 // ------------------------------------------------------- synthetic actions ---
@@ -1715,8 +2095,25 @@ hipError_t launch_encode(uint32_t* drones, int64_t E, int N, const int32_t* orde
     return hipGetLastError();
 }
 
-hipError_t launch_mt_index_check(uint32_t* mt_index, int64_t E, int32_t* err, hipStream_t s) {
-    hipLaunchKernelGGL(drl_mt_index_check_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, mt_index, E, err);
+hipError_t launch_refill(const RefillArgs& a, hipStream_t s) {
+    const int64_t blocks = (a.E + kRefillEnvs - 1) / kRefillEnvs;
+    hipLaunchKernelGGL(drl_refill_kernel, dim3((unsigned)blocks), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_mt_get(const uint32_t* mt, const uint32_t* mt_index, int64_t E, uint32_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(drl_mt_get_kernel, dim3((unsigned)((E * 625 + 255) / 256)), dim3(256), 0, s, mt, mt_index, E, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_mt_block0(uint32_t* mt, uint32_t* mt_index, int64_t E, hipStream_t s) {
+    hipLaunchKernelGGL(drl_mt_block0_kernel, dim3((unsigned)((E * MT_N + 255) / 256)), dim3(256), 0, s, mt, mt_index, E);
+    return hipGetLastError();
+}
+
+hipError_t launch_mt_set(uint32_t* mt, uint32_t* mt_index, int64_t E, const uint32_t* in, int32_t* err, hipStream_t s) {
+    hipLaunchKernelGGL(drl_mt_set_kernel, dim3((unsigned)((E * 625 + 255) / 256)), dim3(256), 0, s, mt, mt_index, E, in,
+                       err);
     return hipGetLastError();
 }
 

@@ -17,8 +17,8 @@ from typing import Optional
 
 import torch
 
-from ._native import (DRL_ERR_BAD_ACTION, DRL_ERR_BAD_STATE, DRL_ERR_NO_FREE_CELL, DRL_MT_WORDS, DRL_STEP_OBS_STREAM, DroneRLError,
-                      DrlState, check, lib)
+from ._native import (DRL_ERR_BAD_ACTION, DRL_ERR_BAD_STATE, DRL_ERR_NO_FREE_CELL, DRL_MT_WORDS, DRL_STEP_OBS_STREAM,
+                      DRL_STEP_REFILL, DroneRLError, DrlState, check, lib)
 from .params import EnvParams
 
 
@@ -36,8 +36,10 @@ class DroneEnvState:
 
     ground : uint8 [E, ground_stride]  object code per cell, row-major (first side*side bytes)
     drones : int32 [E, n_drones]       packed u32 records in dict order O
-    mt     : int32 [E, 640]            CPython MT19937 state words 0..623
-    mt_index: int32 [E]                CPython's MT index (next word; 624 = twist first)
+    mt     : int32 [E, 1344]           two MT19937 blocks + the respawn-candidate ring
+    mt_index: int32 [E]                CPython's MT index (bits 0-9), the block holding the
+                                       stream (bit 10), ring head / count (bits 16-21 / 24-30)
+    (the stream's CPython getstate() words: BatchedDeliveryDrones.mt_words())
     """
     ground: torch.Tensor
     drones: torch.Tensor
@@ -92,6 +94,10 @@ class BatchedDeliveryDrones:
             mt_index=torch.full((E,), 624, dtype=torch.int32, device=dev),
         )
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        # steps between drl_refill top-ups of the respawn-candidate rings (0: never;
+        # the steps then draw every respawn from the MT stream themselves)
+        self.refill_every = int(L.refill_every)
+        self._since_refill = 0
 
     # ------------------------------------------------------------ core API --
     def reset(self, seed: Optional[int] = 0, env_mask: Optional[torch.Tensor] = None) -> DroneEnvState:
@@ -113,8 +119,16 @@ class BatchedDeliveryDrones:
                                  f"env_offset={self.env_offset}, num_envs={self.num_envs}")
         s = self.state.c()
         check(lib().drl_reset(ctypes.byref(self._cp), ctypes.byref(s), int(reseed), seed_base, _ptr(env_mask),
-                              _stream(self.device)), "drl_reset")
+                              _stream(self.device)), "drl_reset")  # (ends with a refill)
+        self._since_refill = 0
         return self.state
+
+    def refill(self):
+        """Top up every env's respawn-candidate ring (drl_refill; step() does it every
+        ``refill_every`` steps).  Never changes results, only where the MT draws happen."""
+        s = self.state.c()
+        check(lib().drl_refill(ctypes.byref(self._cp), ctypes.byref(s), _stream(self.device)), "drl_refill")
+        self._since_refill = 0
 
     def step(self, actions: torch.Tensor, obs_k: int = 0, rewards: Optional[torch.Tensor] = None,
              dones: Optional[torch.Tensor] = None, obs: Optional[torch.Tensor] = None, obs_stream: bool = False):
@@ -141,6 +155,11 @@ class BatchedDeliveryDrones:
             self._check_out(obs, torch.float32, (E, obs_k, W, W, 6), "obs")
         s = self.state.c()
         flags = DRL_STEP_OBS_STREAM if obs_stream else 0
+        if self.refill_every > 0:
+            self._since_refill += 1
+            if self._since_refill >= self.refill_every:
+                self._since_refill = 0
+                flags |= DRL_STEP_REFILL
         check(lib().drl_step_ex(ctypes.byref(self._cp), ctypes.byref(s), _ptr(actions), _ptr(rewards), _ptr(dones),
                                 _ptr(obs) if obs_k else None, int(obs_k), _ptr(self.err), flags,
                                 _stream(self.device)), "drl_step")
@@ -178,7 +197,8 @@ class BatchedDeliveryDrones:
         s = self.state.c()
         check(lib().drl_rollout(ctypes.byref(self._cp), ctypes.byref(s), T, _ptr(actions), E * N, _ptr(rewards),
                                 _ptr(dones), E * N if every_step else 0, _ptr(obs) if obs_k else None, int(obs_k),
-                                ostride, _ptr(self.err), _stream(self.device)), "drl_rollout")
+                                ostride, _ptr(self.err), _stream(self.device)), "drl_rollout")  # (ends with a refill)
+        self._since_refill = 0
         if obs_k:
             return rewards, dones, obs
         return rewards, dones
@@ -224,7 +244,7 @@ class BatchedDeliveryDrones:
                                _ptr(out["x"]), _ptr(out["charge"]), _ptr(out["carrying"]), _stream(self.device)),
               "drl_decode")
         out["ground"] = self.state.ground[:, :G * G].view(E, G, G)
-        out["mt_index"] = self.state.mt_index
+        out["mt_index"] = self.mt_words_device()[:, 624]
         return out
 
     def set_state(self, ground, order, y, x, charge, carrying, mt_words=None):
@@ -251,22 +271,32 @@ class BatchedDeliveryDrones:
             self.set_mt_words(mt_words)
 
     def set_mt_words(self, words625):
-        """Load CPython getstate() words (624 state words + index) for every env."""
+        """Load CPython getstate() words (624 state words + index) for every env
+        (drl_mt_set: block 0, then a refill of the candidate rings)."""
         w = torch.as_tensor(words625, dtype=torch.int64).reshape(-1, 625)
         w = (w & 0xFFFFFFFF).to(torch.int64)
-        w = torch.where(w >= 2**31, w - 2**32, w).to(torch.int32)
         if w.shape[0] == 1:
             w = w.expand(self.num_envs, 625)
+        if w.shape[0] != self.num_envs:
+            raise ValueError(f"need 1 or {self.num_envs} rows of 625 words, got {w.shape[0]}")
         if ((w[:, 624] < 0) | (w[:, 624] > 624)).any():
             raise ValueError("MT index must lie in [0, 624] (CPython setstate)")
-        w = w.to(self.device)
-        self.state.mt[:, :624].copy_(w[:, :624])
-        self.state.mt_index.copy_(w[:, 624])
+        w = torch.where(w >= 2**31, w - 2**32, w).to(torch.int32).to(self.device).contiguous()
+        s = self.state.c()
+        check(lib().drl_mt_set(ctypes.byref(self._cp), ctypes.byref(s), _ptr(w), _ptr(self.err), _stream(self.device)),
+              "drl_mt_set")
+        self._since_refill = 0
+
+    def mt_words_device(self) -> torch.Tensor:
+        """CPython getstate() words of every env, int32 [E, 625] on the device (drl_mt_get)."""
+        out = torch.empty((self.num_envs, 625), dtype=torch.int32, device=self.device)
+        s = self.state.c()
+        check(lib().drl_mt_get(ctypes.byref(self._cp), ctypes.byref(s), _ptr(out), _stream(self.device)), "drl_mt_get")
+        return out
 
     def mt_words(self):
         """CPython getstate() words (624 state words + index) per env, as int64 on the host."""
-        w = torch.cat([self.state.mt[:, :624], self.state.mt_index[:, None]], 1)
-        return w.cpu().to(torch.int64) & 0xFFFFFFFF
+        return self.mt_words_device().cpu().to(torch.int64) & 0xFFFFFFFF
 
     def check_errors(self):
         """Synchronise and raise if a kernel flagged an error since the last check."""

@@ -46,8 +46,16 @@ extern "C" {
 
 typedef struct ihipStream_t* hipStream_t;
 
-#define DRL_ABI_VERSION 3
-#define DRL_MT_WORDS 640     /* per-env MT19937 row: words 0..623 state (row padded to 2560 B) */
+#define DRL_ABI_VERSION 4
+/* Per-env RNG row of `mt` (u32 words, 5376 B):
+ *   [0, 624)     MT19937 block 0     the env's CPython stream lives in block
+ *   [624, 1248)  MT19937 block 1     mt_index.par (the other block is scratch)
+ *   [1248, 1312) respawn-candidate ring (DRL_CAND_SLOTS entries, see drl_refill)
+ *   [1312, 1344) padding (rows 64-B aligned) */
+#define DRL_MT_WORDS 1344
+#define DRL_MT_BLOCK1 624
+#define DRL_MT_RING 1248
+#define DRL_CAND_SLOTS 64
 #define DRL_MAX_DRONES 64
 #define DRL_MAX_SIDE 128
 #define DRL_MAX_RADIUS 8
@@ -96,15 +104,31 @@ typedef struct drl_layout {
     int32_t obs_floats;     /* floats per observed drone: window^2 * 6 */
     int32_t step_group_lanes; /* wavefront lanes per env in drl_step */
     int32_t step_lds_bytes;   /* dynamic LDS per block (one wavefront) of drl_step */
+    int32_t cand_slots;       /* respawn-candidate ring entries per env (DRL_CAND_SLOTS) */
+    int32_t refill_every;     /* recommended drl_refill cadence in steps (DRL_STEP_REFILL) */
 } drl_layout;
 
 /* Device state of num_envs envs (structure of arrays, env-major).
  *  ground : u8  [E][ground_stride]  object code per cell (row-major y*side+x)
  *  drones : u32 [E][n_drones]       one record per drone in dict order:
  *           bits 0-7 y, 8-15 x, 16-23 charge, 24 carrying, 25-31 drone index
- *  mt     : u32 [E][DRL_MT_WORDS]   CPython MT19937 state words 0..623
- *  mt_index: u32 [E]                CPython's MT index (next word; 624 = twist first),
- *                                   kept apart so a wave's envs share one cache line */
+ *  mt     : u32 [E][DRL_MT_WORDS]   two MT19937 blocks + the candidate ring (above)
+ *  mt_index: u32 [E]                bits 0-9 CPython's MT index (next word; 624 =
+ *                                   twist first), bit 10 `par` (the block holding
+ *                                   the stream), bits 16-21 ring head, bits 24-30
+ *                                   ring count; kept apart so a wave's envs share
+ *                                   one cache line.  A plain CPython index (0..624,
+ *                                   upper bits 0) is a valid word: block 0, empty ring.
+ *
+ * The candidate ring is a cache of the env's FUTURE respawn cells: entry k is
+ * the k-th (y, x) pair of accepted randint(0, side-1) draws ahead of the
+ * stream position (bits 0-13 cell y*side+x, bits 16-25 the MT index after its
+ * second draw, bit 26 that index's block).  Those cells depend on the stream
+ * alone, not on the board, so drl_refill can draw them in bulk off the step's
+ * critical path; drl_step consumes them in order, rejects occupied ones
+ * exactly as env.py:226-233 does, and falls back to drawing from the stream
+ * itself when the ring runs dry.  Results never depend on the ring's fill
+ * level: it only moves MT work out of the step. */
 typedef struct drl_state {
     uint8_t* ground;
     uint32_t* drones;
@@ -126,7 +150,8 @@ int drl_layout_query(const drl_params* p, drl_layout* out);
 /* reset() for every env (or every env with d_env_mask[e] != 0).
  * reseed != 0: first re-seed env e's stream as random.seed(seed_base + e)
  * (rl_helpers.py:18), then draw the reset exactly like env.py:68-101.
- * reseed == 0: continue each env's current stream (a plain env.reset()). */
+ * reseed == 0: continue each env's current stream (a plain env.reset()).
+ * Ends with a drl_refill of the respawn-candidate rings. */
 int drl_reset(const drl_params* p, const drl_state* s, int32_t reseed, uint64_t seed_base,
               const uint8_t* d_env_mask, hipStream_t stream);
 
@@ -144,6 +169,9 @@ int drl_step(const drl_params* p, const drl_state* s, const int32_t* d_actions, 
  * Without it the stores are cached, so a consumer launched next (the policy's
  * act) reads them from the caches.  Results are identical either way. */
 #define DRL_STEP_OBS_STREAM 1u
+/* DRL_STEP_REFILL: launch drl_refill after the step (callers pass it every
+ * layout.refill_every steps; the Python env and the env handles do). */
+#define DRL_STEP_REFILL 2u
 int drl_step_ex(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
                 uint8_t* d_dones, float* d_obs, int32_t obs_k, int32_t* d_err, uint32_t flags,
                 hipStream_t stream);
@@ -154,10 +182,25 @@ int drl_step_ex(const drl_params* p, const drl_state* s, const int32_t* d_action
  * writes d_rewards / d_dones + t * out_step_stride and d_obs + t *
  * obs_step_stride (element strides; out/obs stride 0 = every step overwrites
  * the same buffer, leaving the last step's).  The state stays on chip
- * between steps and is written back once at the end. */
+ * between steps and is written back once at the end; the rollout draws its
+ * respawns from the MT stream directly and ends with a drl_refill. */
 int drl_rollout(const drl_params* p, const drl_state* s, int32_t num_steps, const int32_t* d_actions,
                 int64_t act_step_stride, float* d_rewards, uint8_t* d_dones, int64_t out_step_stride, float* d_obs,
                 int32_t obs_k, int64_t obs_step_stride, int32_t* d_err, hipStream_t stream);
+
+/* Top up every env's respawn-candidate ring (see drl_state) from its MT
+ * stream: draws ahead of the stream position, twisting the next MT block into
+ * the scratch block when the ring crosses a block end.  Never changes the
+ * env's observable state.  drl_reset and drl_mt_set end with one. */
+int drl_refill(const drl_params* p, const drl_state* s, hipStream_t stream);
+
+/* The envs' CPython getstate() words: d_words u32 [E][625] = the 624 state
+ * words of the stream's block + the MT index (what random.getstate() holds). */
+int drl_mt_get(const drl_params* p, const drl_state* s, uint32_t* d_words, hipStream_t stream);
+/* random.setstate() for every env from d_words u32 [E][625] (then a refill).
+ * An index outside [0, 624] is clamped to 624 and raises DRL_ERR_BAD_STATE in
+ * d_err (nullable). */
+int drl_mt_set(const drl_params* p, const drl_state* s, const uint32_t* d_words, int32_t* d_err, hipStream_t stream);
 
 /* WindowedGridView observation (wrappers.py:10-31,55-73) of drone indices
  * 0..k-1: f32 [E][k][W][W][6]. */

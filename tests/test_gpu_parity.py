@@ -45,7 +45,7 @@ def oparams(p) -> OParams:
 def gpu_state(env, envs=None):
     d = env.decode()
     out = {k: d[k] for k in ["ground", "order", "y", "x", "charge", "carrying"]}
-    out["mt"] = torch.cat([env.state.mt[:, :624], env.state.mt_index[:, None]], 1)
+    out["mt"] = env.mt_words_device()  # the stream's getstate() words (drl_mt_get)
     if envs is not None:
         idx = torch.as_tensor(envs, device=env.device)
         out = {k: v.index_select(0, idx) for k, v in out.items()}
@@ -216,6 +216,37 @@ def test_rollout_matches_oracle(name, E, steps, every, monkeypatch):
         if check:
             assert_state(gpu_state(env), o.state(), f"{name} step {t}")
             np.testing.assert_array_equal(out[2].cpu().numpy(), o.obs(3, 1), err_msg=f"{name} step {t} obs")
+    env.check_errors()
+
+
+@pytest.mark.parametrize("refill", [0, 1, 3])
+@pytest.mark.parametrize("name,E,steps", [
+    ("c1_8x8_n4", 256, 120),
+    ("c2_16x16_n8", 1024, 150),
+    ("dense_10x10_n8", 600, 150),
+    ("c4_32x32_n16", 256, 80),
+    ("c5_64x64_n32", 96, 60),
+    ("bigside_128_n4", 40, 60),
+])
+def test_candidate_ring_cadence_matches_oracle(name, E, steps, refill):
+    """The respawn-candidate ring never changes results: topped up every step
+    (refill 1), every 3rd, or never after the reset's fill (0: it runs dry and
+    every later respawn is drawn from the stream in the step, from the end of
+    the ring's last entry, which may lie in the next MT block).  Rewards, dones
+    and the full state, MT words included, equal the oracle at every step."""
+    p = EnvParams(**CONFIGS[name])
+    env = Env(p, E)
+    env.refill_every = refill
+    env.reset(seed=17)
+    o = OracleMulti(oparams(p), E)
+    o.reset(17 + np.arange(E))
+    for t in range(1, steps + 1):
+        a = env.synth_actions(seed=31, step=t)
+        r, dn = env.step(a)
+        ro, do = o.step(a.cpu().numpy())
+        assert_rewards(r.cpu().numpy(), ro, f"{name} refill {refill} step {t}")
+        np.testing.assert_array_equal(dn.cpu().numpy().astype(bool), do, err_msg=f"{name} step {t} dones")
+        assert_state(gpu_state(env), o.state(), f"{name} refill {refill} step {t}")
     env.check_errors()
 
 
@@ -611,8 +642,10 @@ def test_rollout_equals_steps(name, E, T, k, monkeypatch):
         assert torch.equal(r[1], out[1][t]), f"{name} step {t} dones"
         if k:
             assert torch.equal(r[2], out[2][t]), f"{name} step {t} obs"
-    for f in ["ground", "drones", "mt", "mt_index"]:
+    for f in ["ground", "drones"]:
         assert torch.equal(getattr(a_env.state, f), getattr(b_env.state, f)), f"{name} final {f}"
+    # the streams (the rings differ: the rollout draws from the stream directly)
+    assert torch.equal(a_env.mt_words_device(), b_env.mt_words_device()), f"{name} final MT state"
     a_env.check_errors()
     b_env.check_errors()
 
