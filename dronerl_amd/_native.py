@@ -14,8 +14,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DRL_LIB") or os.path.join(_HERE, "libdronerl.so")
 
 DRL_ABI_VERSION = 4  # include/dronerl.h
-DRL_MT_WORDS = 1344  # per-env RNG row: two MT blocks + the respawn-candidate ring
-DRL_CAND_SLOTS = 64
+DRL_MT_WORDS = 1408  # per-env RNG row: two MT blocks + the respawn-candidate ring
+DRL_CAND_SLOTS = 128
 DRL_MAX_DRONES = 64
 DRL_MAX_SIDE = 128
 DRL_MAX_RADIUS = 8

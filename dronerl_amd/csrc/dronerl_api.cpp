@@ -83,15 +83,17 @@ int step_group_lanes(int n_drones, int gstride, int cells, int window) {
     return P;
 }
 
-// Steps between refills: a step consumes about 0.19 N candidates at the
-// benchmark shapes (respawns per env-step 1.23 / 1.94 / 3.50 at N = 8 / 16 /
-// 32, SURVEY.md §8 A7, plus rejected and ground-item draws), so a third of the
-// ring lasts about CAND_Q / (0.6 N) steps: 13 at C3, 6 at C4, 3 at C5.
-// DRL_REFILL_EVERY overrides it (A/B runs).
+// Steps between refills.  Ring entries used per env-step, measured at the
+// benchmark shapes with random actions (tools/ring_usage.py): mean 2.06 /
+// 2.56 / 3.44 and at most 17 at N = 8 / 16 / 32; over 16 steps at most 71 /
+// 71 / 93.  CAND_Q / (N/4 + 3) steps keep the worst env well inside the
+// ring: 25 at C3, 18 at C4, 11 at C5 (an env whose ring runs dry draws from
+// the stream in the step: slower, same results).  DRL_REFILL_EVERY overrides
+// it (A/B runs).
 int refill_cadence(int n_drones) {
     if (const char* v = getenv("DRL_REFILL_EVERY")) return atoi(v) > 0 ? atoi(v) : 1;
-    const int r = (int)(DRL_CAND_SLOTS / (0.6 * n_drones));
-    return r < 1 ? 1 : (r > 16 ? 16 : r);
+    const int r = (int)(DRL_CAND_SLOTS / (0.25 * n_drones + 3.0));
+    return r < 1 ? 1 : (r > 32 ? 32 : r);
 }
 
 int validate(const drl_params* p, drl_layout* L) {

@@ -13,15 +13,14 @@ constexpr int MT_WORDS = DRL_MT_WORDS;
 constexpr int MT_ALT = DRL_MT_BLOCK1;  // word offset of MT block 1 in an env's row
 constexpr int MT_RING = DRL_MT_RING;   // word offset of the respawn-candidate ring
 constexpr int CAND_Q = DRL_CAND_SLOTS; // ring entries (power of two)
-static_assert((CAND_Q & (CAND_Q - 1)) == 0 && CAND_Q <= 64, "ring size");
+constexpr int MT_RING_END = DRL_MT_RING_END;  // word: stream position after the ring's last entry
+static_assert((CAND_Q & (CAND_Q - 1)) == 0 && CAND_Q <= 128, "ring size");
 
 // mt_index word (include/dronerl.h): index | par << 10 | head << 16 | count << 24
 __host__ __device__ constexpr int mi_idx(uint32_t w) { return (int)(w & 0x3ffu); }
 __host__ __device__ constexpr int mi_par(uint32_t w) { return (int)((w >> 10) & 1u); }
 __host__ __device__ constexpr int mi_head(uint32_t w) { return (int)((w >> 16) & (uint32_t)(CAND_Q - 1)); }
-__host__ __device__ constexpr int mi_cnt(uint32_t w) {
-    return (int)((w >> 24) & 127u) < CAND_Q ? (int)((w >> 24) & 127u) : CAND_Q;
-}
+__host__ __device__ constexpr int mi_cnt(uint32_t w) { return (int)(w >> 24) < CAND_Q ? (int)(w >> 24) : CAND_Q; }
 __host__ __device__ constexpr uint32_t mi_pack(int idx, int par, int head, int cnt) {
     return (uint32_t)idx | ((uint32_t)par << 10) | ((uint32_t)head << 16) | ((uint32_t)cnt << 24);
 }

@@ -783,11 +783,10 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         // bitmap / ground.
         const int qcnt = env_ok ? mi_cnt(mword) : 0;
         const int GGc = G * G;
-        int start = 0;  // ring entries consumed (group-uniform)
-#pragma unroll
-        for (int r = 0; r < QL; ++r) {
-            if (!__ballot(env_ok && w < total)) break;
-            const int cell = ce_cell(cq[r]);
+        int start = 0;          // ring entries consumed (group-uniform)
+        uint32_t ent_last = 0;  // the last consumed entry (group-uniform)
+        auto batch = [&](const uint32_t cqr, const int r) __attribute__((always_inline)) {
+            const int cell = ce_cell(cqr);
             const bool valid = env_ok && P * r + j < qcnt && cell < GGc;
             const int ccell = valid ? cell : 0;
             const int tg = valid ? cell : -1 - j;  // unique negatives never match
@@ -809,9 +808,10 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
             }
             const int gobj = gl[ccell];
             const bool occ = bm_test(bm, ccell);
+            const int bend = min(P * (r + 1), qcnt);  // end of the batch's valid entries
 #pragma unroll
             for (int cs = 0; cs < 3; ++cs) {  // class steps: drones, packets, dropzones
-                const bool act = env_ok && w < total && start < P * (r + 1);
+                const bool act = env_ok && w < total && start < bend;
                 if (!__ballot(act)) break;
                 const bool isd = w < nR;
                 const int cls_end = isd ? nR : (w < nR + n_pack ? nR + n_pack : total);
@@ -833,25 +833,35 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
                         chg_push(W, grp, nchg, cell);
                     }
                 }
+                // the class ends at its last item, or takes the rest of the batch
+                const bool done = k == need;
+                const uint32_t el = (uint32_t)gshfl<P>((int)cqr, done ? hibit(C) : bend - 1 - P * r, lane);
                 if (act) {
-                    start = (k == need) ? P * r + hibit(C) + 1 : P * (r + 1);
+                    start = done ? P * r + hibit(C) + 1 : bend;
+                    ent_last = el;
                     w += k;
                 }
                 wave_sync();
             }
+        };
+#pragma unroll
+        for (int r = 0; r < QL; ++r) {
+            if (!__ballot(env_ok && w < total && start < qcnt)) break;
+            batch(cq[r], r);
+        }
+        // rare: more candidates than the lanes hold (e.g. many crashes at once):
+        // the ring's next entries, one more round trip per batch
+        for (int r = QL; r < CAND_Q / P; ++r) {
+            if (!__ballot(env_ok && w < total && start < qcnt)) break;
+            const uint32_t* ring = mt_w + (uint32_t)(env_ok ? grp : 0) * MT_WORDS + MT_RING;
+            batch(ring[(mi_head(mword) + j + P * r) & (CAND_Q - 1)], r);
         }
         if (crashed && my_item < w) pos = posidx[my_item];
         // stream position after the consumed entries; a dry ring continues from
-        // the end of the last entry it held (loaded)
+        // the end of its last entry
         const bool dry = env_ok && w < total;
-        const int ncons = dry ? min(qcnt, P * QL) : start;
-        const int ei = ncons > 0 ? ncons - 1 : 0;
-        uint32_t ent = (uint32_t)gshfl<P>((int)cq[0], ei % P, lane);
-#pragma unroll
-        for (int r = 1; r < QL; ++r) {
-            const uint32_t v = (uint32_t)gshfl<P>((int)cq[r], ei % P, lane);
-            ent = (ei / P == r) ? v : ent;
-        }
+        const int ncons = start;
+        const uint32_t ent = ent_last;
         midx = min(ncons > 0 ? ce_idx(ent) : mi_idx(mword), MT_N);
         const int mpar = ncons > 0 ? ce_par(ent) : mi_par(mword);
         // the ring served every item: the new word goes out now (a dry ring's
@@ -1801,27 +1811,26 @@ __global__ void __launch_bounds__(64) drl_refill_kernel(RefillArgs a) {
     unsigned long long rs_t0, rs_t1, rs_a, rs_b, rs_tw = 0, rs_ps = 0, rs_ntw = 0, rs_np = 0;
     DRL_SUBT(rs_t0);
 #endif
-    // ---- round trip 1: every env's mt_index word and ring
-    uint32_t mi[NE], rv[NE];
+    // ---- round trip 1: every env's mt_index word and ring-end position (lane e: env e)
+    uint32_t mi[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) mi[e] = a.mt_index[env0 + min(e, nenv_w - 1)];
+    const uint32_t gend = wrow[(uint32_t)min(lane, nenv_w - 1) * MT_WORDS + MT_RING_END];
+    // per-env state, env e in lane e: count, extended resume position (just
+    // after the ring's last entry, or the stream position for an empty ring),
+    // the last entry's end, pending y (-1: none), next block twisted
+    int v_cnt = CAND_Q, v_gext = 0, v_end = 0, v_y = -1, v_nval = 0, v_twisted = 0, v_par = 0;
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
-        mi[e] = a.mt_index[env0 + min(e, nenv_w - 1)];
-        rv[e] = wrow[(uint32_t)min(e, nenv_w - 1) * MT_WORDS + MT_RING + lane];
-    }
-    // per-env state, env e in lane e: count, extended resume position, pending
-    // y (-1: none), next block twisted, done
-    int v_cnt = CAND_Q, v_gext = 0, v_y = -1, v_nval = 0, v_twisted = 0, v_par = 0;
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        const int cnt = e < nenv_w ? mi_cnt(mi[e]) : CAND_Q;
-        const int head = mi_head(mi[e]), tpar = mi_par(mi[e]);
-        const uint32_t last = (uint32_t)__builtin_amdgcn_readlane((int)rv[e], (head + max(cnt, 1) - 1) & (CAND_Q - 1));
-        const int nval = cnt > 0 && ce_par(last) != tpar;
-        const int gext = cnt > 0 ? min(ce_idx(last), MT_N) + (nval ? MT_N : 0) : min(mi_idx(mi[e]), MT_N);
         if (lane == e) {
+            const int cnt = e < nenv_w ? mi_cnt(mi[e]) : CAND_Q;
             v_cnt = cnt;
-            v_gext = gext;
-            v_nval = nval;
+            // gend: MT index | block << 10 after the last entry (absolute block, like an entry's)
+            const int tpar = mi_par(mi[e]);
+            const bool nxt = cnt > 0 && (int)((gend >> 10) & 1u) != tpar;  // in the next block: twisted already
+            v_gext = cnt > 0 ? min((int)(gend & 0x3ffu), MT_N) + (nxt ? MT_N : 0) : min(mi_idx(mi[e]), MT_N);
+            v_end = v_gext;
+            v_nval = nxt;
             v_par = tpar;
         }
     }
@@ -1947,11 +1956,16 @@ __global__ void __launch_bounds__(64) drl_refill_kernel(RefillArgs a) {
             }
             const int tot = hy + __popcll(M);
             const int ny = (tot & 1) ? (int)rank_lds[tot - 1] : -1;
+            const int ncnt = min(cnt + (tot >> 1), CAND_Q);
+            // the end of the pass's last entry (the ring's end from now on)
+            const uint64_t L = __ballot(acc && (ar & 1) && slot == ncnt - 1);
+            const int lend = L ? gext + (__ffsll((unsigned long long)L) - 1) + 1 : -1;
             wave_sync();
             if (lane == e) {
-                v_cnt = min(cnt + (tot >> 1), CAND_Q);
+                v_cnt = ncnt;
                 v_y = ny;
                 v_gext = gext + 64;
+                v_end = lend >= 0 ? lend : v_end;
             }
         }
 #pragma unroll
@@ -1977,7 +1991,11 @@ __global__ void __launch_bounds__(64) drl_refill_kernel(RefillArgs a) {
     uint32_t wout = mi[0];
 #pragma unroll
     for (int e = 1; e < NE; ++e) wout = lane == e ? mi[e] : wout;
-    if (lane < nenv_w) a.mt_index[env0 + lane] = (wout & ~(127u << 24)) | ((uint32_t)v_cnt << 24);
+    if (lane < nenv_w) {
+        a.mt_index[env0 + lane] = (wout & 0x00ffffffu) | ((uint32_t)v_cnt << 24);
+        wrow[(uint32_t)lane * MT_WORDS + MT_RING_END] =
+            v_end <= MT_N ? (uint32_t)v_end | ((uint32_t)v_par << 10) : (uint32_t)(v_end - MT_N) | ((uint32_t)(1 - v_par) << 10);
+    }
 }
 
 // ------------------------------------------------------- synthetic actions ---

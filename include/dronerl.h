@@ -50,12 +50,15 @@ typedef struct ihipStream_t* hipStream_t;
 /* Per-env RNG row of `mt` (u32 words, 5376 B):
  *   [0, 624)     MT19937 block 0     the env's CPython stream lives in block
  *   [624, 1248)  MT19937 block 1     mt_index.par (the other block is scratch)
- *   [1248, 1312) respawn-candidate ring (DRL_CAND_SLOTS entries, see drl_refill)
- *   [1312, 1344) padding (rows 64-B aligned) */
-#define DRL_MT_WORDS 1344
+ *   [1248, 1376) respawn-candidate ring (DRL_CAND_SLOTS entries, see drl_refill)
+ *   1376         the stream position just after the ring's last entry: MT
+ *                index | block << 10 (valid while the ring holds entries)
+ *   [1377, 1408) padding (rows 64-B aligned) */
+#define DRL_MT_WORDS 1408
 #define DRL_MT_BLOCK1 624
 #define DRL_MT_RING 1248
-#define DRL_CAND_SLOTS 64
+#define DRL_MT_RING_END 1376
+#define DRL_CAND_SLOTS 128
 #define DRL_MAX_DRONES 64
 #define DRL_MAX_SIDE 128
 #define DRL_MAX_RADIUS 8
@@ -115,7 +118,7 @@ typedef struct drl_layout {
  *  mt     : u32 [E][DRL_MT_WORDS]   two MT19937 blocks + the candidate ring (above)
  *  mt_index: u32 [E]                bits 0-9 CPython's MT index (next word; 624 =
  *                                   twist first), bit 10 `par` (the block holding
- *                                   the stream), bits 16-21 ring head, bits 24-30
+ *                                   the stream), bits 16-22 ring head, bits 24-31
  *                                   ring count; kept apart so a wave's envs share
  *                                   one cache line.  A plain CPython index (0..624,
  *                                   upper bits 0) is a valid word: block 0, empty ring.

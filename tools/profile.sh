@@ -16,7 +16,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_
            "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT" \
            "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE" ${EXTRA_PMC:-}; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex drl_step -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py $PMC_ARGS > $OUT/pmc$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "${KREGEX:-drl_step|drl_refill}" -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py $PMC_ARGS > $OUT/pmc$i.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "pmc pass $i ($grp) rc=$rc"; tail -5 $OUT/pmc$i.log; fi
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi

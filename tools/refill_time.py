@@ -14,7 +14,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dronerl_amd import BatchedDeliveryDrones, EnvParams  # noqa: E402
 
-CFG = {"c3": (16, 8, 65536), "c4": (32, 16, 65536), "c5": (64, 32, 131072), "c2": (16, 8, 4096)}
+CFG = {"c3": (16, 8, 65536), "c3h": (16, 8, 32768), "c3q": (16, 8, 16384), "c4": (32, 16, 65536), "c5": (64, 32, 131072), "c2": (16, 8, 4096)}
 
 
 def timed_refill(env, s):
@@ -49,7 +49,7 @@ def main():
         for _ in range(args.reps):
             env.refill()
             env._since_refill = 0
-            cnt = (mi >> 24) & 127
+            cnt = (mi >> 24) & 255
             newc = torch.clamp(cnt - k, min=0)
             mi.copy_((mi & 0x00FFFFFF) | (newc << 24))
             ts.append(timed_refill(env, s))
