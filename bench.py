@@ -111,8 +111,8 @@ def measure_traffic(args):
              "--no-pmc-traffic", "--cached-steps", "0"]
     if args.envs:
         child += ["--envs", str(args.envs)]
-    if args.obs_cached:
-        child.append("--obs-cached")
+    if args.obs_stream:
+        child.append("--obs-stream")
     if args.obs_k >= 0:
         child += ["--obs-k", str(args.obs_k)]
     vals = {}
@@ -489,13 +489,15 @@ def main():
     ap.add_argument("--parallel-loop", action="store_true",
                     help="train loop with synth / replay on parallel graph branches (measured slower: the step "
                          "kernel fills every CU in one generation, and co-running kernels delay its waves)")
-    ap.add_argument("--obs-cached", action="store_true",
-                    help="write the per-step observation with cached stores (default: streaming, DRL_STEP_OBS_STREAM)")
+    ap.add_argument("--obs-stream", action="store_true",
+                    help="write the per-step observation with streaming stores (DRL_STEP_OBS_STREAM); default: "
+                         "cached stores, env.step()'s default and what a train_jax-style caller gets")
+    ap.add_argument("--obs-cached", action="store_true", help="(the default; kept for old command lines)")
     ap.add_argument("--obs-k", type=int, default=-1,
                     help="diagnostic: observed drones per step (default: the config's; 0 = step without obs)")
     ap.add_argument("--cached-steps", type=int, default=200,
-                    help="also time this many steps with cached observation stores (the drop-in env.step() "
-                         "default) and report them under `cached_obs` (0 = skip)")
+                    help="also time this many steps with the other observation store mode and report them under "
+                         "`streaming_obs` (or `cached_obs` with --obs-stream) (0 = skip)")
     ap.add_argument("--no-pmc-traffic", action="store_true",
                     help="do not run the rocprofv3 FETCH_SIZE / WRITE_SIZE passes for roofline.traffic")
     args = ap.parse_args()
@@ -544,11 +546,9 @@ def main():
     stream = torch.cuda.current_stream(dev)
     s_p = ctypes.c_void_p(stream.cuda_stream)
 
-    # the observation is bulk output here (nothing reads it before the next
-    # step overwrites it): streaming stores unless --obs-cached.  The train
-    # loop below, whose policy reads the observation right away, keeps cached
-    # stores.
-    flags = 0 if args.obs_cached else DRL_STEP_OBS_STREAM
+    # cached observation stores (env.step()'s default, what a train_jax-style
+    # caller gets) unless --obs-stream; the other mode is timed after it
+    flags = DRL_STEP_OBS_STREAM if args.obs_stream else 0
 
     # the respawn-candidate rings are topped up every refill_every steps (what
     # env.step() does), as a separate drl_refill launch bracketed by its own
@@ -603,12 +603,11 @@ def main():
     achieved = E * R / launch_s / 1e9
     achieved_rw = E * (R + Wb) / launch_s / 1e9
 
-    # the drop-in path: env.step()'s default cached observation stores (a
-    # consumer such as the act kernel reads the observation right away)
+    # the other observation store mode, same steps
     cached = None
-    if args.cached_steps > 0 and K > 0 and not args.obs_cached:
+    if args.cached_steps > 0 and K > 0:
         flags_main = flags
-        flags = 0
+        flags = 0 if args.obs_stream else DRL_STEP_OBS_STREAM
         nc = min(args.cached_steps, args.steps)
         for t in range(min(args.warmup, 20)):
             run(t)
@@ -631,8 +630,11 @@ def main():
         cached = {"value": E * world * nc / cwall, "unit": "env-steps/s", "steps": nc,
                   "ms_per_step": cwall / nc * 1e3, "avg_launch_us": c_launch * 1e6,
                   "frac": E * algorithmic_bytes(G, N, K, W)[0] / c_launch / 1e9 / PEAK_HBM_GBS,
-                  "note": "env.step() / drl_step default (cached observation stores): what a train_jax-style "
-                          "caller whose policy reads the observation next gets"}
+                  "obs_stores": "cached" if args.obs_stream else "streaming",
+                  "note": ("env.step() / drl_step default (cached observation stores): what a train_jax-style "
+                           "caller whose policy reads the observation next gets") if args.obs_stream else
+                          ("drl_step_ex(DRL_STEP_OBS_STREAM): streaming observation stores, for an observation "
+                           "no kernel reads right away; same results")}
 
     # resets (train_jax.py:101-113 resets every 100 steps in C5): timed separately
     resets_per_s = None
@@ -699,7 +701,7 @@ def main():
             "config": {"workload": f"{args.config.upper()}: {G}x{G} grid, {N} drones, {E} envs/GPU, "
                                    f"step + fused obs(K={K})",
                        "grid": G, "n_drones": N, "num_envs_per_gpu": E, "num_envs_total": E * world,
-                       "obs_k": K, "obs_stores": "cached" if args.obs_cached else "streaming",
+                       "obs_k": K, "obs_stores": "streaming" if args.obs_stream else "cached",
                        "parallelism": f"env-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS,
@@ -717,7 +719,7 @@ def main():
                                  "per launch: traffic",
                          "traffic_detail": traffic_src},
             "refill": refill,
-            "cached_obs": cached,
+            ("cached_obs" if args.obs_stream else "streaming_obs"): cached,
             "cpu_baseline": cpu,
             "resets_per_s": resets_per_s,
             "dqn_consumer": dqn,

@@ -864,10 +864,11 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         const uint32_t ent = ent_last;
         midx = min(ncons > 0 ? ce_idx(ent) : mi_idx(mword), MT_N);
         const int mpar = ncons > 0 ? ce_par(ent) : mi_par(mword);
-        // the ring served every item: the new word goes out now (a dry ring's
-        // after the draws below, with the block read back from mrow)
+        // the ring served every item: the new word waits in LDS until the
+        // write-back (a global store now would hold the first later vmcnt
+        // wait); a dry ring's is made after the draws below
         if (env_ok && j == 0 && !dry)
-            a.mt_index[wenv0 + grp] = mi_pack(midx, mpar, (mi_head(mword) + ncons) & (CAND_Q - 1), qcnt - ncons);
+            W.cnt[grp * 4 + 1] = mi_pack(midx, mpar, (mi_head(mword) + ncons) & (CAND_Q - 1), qcnt - ncons);
         mrow += (uint32_t)mpar * MT_ALT;
         wave_sync();
     }
@@ -1068,8 +1069,9 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         posidx[idx] = (uint16_t)pos;
     }
     if constexpr (!ROLL) {  // a dry ring: the stream position after the draws, an empty ring
-        if (env_ok && j == 0 && rounds > 0)
-            a.mt_index[wenv0 + grp] = mi_pack(midx, mrow != mt_w + (uint32_t)grp * MT_WORDS ? 1 : 0, 0, 0);
+        if (env_ok && j == 0)
+            a.mt_index[wenv0 + grp] = rounds > 0 ? mi_pack(midx, mrow != mt_w + (uint32_t)grp * MT_WORDS ? 1 : 0, 0, 0)
+                                                 : W.cnt[grp * 4 + 1];
     }
     wave_sync();
     if (!ROLL && env_ok) {

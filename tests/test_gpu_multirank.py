@@ -124,4 +124,4 @@ def test_bench_two_ranks_gloo_whole_job_json():
     assert d["value"] > 0 and d["ms_per_step"] > 0
     # value = every rank's env-steps over the slowest rank's wall time
     assert d["value"] == pytest.approx(2 * 4096 * 20 / (d["ms_per_step"] * 20 / 1e3), rel=1e-6)
-    assert d["cached_obs"]["value"] > 0
+    assert d["streaming_obs"]["value"] > 0 and d["config"]["obs_stores"] == "cached"
