@@ -34,16 +34,11 @@ __host__ __device__ constexpr uint32_t ce_pack(int cell, int idx, int par) {
 // ring entries each drl_step lane holds (P lanes per env: P * step_cq(P) candidates per step
 // without a second memory round trip; more come from the stream itself)
 constexpr int step_cq(int P) { return P <= 16 ? 2 : 1; }
-// DRL_ROLL_ACT_LDS: drl_rollout loads the next step's actions by LDS-DMA at the end of each step
-#ifndef DRL_ROLL_ACT_LDS
-#define DRL_ROLL_ACT_LDS 1
-#endif
 // DRL_DPP8: P = 8 / 16 claim and crash-order scans by DPP lane swaps instead of ds_bpermute
 #ifndef DRL_DPP8
 #define DRL_DPP8 1
 #endif
-// respawn rounds: D draws per lane (D*P MT outputs per round); the first
-// round's words (>= 16) are prefetched into LDS with the step's other loads
+// dry-ring respawn rounds: D draws per lane (D*P MT outputs per round)
 // (tuning knobs for tools/ab.py builds: DRL_DRAWS_P<P> overrides one width)
 #ifndef DRL_DRAWS_P8
 #define DRL_DRAWS_P8 2
@@ -57,30 +52,10 @@ constexpr int step_cq(int P) { return P <= 16 ? 2 : 1; }
 constexpr int step_draws(int P) {
     return P == 8 ? DRL_DRAWS_P8 : P == 16 ? DRL_DRAWS_P16 : P == 32 ? DRL_DRAWS_P32 : 1;
 }
-// drl_rollout keeps one draw per lane at P = 8: two spill under its 64-VGPR cap
-#ifndef DRL_ROLL_DRAWS_P8
-#define DRL_ROLL_DRAWS_P8 1
-#endif
-constexpr int roll_draws(int P) { return P == 8 ? DRL_ROLL_DRAWS_P8 : step_draws(P); }
-// MT words prefetched per env with the step's first loads: at least one
-// round's worth and 16; drl_step at P = 8 takes two rounds' (DRL_PF_P8), the
-// rollout one.  step_pf sizes the LDS area for both kernels.
-#ifndef DRL_PF_P8
-#define DRL_PF_P8 32
-#endif
-#ifndef DRL_PF_P16
-#define DRL_PF_P16 16
-#endif
-#ifndef DRL_PF_P32
-#define DRL_PF_P32 16
-#endif
-constexpr int pf_for(int D, int P, int floor) { return D * P < floor ? floor : D * P; }
-constexpr int roll_pf(int P) { return pf_for(roll_draws(P), P, 16); }
-constexpr int step_pf(int P) {
-    return pf_for(step_draws(P), P, P == 8 ? DRL_PF_P8 : P == 16 ? DRL_PF_P16 : P == 32 ? DRL_PF_P32 : 16) > roll_pf(P)
-               ? pf_for(step_draws(P), P, P == 8 ? DRL_PF_P8 : P == 16 ? DRL_PF_P16 : P == 32 ? DRL_PF_P32 : 16)
-               : roll_pf(P);
-}
+// drl_rollout (several steps per launch, state on chip) runs at P >= 16;
+// narrower groups roll out as drl_step launches (the 64-VGPR cap of their
+// 8-waves-per-SIMD occupancy leaves no room for the rollout's carried state)
+constexpr int kRolloutMinLanes = 16;
 constexpr int OBS_U = 1;        // observation cells per lane per pass (stage: OBS_U*1536 B per wave)
 
 // Per-env LDS layout of drl_step (WaveLds in dronerl_kernels.hip).  Shared by
@@ -274,7 +249,6 @@ hipError_t launch_encode(uint32_t* drones, int64_t E, int N, const int32_t* orde
                          const int32_t* x, const int32_t* c, const uint8_t* k, hipStream_t s);
 hipError_t launch_refill(const RefillArgs& a, hipStream_t s);
 hipError_t launch_mt_get(const uint32_t* mt, const uint32_t* mt_index, int64_t E, uint32_t* out, hipStream_t s);
-hipError_t launch_mt_block0(uint32_t* mt, uint32_t* mt_index, int64_t E, hipStream_t s);
 hipError_t launch_mt_set(uint32_t* mt, uint32_t* mt_index, int64_t E, const uint32_t* in, int32_t* err, hipStream_t s);
 hipError_t launch_synth(uint64_t seed, uint64_t step, int64_t env_offset, int64_t E, int N, int32_t* out,
                         hipStream_t s);

@@ -14,7 +14,8 @@
 //      items from the accepted (y, x) pairs with ballots.  The observation
 //      window is written from LDS with 16-B stores (streaming on request).
 //  drl_rollout_kernel<P>  the same per step, several steps per launch with
-//      the state on chip.
+//      the state on chip (P >= 16; narrower groups roll out as drl_step
+//      launches).
 //  drl_obs_kernel<P>   the same geometry, observation only.
 //  drl_reset_wave_kernel  one wavefront per env: MT state in registers,
 //      batched Fisher-Yates shuffles (64 draws per step) over an LDS list.
@@ -57,6 +58,18 @@ __device__ unsigned long long* g_stamps;
     do {            \
     } while (0)
 #endif
+
+// LDS pointer types: address arithmetic on them stays 32-bit (generic
+// pointers into LDS cost 64-bit math and registers the 64-VGPR kernels lack)
+typedef __attribute__((address_space(3))) uint8_t l_u8;
+typedef __attribute__((address_space(3))) uint16_t l_u16;
+typedef __attribute__((address_space(3))) uint32_t l_u32;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) u32x2 l_u2;
+typedef __attribute__((address_space(3))) u32x4 l_u4;
+typedef __attribute__((address_space(3))) f32x2 l_f2;
 
 // ---------------------------------------------------------------- helpers ---
 __device__ __forceinline__ void wave_sync() {
@@ -230,43 +243,43 @@ using GeoRT = Geo<0, 0, 0, -1>;
 //   -- scratch, dead once the step is written back; the observation's
 //      transpose stage (OBS_U*1536 B per wave) aliases it --
 //   bm     u32 [bm]       drone-occupancy bitmap of the cells (respawn mask)
-//   mtw    u32 [pf]       next MT words of the env's stream (prefetched, step_pf(P))
+//   stash  u32 [P]        drl_rollout: the drone records between steps (O order)
 //   chg    u16 [nchg]     ground cells changed this step (written back as bytes)
 //   cnt    u32 [4]        chg count
 struct WaveLds {
-    uint8_t* gl;
-    uint8_t* paint;
-    uint16_t* posidx;
-    uint32_t* bm;
-    uint32_t* mtw;
-    uint16_t* chg;
-    uint32_t* cnt;
-    unsigned char* stage;
+    l_u8* gl;
+    l_u8* paint;
+    l_u16* posidx;
+    l_u32* bm;
+    l_u32* stash;
+    l_u16* chg;
+    l_u32* cnt;
+    l_u8* stage;
 };
 
 template <class GEO>
-__device__ __forceinline__ WaveLds carve(unsigned char* wb, int gpw, int pf, const GEO& g) {
+__device__ __forceinline__ WaveLds carve(l_u8* wb, int gpw, int P, const GEO& g) {
     WaveLds w;
     w.gl = wb;
     wb += gpw * g.gstride();
     w.paint = wb;
     wb += gpw * g.lds_paint();
-    w.posidx = reinterpret_cast<uint16_t*>(wb);
+    w.posidx = reinterpret_cast<l_u16*>(wb);
     wb += gpw * g.np() * 2;
     w.stage = wb;
-    w.bm = reinterpret_cast<uint32_t*>(wb);
+    w.bm = reinterpret_cast<l_u32*>(wb);
     wb += gpw * g.lds_bm();
-    w.mtw = reinterpret_cast<uint32_t*>(wb);
-    wb += gpw * pf * 4;
-    w.chg = reinterpret_cast<uint16_t*>(wb);
+    w.stash = reinterpret_cast<l_u32*>(wb);
+    wb += gpw * P * 4;
+    w.chg = reinterpret_cast<l_u16*>(wb);
     wb += gpw * g.lds_chg();
-    w.cnt = reinterpret_cast<uint32_t*>(wb);
+    w.cnt = reinterpret_cast<l_u32*>(wb);
     return w;
 }
 
 // Async copy of the wave's grounds (contiguous in HBM, env-major) into LDS:
 // global_load_lds_dwordx4, 1 KiB per wave-instruction, no VGPR round trip.
-__device__ __forceinline__ void stage_ground_dma(const uint8_t* __restrict__ src, int nbytes, uint8_t* gl, int lane) {
+__device__ __forceinline__ void stage_ground_dma(const uint8_t* __restrict__ src, int nbytes, l_u8* gl, int lane) {
     const int nvec = nbytes / 16;
     for (int v0 = 0; v0 < nvec; v0 += 64) {
         if (v0 + lane < nvec)
@@ -281,7 +294,7 @@ __device__ __forceinline__ void stage_ground_dma(const uint8_t* __restrict__ src
 // loop).  Vectors past the wave's valid envs re-read the last valid vector
 // into LDS the wave does not use.
 template <int NV>
-__device__ __forceinline__ void stage_ground_dma_n(const uint8_t* __restrict__ src, int nbytes, uint8_t* gl, int lane) {
+__device__ __forceinline__ void stage_ground_dma_n(const uint8_t* __restrict__ src, int nbytes, l_u8* gl, int lane) {
     const uint32_t last = (uint32_t)(nbytes / 16 - 1);
 #pragma unroll
     for (int v0 = 0; v0 < NV; v0 += 64) {
@@ -299,19 +312,19 @@ __device__ __forceinline__ void stage_ground_dma_n(const uint8_t* __restrict__ s
 // train loop 73.6 us/step cached vs 76.5 streaming, although the step alone
 // is 11% faster streaming).
 template <bool NT>
-__device__ __forceinline__ void store_obs16(uint4* p, uint4 v) {
+__device__ __forceinline__ void store_obs16(uint4* p, u32x4 v) {
     if constexpr (NT) {
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        __builtin_nontemporal_store((u32x4){v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(p));
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
     } else {
-        *p = v;
+        *reinterpret_cast<u32x4*>(p) = v;
     }
 }
 
 // Zero [nbytes) of LDS (16-B multiple) cooperatively.
-__device__ __forceinline__ void lds_zero(void* p, int nbytes, int lane) {
-    uint4* q = reinterpret_cast<uint4*>(p);
-    for (int v = lane; v < nbytes / 16; v += 64) q[v] = make_uint4(0u, 0u, 0u, 0u);
+template <class T>
+__device__ __forceinline__ void lds_zero(T* p, int nbytes, int lane) {
+    l_u4* q = reinterpret_cast<l_u4*>(p);
+    for (int v = lane; v < nbytes / 16; v += 64) q[v] = (u32x4){0u, 0u, 0u, 0u};
 }
 
 // ------------------------------------------------------- observation write ---
@@ -365,16 +378,16 @@ __device__ __forceinline__ void write_obs_wave(float* __restrict__ base, int nen
         }
         if (wide) {
             // transpose through LDS: lane u*64+l's 24 B at stage[(u*64+l)*24], then 16-B stores
-            float2* st = reinterpret_cast<float2*>(w.stage);
+            l_f2* st = reinterpret_cast<l_f2*>(w.stage);
 #pragma unroll
             for (int u = 0; u < OBS_U; ++u) {
                 const int slot = (u * 64 + lane) * 3;
-                st[slot] = v[u][0];
-                st[slot + 1] = v[u][1];
-                st[slot + 2] = v[u][2];
+                st[slot] = (f32x2){v[u][0].x, v[u][0].y};
+                st[slot + 1] = (f32x2){v[u][1].x, v[u][1].y};
+                st[slot + 2] = (f32x2){v[u][2].x, v[u][2].y};
             }
             wave_sync();
-            const uint4* sv = reinterpret_cast<const uint4*>(w.stage);
+            const l_u4* sv = reinterpret_cast<const l_u4*>(w.stage);
             uint4* dst = reinterpret_cast<uint4*>(base + 6u * q0);
             if (q0 + 64u * OBS_U <= ncell) {  // full pass: 96*OBS_U 16-B pieces
 #pragma unroll
@@ -386,7 +399,7 @@ __device__ __forceinline__ void write_obs_wave(float* __restrict__ base, int nen
                     if (t * 16u + 16u <= nbytes) {
                         store_obs16<NT>(&dst[t], sv[t]);
                     } else {  // 8-byte tail
-                        reinterpret_cast<uint2*>(dst + t)[0] = reinterpret_cast<const uint2*>(sv + t)[0];
+                        reinterpret_cast<u32x2*>(dst + t)[0] = reinterpret_cast<const l_u2*>(sv + t)[0];
                     }
                 }
             }
@@ -409,7 +422,7 @@ __device__ __forceinline__ void write_obs_wave(float* __restrict__ base, int nen
 // Each drone paints its air byte into every observed window (drone indices
 // 0..K-1) that contains it.  posidx must be final.
 template <class GEO>
-__device__ __forceinline__ void paint_windows(uint8_t* paint, const uint16_t* posidx, int y, int x, uint8_t airbyte,
+__device__ __forceinline__ void paint_windows(l_u8* paint, const l_u16* posidx, int y, int x, uint8_t airbyte,
                                               const GEO& g) {
     const int W = (int)g.W(), K = g.K(), R = g.radius();
     for (int k = 0; k < K; ++k) {
@@ -422,12 +435,12 @@ __device__ __forceinline__ void paint_windows(uint8_t* paint, const uint16_t* po
 }
 
 __device__ __forceinline__ void chg_push(const WaveLds& w, int grp, int nchg_cap, int cell) {
-    const uint32_t q = atomicAdd(&w.cnt[grp * 4], 1u);
+    const uint32_t q = __atomic_fetch_add(&w.cnt[grp * 4], 1u, __ATOMIC_RELAXED);
     if (q < (uint32_t)nchg_cap) w.chg[grp * nchg_cap + q] = (uint16_t)cell;
 }
 
-__device__ __forceinline__ bool bm_test(const uint32_t* bm, int cell) { return (bm[cell >> 5] >> (cell & 31)) & 1u; }
-__device__ __forceinline__ void bm_set(uint32_t* bm, int cell) { atomicOr(&bm[cell >> 5], 1u << (cell & 31)); }
+__device__ __forceinline__ bool bm_test(const l_u32* bm, int cell) { return (bm[cell >> 5] >> (cell & 31)) & 1u; }
+__device__ __forceinline__ void bm_set(l_u32* bm, int cell) { __atomic_fetch_or(&bm[cell >> 5], 1u << (cell & 31), __ATOMIC_RELAXED); }
 
 // Group-relative lane masks: 32-bit when a group fits a 32-lane half.
 template <int P> struct GMaskT { using type = uint32_t; };  // P <= 32
@@ -500,10 +513,9 @@ template <int P, class GEO, bool ROLL, bool NT>
 __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     using GMask = typename GMaskT<P>::type;
     constexpr int GPW = 64 / P;
-    constexpr int D = ROLL ? roll_draws(P) : step_draws(P);  // draws per lane per respawn round
-    constexpr int PF = ROLL ? roll_pf(P) : step_pf(P);  // prefetched MT words per env
-    constexpr int PFR = (PF + P - 1) / P;        // prefetched MT words per lane (rollout)
-    constexpr int QL = step_cq(P);               // ring entries per lane (step)
+    static_assert(!ROLL || P >= kRolloutMinLanes, "narrow groups roll out as drl_step launches");
+    constexpr int D = step_draws(P);             // draws per lane per dry-ring respawn round
+    constexpr int QL = step_cq(P);               // ring entries per lane per batch
     using CM = typename GMaskT<(P * D <= 32 ? 32 : 64)>::type;  // round-position masks
     constexpr int CH = P < 16 ? P : 16;        // shuffle batch
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -515,7 +527,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     if (nenv_w <= 0) return;
     const bool env_ok0 = grp0 < nenv_w;
     const int G = g.side(), N = g.n(), gstride = g.gstride(), nchg = g.nchg();
-    const WaveLds W = carve(smem, GPW, PF, g);
+    const WaveLds W = carve((l_u8*)smem, GPW, P, g);
     // the wave's slices of the state (scalar bases)
     uint32_t* const drones_w = a.drones + wenv0 * N;
     uint32_t* const mt_w = a.mt + wenv0 * MT_WORDS;
@@ -523,12 +535,11 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     const uint32_t rl0 = (uint32_t)(grp0 * N);  // lane's env offset in [env][drone] arrays of the wave
 
     DRL_STAMP(0);
-    // ---- loads, in one round trip plus the MT-word prefetch: the env's MT
-    // index (one load per lane, all lanes of a group at one address), then the
-    // LDS zeroing (LDS writes must precede the LDS-DMA or they wait for it),
-    // the drone record and the action of drone index j, the ground by LDS-DMA,
-    // and last the MT words, which need the index.  Consumers of the ground
-    // and MT words come after the claims scan.
+    // ---- loads, in one round trip: the env's mt_index word (one load per
+    // lane, all lanes of a group at one address), then the LDS zeroing (LDS
+    // writes must precede the LDS-DMA or they wait for it), the drone record
+    // and the action of drone index j, the ground by LDS-DMA.  Consumers of
+    // the ground come after the claims scan.
     uint32_t mi[GPW];  // uniform addresses, nothing written before: scalar loads (lgkmcnt)
 #pragma unroll
     for (int e = 0; e < GPW; ++e) mi[e] = a.mt_index[wenv0 + min(e, nenv_w - 1)];
@@ -551,57 +562,40 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     uint32_t rec = active0 ? rec_ld : 0u;
     int my_action = active0 ? act_ld : 4;
     if (!env_ok0) mword = (uint32_t)MT_N;
-    // the stream position: drl_rollout reads it now (its stream is in block 0:
-    // drl_rollout launches drl_mt_block0_kernel first); drl_step only after
-    // the ring's entries, which carry it along, so nothing holds it across
-    // the claim phase
-    int midx = ROLL ? min(mi_idx(mword), MT_N) : 0;
-    uint32_t* const stash = W.mtw;  // ROLL: records between steps ([GPW][P], O order)
+    // the stream position is read only after the ring's entries (they carry
+    // it along), so nothing holds it across the claim phase; a rollout keeps
+    // the word (index, block, ring head / count) in a register between steps
+    int midx = 0;
+    l_u32* const stash = W.stash;  // ROLL: records between steps ([GPW][P], O order)
+    uint32_t cq[QL];  // the step's ring entries
+    auto ring_issue = [&](const uint32_t mw) __attribute__((always_inline)) {
+        const uint32_t rbase = (uint32_t)(env_ok0 ? grp0 : 0) * MT_WORDS + MT_RING;
+        const int qh = mi_head(mw);
+#pragma unroll
+        for (int r = 0; r < QL; ++r) cq[r] = mt_w[rbase + ((qh + j0 + P * r) & (CAND_Q - 1))];
+    };
     int act_next = 4;
     const int T = ROLL ? a.steps : 1;
-#if DRL_ROLL_ACT_LDS
-    // rollout: the next step's actions go straight to LDS (LDS-DMA into the
-    // change-list area, unused by rollouts) at the end of each step, so no
-    // register carries them across the observation phase
-    // (only where the 64-VGPR cap made the rollout spill: P <= 8 with the observation)
-    constexpr bool kActLds =
-        ROLL && P <= 8 && GEO::kObs && GEO::kN > 0 && GPW * lay::chg_bytes(GEO::kN > 0 ? GEO::kN : 1) >= 256;
-#else
-    constexpr bool kActLds = false;
-#endif
-    uint32_t* const actb = reinterpret_cast<uint32_t*>(W.chg);
-    if constexpr (kActLds) {  // lane i's action (index li) at actb[i], as the LDS-DMA leaves it
-        actb[lane0] = (uint32_t)act_ld;
-        wave_sync();
-    }
     for (int t = 0; t < T; ++t) {
-    // per-lane indices and LDS pointers, re-derived every step from an opaque
-    // copy of the lane id: in a rollout under the 64-VGPR cap (P <= 8),
-    // hoisting them (and the shuffle addresses) out of the loop spills
-    int lane_l = lane0;
-    if constexpr (ROLL && P <= 8) asm volatile("" : "+v"(lane_l));
-    const int lane = lane_l, grp = lane / P, j = lane % P;
+    const int lane = lane0, grp = lane / P, j = lane % P;
     const bool env_ok = grp < nenv_w;
     const bool active = env_ok && j < N;
     const uint32_t rl = (uint32_t)(grp * N);
     const uint32_t li = min(rl + (uint32_t)j, (uint32_t)(nenv_w * N - 1));
-    uint8_t* gl = W.gl + grp * gstride;
-    uint32_t* bm = W.bm + grp * (g.lds_bm() / 4);
-    uint32_t* mtw = W.mtw + grp * PF;
-    uint16_t* posidx = W.posidx + grp * g.np();
+    l_u8* gl = W.gl + grp * gstride;
+    l_u32* bm = W.bm + grp * (g.lds_bm() / 4);
+    l_u16* posidx = W.posidx + grp * g.np();
     const uint32_t* mrow = mt_w + (uint32_t)(env_ok ? grp : 0) * MT_WORDS;  // drl_step: set after the ring
     if constexpr (ROLL) {
         if (t > 0) {  // the previous step left its records in the stash
             rec = active ? stash[lane] : 0u;
-            if constexpr (kActLds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the actions' LDS-DMA
-            else my_action = active ? act_next : 4;
+            my_action = active ? act_next : 4;
             wave_sync();
             lds_zero(W.bm, GPW * g.lds_bm(), lane);
             if (GEO::kObs && a.obs) lds_zero(W.paint, GPW * g.lds_paint(), lane);
             wave_sync();
         }
-        if constexpr (!kActLds)
-            if (t + 1 < T) act_next = a.actions[(t + 1) * a.act_tstride + wenv0 * N + li];
+        if (t + 1 < T) act_next = a.actions[(t + 1) * a.act_tstride + wenv0 * N + li];
     }
 
     DRL_STAMP(1);
@@ -610,26 +604,24 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     int c = (rec >> 16) & 255u;
     int carry = (rec >> 24) & 1u;
     int act;  // actions are by drone index (env.py:125)
-    if constexpr (kActLds) act = (int)actb[grp * P + idx];  // lane grp*P + idx holds index grp*N + idx
-    else act = gshfl<P>(my_action, idx, lane);
-    // MT-word prefetch: issued once the records have landed (LDS-DMA makes the
-    // compiler wait for every outstanding load before the first record use),
-    // so its latency overlaps the claim / effect / ordering phases
-    // drl_step: the env's next P*QL ring entries (drl_refill drew them ahead)
-    // instead; the MT words are read only if the ring runs dry.
+    act = gshfl<P>(my_action, idx, lane);
+    // The env's next P*QL ring entries (drl_refill drew them ahead), issued
+    // once the records have landed (LDS-DMA makes the compiler wait for every
+    // outstanding load before the first record use), so their latency
+    // overlaps the claim / effect / ordering phases.  MT words are read only
+    // if the ring runs dry.
     __builtin_amdgcn_sched_barrier(0);
-    const int pf_base0 = midx;
-    int pfn = ROLL ? min(PF, MT_N - midx) : 0;
-    uint32_t pfw[ROLL ? PFR : 1];  // next MT words of the stream (addresses clamped: no per-word branch)
-    uint32_t cq[ROLL ? 1 : QL];    // ring entries head + j + P*r
+    ring_issue(mword);
+    // a rollout outlives its rings (one refill per launch): once an env's ring
+    // is empty, its first respawn round's MT words are loaded here too, so
+    // the dry draws do not start with a round trip
+    [[maybe_unused]] uint32_t pfq[ROLL ? D : 1];
+    [[maybe_unused]] bool pf_live = false;
     if constexpr (ROLL) {
+        pf_live = mi_cnt(mword) == 0 && mi_idx(mword) + D * P <= MT_N;
+        const uint32_t* src = mt_w + (uint32_t)(env_ok ? grp : 0) * MT_WORDS + (uint32_t)mi_par(mword) * MT_ALT;
 #pragma unroll
-        for (int r = 0; r < PFR; ++r) pfw[r] = mrow[min(midx + j + P * r, MT_N - 1)];
-    } else {
-        const uint32_t* ring = mt_w + (uint32_t)(env_ok ? grp : 0) * MT_WORDS + MT_RING;
-        const int qhead = mi_head(mword);
-#pragma unroll
-        for (int r = 0; r < QL; ++r) cq[r] = ring[(qhead + j + P * r) & (CAND_Q - 1)];
+        for (int q = 0; q < D; ++q) pfq[q] = load_l2(src + min(mi_idx(mword) + q * P + j, MT_N - 1));
     }
     __builtin_amdgcn_sched_barrier(0);
     if (active) {
@@ -758,11 +750,6 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     // every item: the round's candidate cells are read from LDS once and
     // several items are placed per round, later items seeing the cells placed
     // earlier in the round through register compares.
-    if constexpr (ROLL) {
-#pragma unroll
-        for (int r = 0; r < PFR; ++r)
-            if (j + P * r < pfn) mtw[j + P * r] = pfw[r];
-    }
 #ifdef DRL_DIAG_NO_RESPAWN  // timing-only diagnostic build (wrong results): the step without its respawn rounds
     int w = total, have_y = 0, yv = 0;
 #else
@@ -770,8 +757,8 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
 #endif
     const int shift = 32 - g.kbits();
     const int my_item = crashed ? newslot - nS : -1;  // this drone's respawn item
-    if constexpr (!ROLL) {
-        // ---- fast path (drl_step): the ring's candidate cells, i.e. the
+    {
+        // ---- fast path: the ring's candidate cells, i.e. the
         // stream's next accepted (y, x) pairs, P per batch, one per lane.  An
         // item takes the first candidate after the previous item's that is free
         // under its mask, so the items of one class (drones: drones |
@@ -830,7 +817,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
                         bm_set(bm, cell);
                     } else {
                         gl[cell] = (w + rank < nR + n_pack) ? OBJ_PACKET : OBJ_DROPZONE;
-                        chg_push(W, grp, nchg, cell);
+                        if constexpr (!ROLL) chg_push(W, grp, nchg, cell);
                     }
                 }
                 // the class ends at its last item, or takes the rest of the batch
@@ -859,7 +846,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         if (crashed && my_item < w) pos = posidx[my_item];
         // stream position after the consumed entries; a dry ring continues from
         // the end of its last entry
-        const bool dry = env_ok && w < total;
+        const bool dry = env_ok && w < total;  // (the ring's loaded entries are used up)
         const int ncons = start;
         const uint32_t ent = ent_last;
         midx = min(ncons > 0 ? ce_idx(ent) : mi_idx(mword), MT_N);
@@ -867,13 +854,15 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         // the ring served every item: the new word waits in LDS until the
         // write-back (a global store now would hold the first later vmcnt
         // wait); a dry ring's is made after the draws below
-        if (env_ok && j == 0 && !dry)
-            W.cnt[grp * 4 + 1] = mi_pack(midx, mpar, (mi_head(mword) + ncons) & (CAND_Q - 1), qcnt - ncons);
+        const uint32_t nword = mi_pack(midx, mpar, (mi_head(mword) + ncons) & (CAND_Q - 1), qcnt - ncons);
+        if constexpr (ROLL) {
+            if (!dry) mword = nword;
+        } else if (env_ok && j == 0 && !dry) {
+            W.cnt[grp * 4 + 1] = nword;
+        }
         mrow += (uint32_t)mpar * MT_ALT;
         wave_sync();
     }
-    int pf_base = pf_base0;
-    if constexpr (!ROLL) pf_base = midx;
     uint32_t rounds = 0;
     [[maybe_unused]] uint32_t rounds_w = 0;  // wave-level loop trips (diagnostics)
     [[maybe_unused]] unsigned long long sub_t0 = 0, sub_t1 = 0, sub_t2 = 0, sub_t3 = 0, sub_acc[4] = {0, 0, 0, 0};
@@ -886,25 +875,15 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         while (need) {
             const int tl = __ffsll((unsigned long long)need) - 1;
             need &= need - 1ull;
-#if !defined(DRL_DIAG_NO_TWIST) && !defined(DRL_DIAG_TWIST_FREE)  // timing-only builds (wrong streams)
-            if constexpr (ROLL) {  // the rollout's streams are in block 0
-                twist_wave(mt_w + (uint32_t)(tl / P) * MT_WORDS, lane);
-            } else {  // lane tl's stream block (either)
+#ifndef DRL_DIAG_NO_TWIST  // timing-only builds (wrong streams)
+            {  // lane tl's stream block (either)
                 const uint64_t pr = (uint64_t)(uintptr_t)mrow;
                 const uint64_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pr, tl);
                 const uint64_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pr >> 32), tl);
                 twist_wave(reinterpret_cast<uint32_t*>((hi << 32) | lo), lane);
             }
 #endif
-            if (grp == tl / P) {
-                midx = 0;
-                pf_base = 0;
-#ifdef DRL_DIAG_TWIST_FREE  // timing-only: as if the new block's first words were prefetched
-                pfn = PF;
-#else
-                pfn = 0;  // prefetched words are stale now
-#endif
-            }
+            if (grp == tl / P) midx = 0;
         }
         // ---- one round: D*P consecutive draws of this env's stream; position
         // d = q*P + j is lane j's q-th draw (branch-free; groups without work
@@ -919,13 +898,9 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         for (int q = 0; q < D; ++q) {
             const int d = q * P + j;
             const bool valid = work && d < avail;
-            const int off = midx - pf_base + d;
-            const bool inpf = off < pfn;
-            uint32_t word = mtw[min(max(off, 0), PF - 1)];
-            if (__ballot(valid && !inpf)) {  // beyond the prefetched words (rare)
-                const uint32_t gw = (valid && !inpf) ? load_l2(mrow + midx + d) : 0u;
-                word = inpf ? word : gw;
-            }
+            uint32_t word = 0u;
+            if constexpr (ROLL) word = pfq[q];  // (pf_live: the same words)
+            if (__ballot(valid && !pf_live)) word = (valid && !pf_live) ? load_l2(mrow + midx + d) : word;
             rq[q] = valid ? (int)(temper(word) >> shift) : G;
             accq[q] = rq[q] < G;
             mq[q] = gballot<P>(accq[q], gshift);
@@ -1010,6 +985,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
             }
         }
         DRL_SUBT(sub_t3);
+        if constexpr (ROLL) pf_live = false;
         if (work) {
             if (w >= total) {
                 midx += last + 1;  // draws after the last placement stay unconsumed
@@ -1068,15 +1044,16 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         a.dones[t * a.out_tstride + wenv0 * N + (rl + idx)] = crashed ? 1 : 0;
         posidx[idx] = (uint16_t)pos;
     }
-    if constexpr (!ROLL) {  // a dry ring: the stream position after the draws, an empty ring
-        if (env_ok && j == 0)
-            a.mt_index[wenv0 + grp] = rounds > 0 ? mi_pack(midx, mrow != mt_w + (uint32_t)grp * MT_WORDS ? 1 : 0, 0, 0)
-                                                 : W.cnt[grp * 4 + 1];
+    if constexpr (ROLL) {  // a dry ring: the stream position after the draws, an empty ring
+        if (rounds > 0) mword = mi_pack(midx, mrow != mt_w + (uint32_t)(env_ok ? grp : 0) * MT_WORDS ? 1 : 0, 0, 0);
+    } else if (env_ok && j == 0) {
+        a.mt_index[wenv0 + grp] = rounds > 0 ? mi_pack(midx, mrow != mt_w + (uint32_t)grp * MT_WORDS ? 1 : 0, 0, 0)
+                                             : W.cnt[grp * 4 + 1];
     }
     wave_sync();
     if (!ROLL && env_ok) {
         const uint32_t nc = W.cnt[grp * 4];
-        const uint16_t* ch = W.chg + grp * nchg;
+        const l_u16* ch = W.chg + grp * nchg;
         uint8_t* gdst = ground_w + (uint32_t)(grp * gstride);
         // Changes per step <= 4N (N pickups/deliveries, 2N respawned packets and
         // dropzones, N pick-after-respawn) < the list's 6N + 2 entries, so the
@@ -1098,20 +1075,14 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     if constexpr (ROLL) {  // records to the stash (the observation stage aliased it until here)
         wave_sync();
         if (active) stash[grp * P + newslot] = rec_out;
-        if constexpr (kActLds) {
-            if (t + 1 < T)  // after the last LDS write of the step (LDS writes after an LDS-DMA wait for it)
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void*)(a.actions + (t + 1) * a.act_tstride + wenv0 * N + li),
-                    (__attribute__((address_space(3))) void*)actb, 4, 0, 0);
-        }
     }
     }  // steps
     if constexpr (ROLL) {  // write the state back once: records, MT index, whole grounds
         wave_sync();
         if (active0) drones_w[rl0 + j0] = stash[lane0];
-        if (env_ok0 && j0 == 0) a.mt_index[wenv0 + grp0] = (uint32_t)midx;  // block 0, empty ring (stale now)
-        const uint4* src = reinterpret_cast<const uint4*>(W.gl);
-        uint4* dst = reinterpret_cast<uint4*>(ground_w);
+        if (env_ok0 && j0 == 0) a.mt_index[wenv0 + grp0] = mword;
+        const l_u4* src = reinterpret_cast<const l_u4*>(W.gl);
+        u32x4* dst = reinterpret_cast<u32x4*>(ground_w);
         for (int v = lane0; v < nenv_w * gstride / 16; v += 64) dst[v] = src[v];
     }
 }
@@ -1126,10 +1097,9 @@ drl_step_kernel(StepArgs a) {
     step_batch<P, GEO, false, NT>(a, (int64_t)blockIdx.x * (64 / P));
 }
 
-// drl_rollout: a.steps steps per launch, same wave layout.
+// drl_rollout: a.steps steps per launch, same wave layout (P >= 16).
 template <int P, class GEO>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : 1, 8)))
-drl_rollout_kernel(StepArgs a) {
+__global__ void __launch_bounds__(64) drl_rollout_kernel(StepArgs a) {
     step_batch<P, GEO, true, true>(a, (int64_t)blockIdx.x * (64 / P));
 }
 
@@ -1147,7 +1117,7 @@ __global__ void __launch_bounds__(64) drl_obs_kernel(StepArgs a) {
     if (nenv_w <= 0) return;
     const bool env_ok = grp < nenv_w;
     const int N = g.n(), gstride = g.gstride();
-    const WaveLds W = carve(smem, GPW, step_pf(P), g);
+    const WaveLds W = carve((l_u8*)smem, GPW, P, g);
     stage_ground_dma(a.ground + wenv0 * gstride, nenv_w * gstride, W.gl, lane);
     lds_zero(W.paint, GPW * g.lds_paint(), lane);
     const bool active = env_ok && j < N;
@@ -1155,7 +1125,7 @@ __global__ void __launch_bounds__(64) drl_obs_kernel(StepArgs a) {
     const int y = rec & 255u, x = (rec >> 8) & 255u;
     const int c = (rec >> 16) & 255u, carry = (rec >> 24) & 1u;
     const int idx = ((int)(rec >> 25) < N) ? (int)(rec >> 25) : j;
-    uint16_t* posidx = W.posidx + grp * g.np();
+    l_u16* posidx = W.posidx + grp * g.np();
     if (active) posidx[idx] = (uint16_t)(y * g.side() + x);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
@@ -1758,17 +1728,6 @@ __global__ void drl_mt_set_kernel(uint32_t* __restrict__ mt, uint32_t* __restric
     }
 }
 
-// drl_rollout draws from block 0 only: move a stream held in block 1 there.
-// (mt_index is left alone: every thread of the env reads its block bit; the
-// rollout writes the word back as block 0 with an empty ring.)
-__global__ void drl_mt_block0_kernel(uint32_t* __restrict__ mt, const uint32_t* __restrict__ mt_index, int64_t E) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= E * MT_N) return;
-    const int64_t e = t / MT_N;
-    const int k = (int)(t - e * MT_N);
-    if (mi_par(mt_index[e])) mt[e * MT_WORDS + k] = mt[e * MT_WORDS + MT_ALT + k];
-}
-
 // ---------------------------------------------------------------- refill ---
 // drl_refill: top up each env's respawn-candidate ring (include/dronerl.h).
 // The candidates are the (y, x) pairs of consecutive accepted randint(0,
@@ -2035,7 +1994,8 @@ static hipError_t launch_step_t(const StepArgs& a, hipStream_t s, int mode) {
         if constexpr (GEO::kObs) hipLaunchKernelGGL((drl_obs_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
         else return hipErrorInvalidValue;
     } else if (mode == kRolloutMode) {
-        hipLaunchKernelGGL((drl_rollout_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
+        if constexpr (P >= kRolloutMinLanes) hipLaunchKernelGGL((drl_rollout_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
+        else return hipErrorInvalidValue;
     } else if (GEO::kObs && a.obs && a.obs_nt) {
         hipLaunchKernelGGL((drl_step_kernel<P, GEO, GEO::kObs>), grid, block, a.wave_lds, s, a);
     } else {
@@ -2123,11 +2083,6 @@ hipError_t launch_refill(const RefillArgs& a, hipStream_t s) {
 
 hipError_t launch_mt_get(const uint32_t* mt, const uint32_t* mt_index, int64_t E, uint32_t* out, hipStream_t s) {
     hipLaunchKernelGGL(drl_mt_get_kernel, dim3((unsigned)((E * 625 + 255) / 256)), dim3(256), 0, s, mt, mt_index, E, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_mt_block0(uint32_t* mt, uint32_t* mt_index, int64_t E, hipStream_t s) {
-    hipLaunchKernelGGL(drl_mt_block0_kernel, dim3((unsigned)((E * MT_N + 255) / 256)), dim3(256), 0, s, mt, mt_index, E);
     return hipGetLastError();
 }
 

@@ -179,14 +179,16 @@ int drl_step_ex(const drl_params* p, const drl_state* s, const int32_t* d_action
                 uint8_t* d_dones, float* d_obs, int32_t obs_k, int32_t* d_err, uint32_t flags,
                 hipStream_t stream);
 
-/* num_steps steps in one launch (jax_impl run_steps, env/env.py:252-272, with
- * the rewards, dones and observation of every step): identical results to
- * num_steps drl_step calls.  Step t reads d_actions + t * act_step_stride and
- * writes d_rewards / d_dones + t * out_step_stride and d_obs + t *
- * obs_step_stride (element strides; out/obs stride 0 = every step overwrites
- * the same buffer, leaving the last step's).  The state stays on chip
- * between steps and is written back once at the end; the rollout draws its
- * respawns from the MT stream directly and ends with a drl_refill. */
+/* num_steps steps (jax_impl run_steps, env/env.py:252-272, with the rewards,
+ * dones and observation of every step): identical results to num_steps
+ * drl_step calls.  Step t reads d_actions + t * act_step_stride and writes
+ * d_rewards / d_dones + t * out_step_stride and d_obs + t * obs_step_stride
+ * (element strides; out/obs stride 0 = every step overwrites the same
+ * buffer, leaving the last step's).  With layout.step_group_lanes >= 16 the
+ * steps run in one launch with the state on chip, written back once at the
+ * end (respawns take ring entries while they last, then draw from the
+ * stream); narrower groups run one drl_step launch per step with a refill
+ * every layout.refill_every steps.  Ends with a drl_refill either way. */
 int drl_rollout(const drl_params* p, const drl_state* s, int32_t num_steps, const int32_t* d_actions,
                 int64_t act_step_stride, float* d_rewards, uint8_t* d_dones, int64_t out_step_stride, float* d_obs,
                 int32_t obs_k, int64_t obs_step_stride, int32_t* d_err, hipStream_t stream);

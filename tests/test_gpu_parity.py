@@ -612,10 +612,13 @@ def test_grid_obs_vs_oracle_state_and_compat_gridview():
     ("c2_16x16_n8", 1000, 60, 1),
     ("c2_16x16_n8", 257, 30, 0),
     ("c2_16x16_n8", 65, 25, 3),
-    ("c4_32x32_n16", 300, 30, 1),
-    ("c5_64x64_n32", 64, 20, 1),
+    # P >= 16 (the on-chip rollout kernel): long enough to use up the rings
+    # and continue from the streams within the launch
+    ("c4_32x32_n16", 300, 90, 1),
+    ("c4_32x32_n16|rt", 100, 70, 0),
+    ("c5_64x64_n32", 64, 70, 1),
     ("n6_11x11", 129, 50, 2),
-    ("n33_26x26", 33, 20, 1),
+    ("n33_26x26", 33, 60, 1),
     ("pool_5x5_n2", 100, 80, 1),
     ("dense_10x10_n8", 200, 60, 1),
     ("c2_16x16_n8|rt", 333, 30, 1),
@@ -644,7 +647,7 @@ def test_rollout_equals_steps(name, E, T, k, monkeypatch):
             assert torch.equal(r[2], out[2][t]), f"{name} step {t} obs"
     for f in ["ground", "drones"]:
         assert torch.equal(getattr(a_env.state, f), getattr(b_env.state, f)), f"{name} final {f}"
-    # the streams (the rings differ: the rollout draws from the stream directly)
+    # the streams (the rings may differ: refills at other points)
     assert torch.equal(a_env.mt_words_device(), b_env.mt_words_device()), f"{name} final MT state"
     a_env.check_errors()
     b_env.check_errors()
