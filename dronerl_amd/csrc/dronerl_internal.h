@@ -56,6 +56,12 @@ constexpr int step_draws(int P) {
 // narrower groups roll out as drl_step launches (the 64-VGPR cap of their
 // 8-waves-per-SIMD occupancy leaves no room for the rollout's carried state)
 constexpr int kRolloutMinLanes = 16;
+// DRL_ROLL_RING=0 builds a drl_rollout that discards the rings' entries and
+// draws every respawn from the stream (the round-1 rollout's registers: one
+// more wave per SIMD at C5); not yet measured against the default
+#ifndef DRL_ROLL_RING
+#define DRL_ROLL_RING 1
+#endif
 constexpr int OBS_U = 1;        // observation cells per lane per pass (stage: OBS_U*1536 B per wave)
 
 // Per-env LDS layout of drl_step (WaveLds in dronerl_kernels.hip).  Shared by

@@ -38,8 +38,8 @@ __device__ unsigned long long* g_stamps;
         unsigned long long t_;                                                           \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
         const int64_t sw_ = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); \
-        if ((threadIdx.x & 63) == 0) g_stamps[sw_ * 16 + (i)] = t_;                      \
-        if ((threadIdx.x & 63) == 0 && ((i) == 0 || (i) == 6))                           \
+        if ((threadIdx.x & 63) == 0 && g_stamps) g_stamps[sw_ * 16 + (i)] = t_;          \
+        if ((threadIdx.x & 63) == 0 && g_stamps && ((i) == 0 || (i) == 6))               \
             g_stamps[sw_ * 16 + 8 + (i) / 6] = __builtin_amdgcn_s_memrealtime();         \
         __builtin_amdgcn_sched_barrier(0);                                               \
     } while (0)
@@ -50,12 +50,31 @@ __device__ unsigned long long* g_stamps;
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");   \
         __builtin_amdgcn_sched_barrier(0);                                           \
     } while (0)
+// reset: clocks accumulated per category (uniform, in SGPRs), written at the end
+#define DRL_RS_DECL unsigned long long rs_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, rs_t0 = 0, rs_t1 = 0, rs_tt = 0
+#define DRL_RS_BEGIN() DRL_SUBT(rs_t0)
+#define DRL_RS_END(k)           \
+    do {                        \
+        DRL_SUBT(rs_t1);        \
+        rs_acc[k] += rs_t1 - rs_t0; \
+    } while (0)
+#define DRL_RS_COUNT(k) (++rs_acc[k])
 #else
 #define DRL_STAMP(i) \
     do {             \
     } while (0)
 #define DRL_SUBT(v) \
     do {            \
+    } while (0)
+#define DRL_RS_DECL
+#define DRL_RS_BEGIN() \
+    do {               \
+    } while (0)
+#define DRL_RS_END(k) \
+    do {              \
+    } while (0)
+#define DRL_RS_COUNT(k) \
+    do {                \
     } while (0)
 #endif
 
@@ -567,6 +586,13 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     // the word (index, block, ring head / count) in a register between steps
     int midx = 0;
     l_u32* const stash = W.stash;  // ROLL: records between steps ([GPW][P], O order)
+    // drl_rollout takes the rings' entries while they last, then draws from
+    // the stream.  DRL_ROLL_RING=0 discards the entries instead (they are a
+    // cache of the same draws; the refill at the end rebuilds them), which
+    // frees the ring code's registers: C5's rollout runs 3 waves per SIMD with
+    // it (126 -> 138 VGPRs) and measured 134-136 us/step against 119.5 for
+    // round 1's ring-less rollout.
+    constexpr bool kRing = !ROLL || DRL_ROLL_RING;
     uint32_t cq[QL];  // the step's ring entries
     auto ring_issue = [&](const uint32_t mw) __attribute__((always_inline)) {
         const uint32_t rbase = (uint32_t)(env_ok0 ? grp0 : 0) * MT_WORDS + MT_RING;
@@ -611,14 +637,14 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     // overlaps the claim / effect / ordering phases.  MT words are read only
     // if the ring runs dry.
     __builtin_amdgcn_sched_barrier(0);
-    ring_issue(mword);
-    // a rollout outlives its rings (one refill per launch): once an env's ring
-    // is empty, its first respawn round's MT words are loaded here too, so
-    // the dry draws do not start with a round trip
+    if constexpr (kRing) ring_issue(mword);
+    // once a rollout's ring is empty (or discarded), the first respawn
+    // round's MT words are loaded here too, so the stream draws do not start
+    // with a round trip
     [[maybe_unused]] uint32_t pfq[ROLL ? D : 1];
     [[maybe_unused]] bool pf_live = false;
     if constexpr (ROLL) {
-        pf_live = mi_cnt(mword) == 0 && mi_idx(mword) + D * P <= MT_N;
+        pf_live = (!kRing || mi_cnt(mword) == 0) && mi_idx(mword) + D * P <= MT_N;
         const uint32_t* src = mt_w + (uint32_t)(env_ok ? grp : 0) * MT_WORDS + (uint32_t)mi_par(mword) * MT_ALT;
 #pragma unroll
         for (int q = 0; q < D; ++q) pfq[q] = load_l2(src + min(mi_idx(mword) + q * P + j, MT_N - 1));
@@ -768,7 +794,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         // took).  One ballot and a rank place a whole class; the next class
         // starts after its last item.  Earlier batches' placements are in the
         // bitmap / ground.
-        const int qcnt = env_ok ? mi_cnt(mword) : 0;
+        const int qcnt = (kRing && env_ok) ? mi_cnt(mword) : 0;
         const int GGc = G * G;
         int start = 0;          // ring entries consumed (group-uniform)
         uint32_t ent_last = 0;  // the last consumed entry (group-uniform)
@@ -831,17 +857,19 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
                 wave_sync();
             }
         };
+        if constexpr (kRing) {
 #pragma unroll
-        for (int r = 0; r < QL; ++r) {
-            if (!__ballot(env_ok && w < total && start < qcnt)) break;
-            batch(cq[r], r);
-        }
-        // rare: more candidates than the lanes hold (e.g. many crashes at once):
-        // the ring's next entries, one more round trip per batch
-        for (int r = QL; r < CAND_Q / P; ++r) {
-            if (!__ballot(env_ok && w < total && start < qcnt)) break;
-            const uint32_t* ring = mt_w + (uint32_t)(env_ok ? grp : 0) * MT_WORDS + MT_RING;
-            batch(ring[(mi_head(mword) + j + P * r) & (CAND_Q - 1)], r);
+            for (int r = 0; r < QL; ++r) {
+                if (!__ballot(env_ok && w < total && start < qcnt)) break;
+                batch(cq[r], r);
+            }
+            // rare: more candidates than the lanes hold (e.g. many crashes at once):
+            // the ring's next entries, one more round trip per batch
+            for (int r = QL; r < CAND_Q / P; ++r) {
+                if (!__ballot(env_ok && w < total && start < qcnt)) break;
+                const uint32_t* ring = mt_w + (uint32_t)(env_ok ? grp : 0) * MT_WORDS + MT_RING;
+                batch(ring[(mi_head(mword) + j + P * r) & (CAND_Q - 1)], r);
+            }
         }
         if (crashed && my_item < w) pos = posidx[my_item];
         // stream position after the consumed entries; a dry ring continues from
@@ -1018,12 +1046,12 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
 #ifdef DRL_STAMPS
     if (lane == 0)
         for (int k = 0; k < 4; ++k)
-            g_stamps[((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + 10 + k] = sub_acc[k];
+            if (g_stamps) g_stamps[((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + 10 + k] = sub_acc[k];
 #endif
 
     DRL_STAMP(4);
 #ifdef DRL_STAMPS
-    if (lane == 0) g_stamps[((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + 7] = __builtin_amdgcn_readfirstlane(rounds_w);
+    if (lane == 0 && g_stamps) g_stamps[((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + 7] = __builtin_amdgcn_readfirstlane(rounds_w);
 #endif
     // ---- _pick_packets_after_respawn (env.py:217-224): distinct cells, parallel
     if (active && pos < 0) pos = 0;  // unreachable for valid params (respawn always finds a cell)
@@ -1550,10 +1578,13 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
             }
         }
     };
+    DRL_RS_DECL;
+    DRL_SUBT(rs_tt);
     settle();
     while (phase <= 4) {
         // ---- the current 64-word chunk of the env's stream (twist first when
         // it is used up): the single twist site
+        DRL_RS_BEGIN();
         if (midx >= MT_N) {
             if (rot)
                 for (; rot < 10; ++rot) rotate();  // back to canonical order (rot is 9 here)
@@ -1561,11 +1592,13 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
             midx = 0;
             rot = 0;
             tcur = temper(x[0]);
+            DRL_RS_COUNT(7);
         } else if ((midx >> 6) != rot) {  // next chunk
             rotate();
             ++rot;
             tcur = temper(x[0]);
         }
+        DRL_RS_END(1);
         const int c = rot;
         const int end = min(64 * c + 64, MT_N);
         // ---- consume the chunk's draws for the current phase (tight loops;
@@ -1574,10 +1607,14 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
             // the last shuffle only needs its top n_stat positions: below them
             // the draws are consumed without swapping
             const bool count_only = phase == 4 && si < n - a.n_stat;
+            DRL_RS_BEGIN();
             midx = 64 * c + fy_chunk(list, htab, ptab, tcur, lane, midx - 64 * c, end - 64 * c, si, ++epoch,
                                      count_only);
+            DRL_RS_END(count_only ? 2 : 0);
+            DRL_RS_COUNT(count_only ? 8 : 6);
             if (si != 0) continue;  // the shuffle goes on: nothing to settle
         } else if (phase != 1) {  // Fisher-Yates steps of a shuffle, one draw at a time; lane 0 swaps
+            DRL_RS_BEGIN();
             int kb_s = bitlen((uint32_t)si + 1u);
             while (midx < end && si >= 1) {
                 const uint32_t rr = (uint32_t)__builtin_amdgcn_readlane(tcur, midx & 63) >> (32 - kb_s);
@@ -1592,6 +1629,7 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
                     kb_s = bitlen((uint32_t)si + 1u);
                 }
             }
+            DRL_RS_END(3);
         } else if (a.pool_branch) {
             while (midx < end && si < N) {
                 const uint32_t m = (uint32_t)(n - si);
@@ -1607,6 +1645,7 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
                 }
             }
         } else {
+            DRL_RS_BEGIN();
             while (midx < end && si < N) {
                 const uint32_t rr = (uint32_t)__builtin_amdgcn_readlane(tcur, midx & 63) >> (32 - kb);
                 ++midx;
@@ -1615,10 +1654,19 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
                     ++si;
                 }
             }
+            DRL_RS_END(4);
         }
+        DRL_RS_BEGIN();
         settle();
+        DRL_RS_END(5);
     }
     wave_sync();
+#ifdef DRL_STAMPS
+    DRL_SUBT(rs_t1);
+    rs_acc[9] = rs_t1 - rs_tt;
+    if (lane == 0 && g_stamps)
+        for (int k = 0; k < 10; ++k) g_stamps[env * 16 + k] = rs_acc[k];
+#endif
 
     // drones in index order (dict order 0..N-1), then _pick_packets_after_respawn
     // (distinct cells: parallel)
@@ -1941,7 +1989,7 @@ __global__ void __launch_bounds__(64) drl_refill_kernel(RefillArgs a) {
     {
         unsigned long long t_end;
         DRL_SUBT(t_end);
-        if (lane == 0) {
+        if (lane == 0 && g_stamps) {
             unsigned long long* r = g_stamps + (int64_t)blockIdx.x * 16;
             r[0] = rs_t0; r[1] = rs_t1 - rs_t0; r[2] = rs_tw; r[3] = rs_ps; r[4] = t_end - rs_t0; r[5] = rs_ntw;
             r[6] = rs_np; r[7] = __builtin_amdgcn_s_memrealtime();

@@ -62,7 +62,8 @@ def main():
     env.reset(seed=0)
     P = env.layout.step_group_lanes
     nwaves = (E + 64 // P - 1) // (64 // P)
-    stamps = torch.zeros((nwaves + 64, 16), dtype=torch.int64, device="cuda")
+    # rows for every kernel of the stamps build: step waves, refill waves (E/4), resets (E)
+    stamps = torch.zeros((max(nwaves, E) + 64, 16), dtype=torch.int64, device="cuda")
     assert L.drl_debug_set_stamps(ctypes.c_void_p(stamps.data_ptr())) == 0
     acc = []
     rounds = []
