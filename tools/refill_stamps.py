@@ -28,7 +28,7 @@ def main():
     args = ap.parse_args()
     from stamps import build_stamps_lib
     if args.prebuilt:
-        path = os.path.join(REPO, "dronerl_amd", f"libdronerl_stamps{args.tag}.so")
+        path = os.path.join(REPO, "tools", f"libdronerl_stamps{args.tag}.so")
     else:
         path = build_stamps_lib([f for f in args.flags.split(",") if f], args.tag)
     if args.build_only:

@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--prebuilt", action="store_true")
     args = ap.parse_args()
     from stamps import build_stamps_lib
-    path = os.path.join(REPO, "dronerl_amd", "libdronerl_stamps.so") if args.prebuilt else build_stamps_lib()
+    path = os.path.join(REPO, "tools", "libdronerl_stamps.so") if args.prebuilt else build_stamps_lib()
     import dronerl_amd._native as nat
     nat.LIB_PATH = os.environ["DRL_LIB"] = path
     L = nat.lib()

@@ -23,7 +23,7 @@ import torch  # noqa: E402
 
 def build_stamps_lib(flags=(), tag=""):
     from dronerl_amd import build as b
-    out = os.path.join(REPO, "dronerl_amd", f"libdronerl_stamps{tag}.so")
+    out = os.path.join(REPO, "tools", f"libdronerl_stamps{tag}.so")  # never beside the product library
     cmd = [b.hipcc(), f"--offload-arch={b.ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DDRL_STAMPS",
            "-I", os.path.join(REPO, "include"), "-o", out] + list(flags) + b.SOURCES
     subprocess.run(cmd, check=True)
@@ -43,7 +43,7 @@ def main():
     args = ap.parse_args()
     flags = [f for f in args.flags.split(",") if f]
     if args.prebuilt:
-        path = os.path.join(REPO, "dronerl_amd", f"libdronerl_stamps{args.tag}.so")
+        path = os.path.join(REPO, "tools", f"libdronerl_stamps{args.tag}.so")
     else:
         path = build_stamps_lib(flags, args.tag)
     if args.build_only:
