@@ -45,6 +45,7 @@ int bit_length(uint32_t n) {
 constexpr int kStepLdsTarget = 64 * 1024;   // per block
 constexpr int kLdsMax = 160 * 1024;
 constexpr int kResetLdsTarget = 64 * 1024;
+constexpr int kFySerial = 4;    // reset (wave kernel): i-range writers per chunk resolved serially
 constexpr int kFyBatchMin = 1;  // reset (wave kernel): shuffle 64 draws at a time down to si = 1 (measured best)
 
 using drl::lay::r16;
@@ -265,13 +266,15 @@ int drl_reset(const drl_params* p, const drl_state* s, int32_t reseed, uint64_t 
     a.lanes = lanes > 64 ? 64 : lanes;
     a.block_lds = a.lanes * a.lane_lds;
     // one wavefront per env (DRL_RESET_WAVE=0 selects the lane-per-env kernel, for A/B)
-    a.wave_lds = drl::lay::fy_table_bytes + (2 * a.list_cap + 128 + (a.pool_branch ? 2 * a.list_cap : 0) + 15) / 16 * 16;
+    a.wave_lds = drl::lay::fy_table_bytes(GG) + (2 * a.list_cap + 256 + (a.pool_branch ? 2 * a.list_cap : 0) + 15) / 16 * 16;
     {
         const char* w = getenv("DRL_RESET_WAVE");
         a.wave_per_env = w ? atoi(w) : 1;
         const char* f = getenv("DRL_FY_BATCH_MIN");
         a.fy_batch_min = f ? atoi(f) : kFyBatchMin;
         if (a.fy_batch_min < 1) a.fy_batch_min = 1;
+        const char* c = getenv("DRL_FY_SERIAL");
+        a.fy_serial = c ? atoi(c) : kFySerial;
     }
     a.div_side = drl::make_fastdiv((uint32_t)p->side);
     hipError_t e = drl::launch_reset(a, stream);

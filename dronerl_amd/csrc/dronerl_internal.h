@@ -87,8 +87,9 @@ constexpr int qn_waves = DRL_QN_WAVES;  // act kernel: waves per workgroup (one 
 #define DRL_QN_TILES 2
 #endif
 constexpr int qn_tiles = DRL_QN_TILES;  // act kernel: 16-env tiles per pass sharing each weight fragment
-constexpr int fy_buckets = 256;                                   // reset: j-hash buckets (x2 hashes)
-constexpr int fy_table_bytes = (2 * fy_buckets + 64) * 4;        // ... + the 64 i slots, u32 each
+// reset (wave kernel): the batched shuffle's bitmap of j's (one bit per cell, in 16-B units) and
+// its 64 i-slot words
+constexpr int fy_table_bytes(int cells) { return ((((cells + 31) / 32 + 3) & ~3) + 64) * 4; }
 }  // namespace lay
 
 enum : int { OBJ_EMPTY = 0, OBJ_SKYSCRAPER = 2, OBJ_STATION = 3, OBJ_DROPZONE = 4, OBJ_PACKET = 5 };
@@ -166,6 +167,7 @@ struct ResetArgs {
     int lanes, lane_lds, list_cap, block_lds, pool_branch;
     int wave_per_env, wave_lds;  // drl_reset_wave_kernel (large grids) and its LDS bytes
     int fy_batch_min;            // wave kernel: shuffle 64 draws at a time while si >= this
+    int fy_serial;               // ... i-range writers per chunk resolved by readlanes (more: table + jumps)
     FastDiv div_side;
 };
 

@@ -130,27 +130,53 @@ __device__ __forceinline__ uint32_t pack_drone(int y, int x, int c, int carry, i
 // > c), mt[i-227] (i >= 227) and mt[0] (i = 623) are already new (chunks < c).
 // Lane offsets are constants (397 = 6*64 + 13, 227 = 4*64 - 29).
 __device__ __forceinline__ void twist_regs(uint32_t (&x)[10], int lane) {
-#pragma unroll
-    for (int c = 0; c < 10; ++c) {
-        const int i = 64 * c + lane;
-        // mt[i+1]: DPP wave_shl:1 (lane l reads lane l+1); lane 63 takes lane 0 of the next chunk
+    // mt[i+397] (old) or mt[i-227] (new): one bpermute per chunk, the source
+    // register chosen by the SENDING lane (the two source chunks occupy
+    // disjoint lane ranges); chunk 3 straddles i = 227 and takes two.  The
+    // bpermutes go out in four batches, each as soon as its sources are final
+    // (chunks 0-2 and 3's old half read old chunks 6-9; 3's new half, 4 and 5
+    // read new 0-2; 6-8 read new 2-5; 9 reads new 5-6).
+    // (the empty asm pins both sources in registers: folded into a select of
+    // addresses, the array would be indexed per lane and live in scratch)
+    auto pick = [&](bool lo, uint32_t a, uint32_t b) __attribute__((always_inline)) {
+        asm volatile("" : "+v"(a), "+v"(b));
+        return lo ? a : b;
+    };
+    auto far_old = [&](int c) __attribute__((always_inline)) {
+        return (uint32_t)__shfl(pick(lane < 13, x[c + 7], x[c + 6]), (lane + 13) & 63);
+    };
+    auto far_new = [&](int c) __attribute__((always_inline)) {
+        return (uint32_t)__shfl(pick(lane < 29, x[c - 3], x[c - 4]), (lane + 29) & 63);
+    };
+    auto step = [&](int c, uint32_t far) __attribute__((always_inline)) {
+        // mt[i+1]: DPP wave_shl:1 (lane l reads lane l+1); lane 63 takes lane 0
+        // of the next (old) chunk, and word 623 the new mt[0]
         uint32_t nxt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x[c], 0x130, 0xf, 0xf, false);
         if (c < 9) {
             const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)x[c + 1], 0);
             if (lane == 63) nxt = n0;
         } else {
-            const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)x[0], 0);  // new mt[0]
-            if (i == MT_N - 1) nxt = m0;
+            const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)x[0], 0);
+            if (lane == MT_N - 1 - 576) nxt = m0;
         }
-        const int l13 = lane + 13, l29 = lane + 29;
-        const uint32_t fo_a = (c + 6 < 10) ? __shfl(x[(c + 6) % 10], l13 & 63) : 0u;
-        const uint32_t fo_b = (c + 7 < 10) ? __shfl(x[(c + 7) % 10], l13 & 63) : 0u;
-        const uint32_t fn_a = (c >= 4) ? __shfl(x[(c + 6) % 10], l29 & 63) : 0u;  // x[c-4]
-        const uint32_t fn_b = (c >= 3) ? __shfl(x[(c + 7) % 10], l29 & 63) : 0u;  // x[c-3]
-        const uint32_t far = (i < MT_N - MT_M) ? (l13 < 64 ? fo_a : fo_b) : (l29 < 64 ? fn_a : fn_b);
         const uint32_t y = (x[c] & 0x80000000u) | (nxt & 0x7fffffffu);
         x[c] = far ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-    }
+    };
+    const uint32_t f0 = far_old(0), f1 = far_old(1), f2 = far_old(2);
+    const uint32_t f3o = (uint32_t)__shfl(x[9], (lane + 13) & 63);
+    step(0, f0);
+    step(1, f1);
+    step(2, f2);
+    const uint32_t f3n = (uint32_t)__shfl(x[0], (lane + 29) & 63);
+    const uint32_t f4 = far_new(4), f5 = far_new(5);
+    step(3, lane < MT_N - MT_M - 192 ? f3o : f3n);
+    step(4, f4);
+    step(5, f5);
+    const uint32_t f6 = far_new(6), f7 = far_new(7), f8 = far_new(8);
+    step(6, f6);
+    step(7, f7);
+    step(8, f8);
+    step(9, far_new(9));
 }
 
 // In-place twist of the env row in global memory (register-resident).
@@ -1393,8 +1419,6 @@ __global__ void __launch_bounds__(64) drl_reset_kernel(ResetArgs a) {
 }
 
 // ------------------------------------------------------- reset (wave/env) ---
-constexpr int kFyBuckets = lay::fy_buckets;
-
 __device__ __forceinline__ int mbcnt64(uint64_t m) {  // set bits of m below this lane
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -1405,90 +1429,204 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {  // set bits of m below thi
 // list advance exactly as the one-draw-at-a-time loop would leave them.
 //  1. acceptance: draw k is consumed iff fewer than si0 draws before it were
 //     accepted, and accepted iff r_k = u_k >> (32 - bitlen(s_k + 1)) <= s_k
-//     with s_k = si0 - (#accepted before k).  Membership of k depends only on
-//     lanes below k, so iterating the ballot from any start reaches the
-//     sequential answer, lanes settling left to right (usually 2-3 rounds).
+//     with s_k = si0 - (#accepted before k).  When bitlen(s + 1) is the same
+//     for every s the chunk can reach (all but ~12 chunks of a shuffle), r_k is
+//     fixed and #accepted-before lies in [0, k - l0]: one ballot of each bound
+//     decides every lane outside a narrow band; lanes inside it (and chunks
+//     whose width changes) iterate the ballot to its fixed point, lanes
+//     settling left to right.
 //  2. accepted draw t (rank t among them) swaps i_t = si0 - t with j_t = r_t.
 //     With A_t / B_t the values at i_t / j_t just before step t: i_t ends as
 //     B_t (later steps only touch smaller positions); A_t = A_p, p = the last
 //     earlier step whose j was i_t (else the original list[i_t]); B_t = A_q,
 //     q = the last earlier step with the same j (else the original list[j_t]);
-//     each j position ends as A of its last writer.  p comes from a 64-slot
-//     table over the i range (max writer lane, tagged with the batch epoch).
-//     For q, two 256-bucket tables keep the max writer lane per bucket of two
-//     hashes of j: a lane that is the max of either bucket has no later lane
-//     with its j (it is the last writer); the others -- every lane with a
-//     later duplicate, plus rare double hash collisions -- are the sources of
-//     an exact readlane loop that sets q for the later lanes with the same j.
-__device__ __forceinline__ int fy_chunk(uint16_t* list, uint32_t* htab, uint32_t* ptab, uint32_t u, int lane, int l0,
-                                        int l1, int& si, int epoch, bool count_only) {
-    const int si0 = si;
-    const bool valid = lane >= l0 && lane < l1;
-    uint64_t S = __ballot(valid);
-    for (;;) {
-        const int tk = mbcnt64(S), sk = si0 - tk;
-        const uint32_t rk = u >> (32 - bitlen((uint32_t)max(sk, 1) + 1u));
-        const uint64_t S2 = __ballot(valid && sk >= 1 && (int)rk <= sk);
-        if (S2 == S) break;
-        S = S2;
+//     each j position ends as A of its last writer.
+//     * p: the lanes whose j lies in the chunk's own i range are found by a
+//       compare (no LDS); an ascending readlane pass hands each one's A to
+//       the lane owning that i (ascending = the last writer wins, and its own
+//       A is final by then).  About 1.3 such lanes per chunk on average at
+//       64x64; past `serial_chains` of them (small lists, the ends of
+//       shuffles) a 64-slot table keeps the last writer per i slot and the
+//       chains are pointer-jumped with bpermutes instead.
+//     * q: a bitmap of j's (one bit per cell) OR-ed with return in the same
+//       LDS round trip as the list reads: a lane that finds its bit set has
+//       a repeated j (which lane of a pair sees it does not matter); each
+//       repeated-j group is then ordered by lane with readlanes.
+//     The bitmap bits are cleared by an AND after the writes.
+__device__ __forceinline__ uint64_t bal(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+
+// x[c] for a uniform c outside the hot loop: selects, so the register array
+// never needs a dynamic index (which sends it to scratch)
+__device__ __forceinline__ uint32_t xsel(const uint32_t (&x)[10], int c) {
+    uint32_t v = x[0];
+#pragma unroll
+    for (int k = 1; k < 10; ++k) {
+        uint32_t xk = x[k];
+        asm volatile("" : "+v"(xk));  // a select of values, not of addresses (see twist_regs)
+        v = c == k ? xk : v;
     }
-    const int m = popc(S);
-    si = si0 - m;
-    const int consumed = si == 0 ? hibit(S) + 1 : l1;
-    if (m == 0 || count_only) return consumed;
-    const bool acc = (S >> lane) & 1ull;
-    const int t = mbcnt64(S), s = si0 - t;
-    const uint32_t r = u >> (32 - bitlen((uint32_t)max(s, 1) + 1u));
-    const uint32_t tag = (uint32_t)epoch << 7, me = tag | (uint32_t)(lane + 1);
-    const int j = (int)r, ii = si0 - t, slot = si0 - j;  // slot: j's rank if j lies in the i range
-    const int h1 = j & (kFyBuckets - 1), h2 = kFyBuckets + (int)(((uint32_t)j * 0x9e3779b1u) >> 24);
-    uint32_t a0 = 0, l0j = 0, hv1 = 0, hv2 = 0, pv = 0;
-    if (acc) {
-        a0 = list[ii];
-        l0j = list[j];
-        atomicMax(&htab[h1], me);
-        atomicMax(&htab[h2], me);
-        if (slot < m && slot != t) atomicMax(&ptab[slot], me);
-    }
-    wave_sync();
-    if (acc) {
-        hv1 = htab[h1];
-        hv2 = htab[h2];
-        pv = ptab[t];
-    }
-    const int p = (acc && (pv >> 7) == (uint32_t)epoch) ? (int)(pv & 127u) - 1 : -1;  // writer lane
+    return v;
+}
+
+// Step 2 of a batched chunk: S = accepted lanes (m of them), r = their j.
+// Branch-light: every lane reads (rejected lanes read list[0] and OR a zero
+// bit), rejected lanes store into their own dummy slot (list index `dummy` +
+// lane) instead of running under an exec mask.
+__device__ __forceinline__ void fy_swaps(uint16_t* list, uint32_t* bmap, uint32_t* ptab, int dummy, uint64_t S, int m,
+                                         uint32_t r, int si0, int lane, uint64_t lanebit, int serial_chains) {
+    const bool acc = (S & lanebit) != 0ull;
+    const int t = mbcnt64(S);
+    const int j = acc ? (int)r : 0;
+    const int ii = si0 - t;    // >= 0 on every lane (t <= m <= si0)
+    const int slot = si0 - j;  // j's rank if j lies in the i range; rejected lanes: si0 >= m, none
+    const uint32_t bit = acc ? 1u << (j & 31) : 0u;
+    const uint32_t a0 = list[ii];
+    const uint32_t l0j = list[j];
+    const uint32_t old = __hip_atomic_fetch_or(bmap + (j >> 5), bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    uint64_t W = bal(slot < m);  // writers into the i range (self-swaps included: a no-op below)
     uint32_t A = a0;
-    if (__ballot(p >= 0)) {  // chains of p: jump to the root, whose A is its original list[i]
-        int f = p >= 0 ? p : lane;
+    if (popc(W) <= serial_chains) {
+        while (W) {  // ascending: the lane owning i = j takes this lane's A (rejected lanes' A is never stored)
+            const int k = lobit(W);
+            W &= W - 1;
+            const int sk = __builtin_amdgcn_readlane(slot, k);
+            const uint32_t ak = (uint32_t)__builtin_amdgcn_readlane((int)A, k);
+            if (t == sk) A = ak;
+        }
+    } else {  // many (small lists): last writer per i slot, then pointer jumping to the chain roots
+        const bool w = slot < m && slot != t;
+        if (w) __hip_atomic_fetch_max(ptab + slot, (uint32_t)lane + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        wave_sync();
+        const uint32_t pv = acc ? ptab[t] : 0u;
+        wave_sync();
+        if (w) ptab[slot] = 0u;
+        int f = pv ? (int)pv - 1 : lane;
         for (;;) {
             const int f2 = __shfl(f, f);
-            if (!__ballot(f2 != f)) break;
+            if (!bal(f2 != f)) break;
             f = f2;
         }
         A = __shfl(a0, f);
     }
-    int q = -1;
+    uint64_t D = bal((old & bit) != 0u);
+    uint32_t B = l0j;
     uint64_t notlast = 0;
-    uint64_t src = __ballot(acc && hv1 != me && hv2 != me);
-    while (src) {  // ascending: q ends as the last earlier lane with the same j
-        const int k = lobit(src);
-        src &= src - 1;
-        const int jk = __builtin_amdgcn_readlane(j, k);
-        const uint64_t later = __ballot(j == jk) & S & (~1ull << k);
-        if (later) {
-            notlast |= 1ull << k;
-            if ((later >> lane) & 1ull) q = k;
+    while (D) {  // one repeated-j group per pass; B of each member = A of the member below it
+        const int jk = __builtin_amdgcn_readlane(j, lobit(D));
+        uint64_t G = bal(j == jk) & S;
+        D &= ~G;
+        notlast |= G & ~(1ull << hibit(G));
+        int below = lobit(G);
+        G &= G - 1;
+        while (G) {
+            const int x = lobit(G);
+            G &= G - 1;
+            const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane((int)A, below);
+            if (lane == x) B = ab;
+            below = x;
         }
     }
-    uint32_t B = l0j;
-    if (__ballot(q >= 0)) {
-        const uint32_t Aq = __shfl(A, q >= 0 ? q : lane);
-        if (q >= 0) B = Aq;
-    }
-    if (acc && !((notlast >> lane) & 1ull)) list[j] = (uint16_t)A;  // j positions (i-range ones are rewritten next)
-    if (acc) list[ii] = (uint16_t)B;
+    // j positions first (i-range ones are rewritten next), then the i positions
+    list[((S & ~notlast) & lanebit) ? j : dummy + lane] = (uint16_t)A;
+    list[acc ? ii : dummy + lane] = (uint16_t)B;
+    __hip_atomic_fetch_and(bmap + (j >> 5), ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     wave_sync();
+}
+
+// A chunk anywhere in a shuffle (its first draws, the shuffle's end, a
+// count-only chunk): returns the first lane NOT consumed.
+__device__ __forceinline__ int fy_chunk(uint16_t* list, uint32_t* bmap, uint32_t* ptab, int dummy, uint32_t u, int lane,
+                                        uint64_t lanebit, int l0, int l1, int& si, bool count_only, int serial_chains) {
+    const int si0 = si;
+    const bool valid = lane >= l0 && lane < l1;
+    const int kb = bitlen((uint32_t)si0 + 1u);
+    const int slo = si0 - (l1 - 1 - l0);  // the smallest s a draw of this chunk can see
+    const bool uniform = slo >= 1 && bitlen((uint32_t)slo + 1u) == kb;
+    uint64_t S;
+    uint32_t r = u >> (32 - kb);
+    if (uniform) {
+        const uint64_t H = bal(valid & ((int)r <= si0));
+        S = H;
+        if (bal(valid & ((int)r + (lane - l0) <= si0)) != H) {
+            for (;;) {
+                const uint64_t S2 = bal(valid & ((int)r + mbcnt64(S) <= si0));
+                if (S2 == S) break;
+                S = S2;
+            }
+        }
+    } else {
+        S = bal(valid);
+        for (;;) {
+            const int sk = si0 - mbcnt64(S);
+            const uint32_t rk = u >> (32 - bitlen((uint32_t)max(sk, 1) + 1u));
+            const uint64_t S2 = bal(valid & (sk >= 1) & ((int)rk <= sk));
+            if (S2 == S) break;
+            S = S2;
+        }
+        r = u >> (32 - bitlen((uint32_t)max(si0 - mbcnt64(S), 1) + 1u));
+    }
+    const int m = popc(S);
+    si = si0 - m;
+    const int consumed = si == 0 ? hibit(S) + 1 : l1;
+    if (m != 0 && !count_only) fy_swaps(list, bmap, ptab, dummy, S, m, r, si0, lane, lanebit, serial_chains);
     return consumed;
+}
+
+// The reset's hot loop: whole chunks of one shuffle while every draw of a
+// chunk sees s >= 1 (the shuffle cannot end inside it), the register twist
+// inline, no phase bookkeeping.  The ten chunks of an MT block are unrolled, so
+// each reads its register x[c] by a static index.  Chunks that start below
+// swap_floor only count (the stations' shuffle needs its top positions only).
+// Leaves midx at the next unconsumed draw (MT_N: twist first) and tcur = the
+// tempered chunk holding midx.
+__device__ __forceinline__ void fy_run(uint16_t* list, uint32_t* bmap, uint32_t* ptab, int dummy, uint32_t (&x)[10],
+                                       uint32_t& tcur, int& midx, int& si, int swap_floor, int lane, uint64_t lanebit,
+                                       int serial_chains) {
+    for (;;) {
+        if (midx >= MT_N) {
+            twist_regs(x, lane);
+            midx = 0;
+        }
+#pragma unroll
+        for (int c = 0; c < 10; ++c) {
+            if ((midx >> 6) != c) continue;  // uniform: chunks before midx's are used up
+            const uint32_t u = temper(x[c]);
+            const int l0 = midx & 63, l1 = c == 9 ? MT_N - 576 : 64;
+            const int si0 = si;
+            if (si0 - (l1 - l0) < 1) {
+                tcur = u;
+                return;
+            }
+            const uint64_t V = (~0ull << l0) & (c == 9 ? (1ull << (MT_N - 576)) - 1ull : ~0ull);
+            const int kb = bitlen((uint32_t)si0 + 1u);
+            uint32_t r = u >> (32 - kb);
+            uint64_t S;
+            if (bitlen((uint32_t)(si0 - (l1 - 1 - l0)) + 1u) == kb) {  // one draw width over the chunk
+                const uint64_t H = bal((int)r <= si0) & V;
+                S = H;
+                if ((bal((int)r + lane <= si0 + l0) & V) != H) {
+                    for (;;) {
+                        const uint64_t S2 = bal((int)r + mbcnt64(S) <= si0) & V;
+                        if (S2 == S) break;
+                        S = S2;
+                    }
+                }
+            } else {  // the width drops inside the chunk (s >= 1 on every lane)
+                S = V;
+                for (;;) {
+                    const int sk = si0 - mbcnt64(S);
+                    const uint64_t S2 = bal((int)(u >> (32 - bitlen((uint32_t)sk + 1u))) <= sk) & V;
+                    if (S2 == S) break;
+                    S = S2;
+                }
+                r = u >> (32 - bitlen((uint32_t)(si0 - mbcnt64(S)) + 1u));
+            }
+            const int m = popc(S);
+            if (m != 0 && si0 >= swap_floor) fy_swaps(list, bmap, ptab, dummy, S, m, r, si0, lane, lanebit, serial_chains);
+            si = si0 - m;
+            midx = 64 * c + l1;
+        }
+    }
 }
 
 // One wavefront per env, for large grids (the lane-per-env kernel above is
@@ -1503,20 +1641,23 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
     const int lane = threadIdx.x;
     const int64_t env = blockIdx.x;
     if (env >= a.E || (a.mask != nullptr && a.mask[env] == 0)) return;  // whole wave, uniform
-    uint32_t* htab = reinterpret_cast<uint32_t*>(smem);  // batched shuffle: last writer per j bucket (2 hashes)
-    uint32_t* ptab = htab + 2 * kFyBuckets;               // ... and per i slot
+    uint32_t* bmap = reinterpret_cast<uint32_t*>(smem);  // batched shuffle: one bit per cell (repeated j's)
+    const int bwords = (a.cells + 31) >> 5;
+    uint32_t* ptab = bmap + ((bwords + 3) & ~3);  // ... and the last writer per i slot (many chains)
     uint16_t* list = reinterpret_cast<uint16_t*>(ptab + 64);
     uint16_t* sel = list + a.list_cap;
-    uint16_t* pool = sel + 64;
+    const int dummy = a.list_cap + 64;  // 64 u16 slots the batched shuffle's rejected lanes store into
+    uint16_t* pool = sel + 128;
+    const uint64_t lanebit = 1ull << lane;
     const int GG = a.cells, N = a.n_drones;
     const uint32_t w0 = a.reseed ? 0u : a.mt_index[env];
     const int par = mi_par(w0);  // the block holding the stream (a reseed writes block 0)
     uint32_t* mrow = a.mt + env * MT_WORDS + par * MT_ALT;
     uint8_t* grow = a.ground + env * a.gstride;
-    for (int i = lane; i < 2 * kFyBuckets + 64; i += 64) htab[i] = 0u;
+    for (int i = lane; i < ((bwords + 3) & ~3) + 64; i += 64) bmap[i] = 0u;
 
-    // x[k] holds words 64 * ((k + rot) % 10) + lane: the current chunk is
-    // always x[0] (moving to the next chunk rotates the array by one register)
+    // x[c] holds words 64c + lane (static indices only: fy_run unrolls the
+    // chunks, the rest selects with xsel)
     int midx = a.reseed ? MT_N : min(mi_idx(w0), MT_N);
     int rot = midx < MT_N ? midx >> 6 : 0;
     uint32_t x[10];
@@ -1524,20 +1665,11 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
         mt_seed_regs(x, a.seed_base + (uint64_t)env, lane);
     } else {
 #pragma unroll
-        for (int k = 0; k < 10; ++k) {
-            const int c = k + rot < 10 ? k + rot : k + rot - 10;
-            x[k] = (64 * c + lane < MT_N) ? load_l2(mrow + 64 * c + lane) : 0u;
-        }
+        for (int c = 0; c < 10; ++c) x[c] = (64 * c + lane < MT_N) ? load_l2(mrow + 64 * c + lane) : 0u;
     }
     for (int v = lane; v < a.gstride / 16; v += 64) reinterpret_cast<uint4*>(grow)[v] = make_uint4(0u, 0u, 0u, 0u);
     for (int i = lane; i < GG; i += 64) list[i] = (uint16_t)i;
-    uint32_t tcur = temper(x[0]);
-    auto rotate = [&]() __attribute__((always_inline)) {
-        const uint32_t x0 = x[0];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) x[k] = x[k + 1];
-        x[9] = x0;
-    };
+    uint32_t tcur = temper(xsel(x, rot));
     wave_sync();
 
     // The reset as a phase machine with ONE draw site (the register twist is
@@ -1545,7 +1677,7 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
     // shuffles for packets / dropzones / stations (env.py:68-101, random.py
     // shuffle :380-395 and sample :480-504).
     const int kb = bitlen((uint32_t)(GG - a.n_sky));  // sample's set branch: randbelow(n) bits
-    int n = GG, phase = 0, si = GG - 1, epoch = 0;
+    int n = GG, phase = 0, si = GG - 1;
     uint32_t mine = 0xffffffffu;  // set branch: lane q < N holds selection q
     auto place = [&](int count, uint8_t code) __attribute__((always_inline)) {  // pop `count` from the end
         wave_sync();
@@ -1586,30 +1718,31 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
         // it is used up): the single twist site
         DRL_RS_BEGIN();
         if (midx >= MT_N) {
-            if (rot)
-                for (; rot < 10; ++rot) rotate();  // back to canonical order (rot is 9 here)
             twist_regs(x, lane);
             midx = 0;
             rot = 0;
             tcur = temper(x[0]);
             DRL_RS_COUNT(7);
         } else if ((midx >> 6) != rot) {  // next chunk
-            rotate();
-            ++rot;
-            tcur = temper(x[0]);
+            rot = midx >> 6;
+            tcur = temper(xsel(x, rot));
         }
         DRL_RS_END(1);
         const int c = rot;
         const int end = min(64 * c + 64, MT_N);
         // ---- consume the chunk's draws for the current phase (tight loops;
         // si / midx stay uniform; readlane returns int: shift it as uint32)
-        if (phase != 1 && si >= a.fy_batch_min) {
+        if (phase != 1 && si > 64 && a.fy_batch_min <= 1) {  // the hot loop, until the shuffle's last chunk
+            fy_run(list, bmap, ptab, dummy, x, tcur, midx, si, phase == 4 ? n - a.n_stat : 0, lane, lanebit,
+                   a.fy_serial);
+            continue;
+        } else if (phase != 1 && si >= a.fy_batch_min) {
             // the last shuffle only needs its top n_stat positions: below them
             // the draws are consumed without swapping
             const bool count_only = phase == 4 && si < n - a.n_stat;
             DRL_RS_BEGIN();
-            midx = 64 * c + fy_chunk(list, htab, ptab, tcur, lane, midx - 64 * c, end - 64 * c, si, ++epoch,
-                                     count_only);
+            midx = 64 * c + fy_chunk(list, bmap, ptab, dummy, tcur, lane, lanebit, midx - 64 * c, end - 64 * c, si,
+                                     count_only, a.fy_serial);
             DRL_RS_END(count_only ? 2 : 0);
             DRL_RS_COUNT(count_only ? 8 : 6);
             if (si != 0) continue;  // the shuffle goes on: nothing to settle
@@ -1681,10 +1814,8 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
         a.drones[env * N + lane] = pack_drone((int)py, cell - (int)py * a.side, 100, carry, lane);
     }
 #pragma unroll
-    for (int k = 0; k < 10; ++k) {
-        const int c = k + rot < 10 ? k + rot : k + rot - 10;
-        if (64 * c + lane < MT_N) mrow[64 * c + lane] = x[k];
-    }
+    for (int c = 0; c < 10; ++c)
+        if (64 * c + lane < MT_N) mrow[64 * c + lane] = x[c];
     if (lane == 0) a.mt_index[env] = mi_pack(midx, par, 0, 0);  // the candidate ring is stale: empty
 }
 

@@ -4,7 +4,8 @@
 python tools/reset_rate.py --configs c3,c4,c5 --variants lane,wave,wave_fy64,wave_fy99999
 lane = drl_reset_kernel (lane per env); wave = drl_reset_wave_kernel with the
 batched shuffle (default: down to si = 1; wave_fyN: only while si >= N;
-wave_fy99999 = one draw at a time).  Knobs are env variables read per
+wave_fy99999 = one draw at a time; wave_serN: at most N i-range writers per
+chunk by readlanes, more by the slot table).  Knobs are env variables read per
 drl_reset call.  The streams are seeded once with the lane kernel (so a
 profiler filtered on drl_reset_wave sees only continuing resets); variants are
 timed in interleaved rounds after warm-up resets, and every variant's ground /
@@ -23,7 +24,7 @@ import torch  # noqa: E402
 from bench import CONFIGS  # noqa: E402
 from dronerl_amd import BatchedDeliveryDrones, EnvParams  # noqa: E402
 
-KNOBS = ("DRL_RESET_WAVE", "DRL_FY_BATCH_MIN")
+KNOBS = ("DRL_RESET_WAVE", "DRL_FY_BATCH_MIN", "DRL_FY_SERIAL")
 
 
 def set_knobs(v):
@@ -34,7 +35,9 @@ def set_knobs(v):
     elif v is not None:
         os.environ["DRL_RESET_WAVE"] = "1"
         if "_fy" in v:
-            os.environ["DRL_FY_BATCH_MIN"] = v.split("_fy")[1]
+            os.environ["DRL_FY_BATCH_MIN"] = v.split("_fy")[1].split("_")[0]
+        if "_ser" in v:
+            os.environ["DRL_FY_SERIAL"] = v.split("_ser")[1].split("_")[0]
 
 
 def snap(env):
