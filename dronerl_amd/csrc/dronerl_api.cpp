@@ -275,6 +275,7 @@ int drl_reset(const drl_params* p, const drl_state* s, int32_t reseed, uint64_t 
         if (a.fy_batch_min < 1) a.fy_batch_min = 1;
         const char* c = getenv("DRL_FY_SERIAL");
         a.fy_serial = c ? atoi(c) : kFySerial;
+        a.fy_bwords = drl::lay::fy_bitmap_words(GG);
     }
     a.div_side = drl::make_fastdiv((uint32_t)p->side);
     hipError_t e = drl::launch_reset(a, stream);

@@ -87,9 +87,14 @@ constexpr int qn_waves = DRL_QN_WAVES;  // act kernel: waves per workgroup (one 
 #define DRL_QN_TILES 2
 #endif
 constexpr int qn_tiles = DRL_QN_TILES;  // act kernel: 16-env tiles per pass sharing each weight fragment
-// reset (wave kernel): the batched shuffle's bitmap of j's (one bit per cell, in 16-B units) and
-// its 64 i-slot words
-constexpr int fy_table_bytes(int cells) { return ((((cells + 31) / 32 + 3) & ~3) + 64) * 4; }
+// reset (wave kernel): the batched shuffle's bitmap of j's -- one bit per cell over a power-of-two
+// count of words, at least 64 so that a chunk's ~46 ORs rarely share a word -- and its 64 i-slot words
+constexpr int fy_bitmap_words(int cells) {
+    int w = 64;
+    while (w * 32 < cells) w *= 2;
+    return w;
+}
+constexpr int fy_table_bytes(int cells) { return (fy_bitmap_words(cells) + 64) * 4; }
 }  // namespace lay
 
 enum : int { OBJ_EMPTY = 0, OBJ_SKYSCRAPER = 2, OBJ_STATION = 3, OBJ_DROPZONE = 4, OBJ_PACKET = 5 };
@@ -168,6 +173,7 @@ struct ResetArgs {
     int wave_per_env, wave_lds;  // drl_reset_wave_kernel (large grids) and its LDS bytes
     int fy_batch_min;            // wave kernel: shuffle 64 draws at a time while si >= this
     int fy_serial;               // ... i-range writers per chunk resolved by readlanes (more: table + jumps)
+    int fy_bwords;               // ... words of its j bitmap (lay::fy_bitmap_words)
     FastDiv div_side;
 };
 

@@ -1468,24 +1468,38 @@ __device__ __forceinline__ uint32_t xsel(const uint32_t (&x)[10], int c) {
     return v;
 }
 
-// Step 2 of a batched chunk: S = accepted lanes (m of them), r = their j.
-// Branch-light: every lane reads (rejected lanes read list[0] and OR a zero
-// bit), rejected lanes store into their own dummy slot (list index `dummy` +
-// lane) instead of running under an exec mask.
-__device__ __forceinline__ void fy_swaps(uint16_t* list, uint32_t* bmap, uint32_t* ptab, int dummy, uint64_t S, int m,
-                                         uint32_t r, int si0, int lane, uint64_t lanebit, int serial_chains) {
-    const bool acc = (S & lanebit) != 0ull;
-    const int t = mbcnt64(S);
+// Step 2 of a batched chunk: S = accepted lanes (m of them), acc = this
+// lane's bit of S, t = its rank, r = its j.  Branch-light: every lane reads
+// (rejected lanes read list[0] and OR a zero bit), rejected lanes store into
+// their own dummy slot (list index `dummy` + lane) instead of running under an
+// exec mask.
+struct FyLds {  // the batched shuffle's LDS: list (+ dummy slots at list index `dummy`), j bitmap, i-slot table
+    uint16_t* list;
+    uint32_t* bmap;
+    uint32_t* ptab;
+    int dummy;
+    int bmask, bshift;  // cell j -> bitmap word j & bmask, bit j >> bshift (>= 64 words: few lanes per word)
+    int serial_chains;
+};
+
+__device__ __forceinline__ void fy_swaps(const FyLds& f, uint64_t S, int m, bool acc, int t, uint32_t r, int si0,
+                                         int lane) {
+    uint16_t* const list = f.list;
+    uint32_t* const ptab = f.ptab;
     const int j = acc ? (int)r : 0;
     const int ii = si0 - t;    // >= 0 on every lane (t <= m <= si0)
     const int slot = si0 - j;  // j's rank if j lies in the i range; rejected lanes: si0 >= m, none
-    const uint32_t bit = acc ? 1u << (j & 31) : 0u;
-    const uint32_t a0 = list[ii];
-    const uint32_t l0j = list[j];
-    const uint32_t old = __hip_atomic_fetch_or(bmap + (j >> 5), bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    const uint32_t bit = acc ? 1u << (j >> f.bshift) : 0u;
+    uint32_t* const pw = f.bmap + (j & f.bmask);
+    uint16_t* const pi = list + ii;
+    uint16_t* const pj = list + j;
+    uint16_t* const pd = list + f.dummy + lane;
+    const uint32_t a0 = *pi;
+    const uint32_t l0j = *pj;
+    const uint32_t old = __hip_atomic_fetch_or(pw, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     uint64_t W = bal(slot < m);  // writers into the i range (self-swaps included: a no-op below)
     uint32_t A = a0;
-    if (popc(W) <= serial_chains) {
+    if (popc(W) <= f.serial_chains) {
         while (W) {  // ascending: the lane owning i = j takes this lane's A (rejected lanes' A is never stored)
             const int k = lobit(W);
             W &= W - 1;
@@ -1510,33 +1524,43 @@ __device__ __forceinline__ void fy_swaps(uint16_t* list, uint32_t* bmap, uint32_
     }
     uint64_t D = bal((old & bit) != 0u);
     uint32_t B = l0j;
-    uint64_t notlast = 0;
-    while (D) {  // one repeated-j group per pass; B of each member = A of the member below it
-        const int jk = __builtin_amdgcn_readlane(j, lobit(D));
-        uint64_t G = bal(j == jk) & S;
-        D &= ~G;
-        notlast |= G & ~(1ull << hibit(G));
-        int below = lobit(G);
-        G &= G - 1;
-        while (G) {
-            const int x = lobit(G);
-            G &= G - 1;
-            const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane((int)A, below);
-            if (lane == x) B = ab;
-            below = x;
-        }
+    bool jw = acc;  // this lane writes its j position (the last writer of each repeated j does)
+    if (D) {
+        uint64_t notlast = 0;
+        do {  // one repeated-j group per pass; B of each member = A of the member below it
+            const int jk = __builtin_amdgcn_readlane(j, lobit(D));
+            uint64_t G = bal(j == jk) & S;
+            D &= ~G;
+            const int lo = lobit(G), hi = hibit(G);
+            notlast |= G & ~(1ull << hi);
+            if (popc(G) == 2) {  // a pair (nearly always): one readlane
+                const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane((int)A, lo);
+                if (lane == hi) B = ab;
+            } else {
+                int below = lo;
+                G &= G - 1;
+                while (G) {
+                    const int x = lobit(G);
+                    G &= G - 1;
+                    const uint32_t ab = (uint32_t)__builtin_amdgcn_readlane((int)A, below);
+                    if (lane == x) B = ab;
+                    below = x;
+                }
+            }
+        } while (D);
+        jw = acc && !((notlast >> lane) & 1ull);
     }
     // j positions first (i-range ones are rewritten next), then the i positions
-    list[((S & ~notlast) & lanebit) ? j : dummy + lane] = (uint16_t)A;
-    list[acc ? ii : dummy + lane] = (uint16_t)B;
-    __hip_atomic_fetch_and(bmap + (j >> 5), ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    *(jw ? pj : pd) = (uint16_t)A;
+    *(acc ? pi : pd) = (uint16_t)B;
+    __hip_atomic_fetch_and(pw, ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     wave_sync();
 }
 
 // A chunk anywhere in a shuffle (its first draws, the shuffle's end, a
 // count-only chunk): returns the first lane NOT consumed.
-__device__ __forceinline__ int fy_chunk(uint16_t* list, uint32_t* bmap, uint32_t* ptab, int dummy, uint32_t u, int lane,
-                                        uint64_t lanebit, int l0, int l1, int& si, bool count_only, int serial_chains) {
+__device__ __forceinline__ int fy_chunk(const FyLds& f, uint32_t u, int lane, uint64_t lanebit, int l0, int l1, int& si,
+                                        bool count_only) {
     const int si0 = si;
     const bool valid = lane >= l0 && lane < l1;
     const int kb = bitlen((uint32_t)si0 + 1u);
@@ -1568,65 +1592,67 @@ __device__ __forceinline__ int fy_chunk(uint16_t* list, uint32_t* bmap, uint32_t
     const int m = popc(S);
     si = si0 - m;
     const int consumed = si == 0 ? hibit(S) + 1 : l1;
-    if (m != 0 && !count_only) fy_swaps(list, bmap, ptab, dummy, S, m, r, si0, lane, lanebit, serial_chains);
+    if (m != 0 && !count_only) fy_swaps(f, S, m, (S & lanebit) != 0ull, mbcnt64(S), r, si0, lane);
     return consumed;
 }
 
 // The reset's hot loop: whole chunks of one shuffle while every draw of a
 // chunk sees s >= 1 (the shuffle cannot end inside it), the register twist
-// inline, no phase bookkeeping.  The ten chunks of an MT block are unrolled, so
-// each reads its register x[c] by a static index.  Chunks that start below
-// swap_floor only count (the stations' shuffle needs its top positions only).
-// Leaves midx at the next unconsumed draw (MT_N: twist first) and tcur = the
-// tempered chunk holding midx.
-__device__ __forceinline__ void fy_run(uint16_t* list, uint32_t* bmap, uint32_t* ptab, int dummy, uint32_t (&x)[10],
-                                       uint32_t& tcur, int& midx, int& si, int swap_floor, int lane, uint64_t lanebit,
-                                       int serial_chains) {
+// inline, no phase bookkeeping.  Enters at a chunk boundary (midx % 64 == 0,
+// or MT_N: twist first); the chunk's register x[c] is read with a uniform
+// register index.  Chunks that start below swap_floor only count (the
+// stations' shuffle needs its top positions only).  Returns with midx at the
+// first chunk that could end the shuffle (the caller's general path takes it).
+__device__ __forceinline__ void fy_run(const FyLds& f, uint32_t (&x)[10], int& midx, int& si, int swap_floor, int lane) {
+    int c = midx >> 6;
+    if (midx >= MT_N) {
+        twist_regs(x, lane);
+        c = 0;
+    }
     for (;;) {
-        if (midx >= MT_N) {
-            twist_regs(x, lane);
-            midx = 0;
-        }
-#pragma unroll
-        for (int c = 0; c < 10; ++c) {
-            if ((midx >> 6) != c) continue;  // uniform: chunks before midx's are used up
-            const uint32_t u = temper(x[c]);
-            const int l0 = midx & 63, l1 = c == 9 ? MT_N - 576 : 64;
-            const int si0 = si;
-            if (si0 - (l1 - l0) < 1) {
-                tcur = u;
-                return;
-            }
-            const uint64_t V = (~0ull << l0) & (c == 9 ? (1ull << (MT_N - 576)) - 1ull : ~0ull);
-            const int kb = bitlen((uint32_t)si0 + 1u);
-            uint32_t r = u >> (32 - kb);
-            uint64_t S;
-            if (bitlen((uint32_t)(si0 - (l1 - 1 - l0)) + 1u) == kb) {  // one draw width over the chunk
-                const uint64_t H = bal((int)r <= si0) & V;
-                S = H;
-                if ((bal((int)r + lane <= si0 + l0) & V) != H) {
-                    for (;;) {
-                        const uint64_t S2 = bal((int)r + mbcnt64(S) <= si0) & V;
-                        if (S2 == S) break;
-                        S = S2;
-                    }
-                }
-            } else {  // the width drops inside the chunk (s >= 1 on every lane)
-                S = V;
+        const int cnt = c == 9 ? MT_N - 576 : 64;
+        const int si0 = si;
+        if (si0 - cnt < 1) break;
+        const bool live = lane < cnt;  // chunk 9 holds 48 words
+        const uint64_t L = bal(live);
+        const uint32_t u = temper(x[__builtin_amdgcn_readfirstlane(c)]);
+        const int sh = __builtin_clz((uint32_t)si0 + 1u);  // 32 - bitlen(si0 + 1)
+        uint32_t r = u >> sh;
+        uint64_t S;
+        int t;
+        bool acc;
+        if (__builtin_clz((uint32_t)(si0 - cnt + 2)) == sh) {  // one draw width over the chunk
+            S = bal((int)r <= si0) & L;  // #accepted before a lane lies in [0, lane]
+            if ((bal((int)r + lane <= si0) & L) != S) {
                 for (;;) {
-                    const int sk = si0 - mbcnt64(S);
-                    const uint64_t S2 = bal((int)(u >> (32 - bitlen((uint32_t)sk + 1u))) <= sk) & V;
+                    const uint64_t S2 = bal((int)r + mbcnt64(S) <= si0) & L;
                     if (S2 == S) break;
                     S = S2;
                 }
-                r = u >> (32 - bitlen((uint32_t)(si0 - mbcnt64(S)) + 1u));
             }
-            const int m = popc(S);
-            if (m != 0 && si0 >= swap_floor) fy_swaps(list, bmap, ptab, dummy, S, m, r, si0, lane, lanebit, serial_chains);
-            si = si0 - m;
-            midx = 64 * c + l1;
+            t = mbcnt64(S);
+            acc = live & ((int)r + t <= si0);
+        } else {  // the width drops inside the chunk (s >= 1 on every lane)
+            S = L;
+            for (;;) {
+                const int sk = si0 - mbcnt64(S);
+                const uint64_t S2 = bal((int)(u >> __builtin_clz((uint32_t)sk + 1u)) <= sk) & L;
+                if (S2 == S) break;
+                S = S2;
+            }
+            t = mbcnt64(S);
+            r = u >> __builtin_clz((uint32_t)(si0 - t) + 1u);
+            acc = live & ((int)r <= si0 - t);
+        }
+        const int m = popc(S);
+        if (si0 >= swap_floor) fy_swaps(f, S, m, acc, t, r, si0, lane);
+        si = si0 - m;
+        if (++c == 10) {
+            twist_regs(x, lane);
+            c = 0;
         }
     }
+    midx = 64 * c;
 }
 
 // One wavefront per env, for large grids (the lane-per-env kernel above is
@@ -1641,12 +1667,17 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
     const int lane = threadIdx.x;
     const int64_t env = blockIdx.x;
     if (env >= a.E || (a.mask != nullptr && a.mask[env] == 0)) return;  // whole wave, uniform
-    uint32_t* bmap = reinterpret_cast<uint32_t*>(smem);  // batched shuffle: one bit per cell (repeated j's)
-    const int bwords = (a.cells + 31) >> 5;
-    uint32_t* ptab = bmap + ((bwords + 3) & ~3);  // ... and the last writer per i slot (many chains)
-    uint16_t* list = reinterpret_cast<uint16_t*>(ptab + 64);
+    FyLds f;
+    f.bmap = reinterpret_cast<uint32_t*>(smem);  // batched shuffle: one bit per cell (repeated j's)
+    f.bmask = a.fy_bwords - 1;
+    f.bshift = __builtin_ctz((unsigned)a.fy_bwords);
+    f.ptab = f.bmap + a.fy_bwords;  // ... and the last writer per i slot (many chains)
+    f.list = reinterpret_cast<uint16_t*>(f.ptab + 64);
+    f.dummy = a.list_cap + 64;  // 64 u16 slots the batched shuffle's rejected lanes store into
+    f.serial_chains = a.fy_serial;
+    uint32_t* const bmap = f.bmap;
+    uint16_t* list = f.list;
     uint16_t* sel = list + a.list_cap;
-    const int dummy = a.list_cap + 64;  // 64 u16 slots the batched shuffle's rejected lanes store into
     uint16_t* pool = sel + 128;
     const uint64_t lanebit = 1ull << lane;
     const int GG = a.cells, N = a.n_drones;
@@ -1654,7 +1685,7 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
     const int par = mi_par(w0);  // the block holding the stream (a reseed writes block 0)
     uint32_t* mrow = a.mt + env * MT_WORDS + par * MT_ALT;
     uint8_t* grow = a.ground + env * a.gstride;
-    for (int i = lane; i < ((bwords + 3) & ~3) + 64; i += 64) bmap[i] = 0u;
+    for (int i = lane; i < a.fy_bwords + 64; i += 64) bmap[i] = 0u;
 
     // x[c] holds words 64c + lane (static indices only: fy_run unrolls the
     // chunks, the rest selects with xsel)
@@ -1732,17 +1763,17 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
         const int end = min(64 * c + 64, MT_N);
         // ---- consume the chunk's draws for the current phase (tight loops;
         // si / midx stay uniform; readlane returns int: shift it as uint32)
-        if (phase != 1 && si > 64 && a.fy_batch_min <= 1) {  // the hot loop, until the shuffle's last chunk
-            fy_run(list, bmap, ptab, dummy, x, tcur, midx, si, phase == 4 ? n - a.n_stat : 0, lane, lanebit,
-                   a.fy_serial);
+        if (phase != 1 && si > 64 && (midx & 63) == 0 && a.fy_batch_min <= 1) {
+            // the hot loop from a chunk boundary until the shuffle's last chunk
+            fy_run(f, x, midx, si, phase == 4 ? n - a.n_stat : 0, lane);
+            rot = -1;  // x may have twisted: re-select the chunk
             continue;
         } else if (phase != 1 && si >= a.fy_batch_min) {
             // the last shuffle only needs its top n_stat positions: below them
             // the draws are consumed without swapping
             const bool count_only = phase == 4 && si < n - a.n_stat;
             DRL_RS_BEGIN();
-            midx = 64 * c + fy_chunk(list, bmap, ptab, dummy, tcur, lane, lanebit, midx - 64 * c, end - 64 * c, si,
-                                     count_only, a.fy_serial);
+            midx = 64 * c + fy_chunk(f, tcur, lane, lanebit, midx - 64 * c, end - 64 * c, si, count_only);
             DRL_RS_END(count_only ? 2 : 0);
             DRL_RS_COUNT(count_only ? 8 : 6);
             if (si != 0) continue;  // the shuffle goes on: nothing to settle
