@@ -266,7 +266,7 @@ int drl_reset(const drl_params* p, const drl_state* s, int32_t reseed, uint64_t 
     a.lanes = lanes > 64 ? 64 : lanes;
     a.block_lds = a.lanes * a.lane_lds;
     // one wavefront per env (DRL_RESET_WAVE=0 selects the lane-per-env kernel, for A/B)
-    a.wave_lds = drl::lay::fy_table_bytes(GG) + (2 * a.list_cap + 256 + (a.pool_branch ? 2 * a.list_cap : 0) + 15) / 16 * 16;
+    a.wave_lds = (2 * a.list_cap + 256 + (a.pool_branch ? 2 * a.list_cap : 0) + 15) / 16 * 16;  // + the tables, below
     {
         const char* w = getenv("DRL_RESET_WAVE");
         a.wave_per_env = w ? atoi(w) : 1;
@@ -276,6 +276,7 @@ int drl_reset(const drl_params* p, const drl_state* s, int32_t reseed, uint64_t 
         const char* c = getenv("DRL_FY_SERIAL");
         a.fy_serial = c ? atoi(c) : kFySerial;
         a.fy_bwords = drl::lay::fy_bitmap_words(GG);
+        a.wave_lds += (a.fy_bwords + 64) * 4;
     }
     a.div_side = drl::make_fastdiv((uint32_t)p->side);
     hipError_t e = drl::launch_reset(a, stream);

@@ -94,7 +94,6 @@ constexpr int fy_bitmap_words(int cells) {
     while (w * 32 < cells) w *= 2;
     return w;
 }
-constexpr int fy_table_bytes(int cells) { return (fy_bitmap_words(cells) + 64) * 4; }
 }  // namespace lay
 
 enum : int { OBJ_EMPTY = 0, OBJ_SKYSCRAPER = 2, OBJ_STATION = 3, OBJ_DROPZONE = 4, OBJ_PACKET = 5 };

@@ -1455,24 +1455,6 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {  // set bits of m below thi
 //     The bitmap bits are cleared by an AND after the writes.
 __device__ __forceinline__ uint64_t bal(bool b) { return __builtin_amdgcn_ballot_w64(b); }
 
-// x[c] for a uniform c outside the hot loop: selects, so the register array
-// never needs a dynamic index (which sends it to scratch)
-__device__ __forceinline__ uint32_t xsel(const uint32_t (&x)[10], int c) {
-    uint32_t v = x[0];
-#pragma unroll
-    for (int k = 1; k < 10; ++k) {
-        uint32_t xk = x[k];
-        asm volatile("" : "+v"(xk));  // a select of values, not of addresses (see twist_regs)
-        v = c == k ? xk : v;
-    }
-    return v;
-}
-
-// Step 2 of a batched chunk: S = accepted lanes (m of them), acc = this
-// lane's bit of S, t = its rank, r = its j.  Branch-light: every lane reads
-// (rejected lanes read list[0] and OR a zero bit), rejected lanes store into
-// their own dummy slot (list index `dummy` + lane) instead of running under an
-// exec mask.
 struct FyLds {  // the batched shuffle's LDS: list (+ dummy slots at list index `dummy`), j bitmap, i-slot table
     uint16_t* list;
     uint32_t* bmap;
@@ -1687,8 +1669,8 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
     uint8_t* grow = a.ground + env * a.gstride;
     for (int i = lane; i < a.fy_bwords + 64; i += 64) bmap[i] = 0u;
 
-    // x[c] holds words 64c + lane (static indices only: fy_run unrolls the
-    // chunks, the rest selects with xsel)
+    // x[c] holds words 64c + lane; the current chunk's register is read with
+    // a uniform register index (s_set_gpr_idx), no data movement
     int midx = a.reseed ? MT_N : min(mi_idx(w0), MT_N);
     int rot = midx < MT_N ? midx >> 6 : 0;
     uint32_t x[10];
@@ -1700,7 +1682,7 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
     }
     for (int v = lane; v < a.gstride / 16; v += 64) reinterpret_cast<uint4*>(grow)[v] = make_uint4(0u, 0u, 0u, 0u);
     for (int i = lane; i < GG; i += 64) list[i] = (uint16_t)i;
-    uint32_t tcur = temper(xsel(x, rot));
+    uint32_t tcur = temper(x[__builtin_amdgcn_readfirstlane(rot)]);
     wave_sync();
 
     // The reset as a phase machine with ONE draw site (the register twist is
@@ -1756,7 +1738,7 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
             DRL_RS_COUNT(7);
         } else if ((midx >> 6) != rot) {  // next chunk
             rot = midx >> 6;
-            tcur = temper(xsel(x, rot));
+            tcur = temper(x[__builtin_amdgcn_readfirstlane(rot)]);
         }
         DRL_RS_END(1);
         const int c = rot;

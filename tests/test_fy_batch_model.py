@@ -148,3 +148,4 @@ def test_chunks_compose_to_random_shuffle(n):
             if si == 0 and used < 64:  # the first unconsumed draw is the shuffle's next word
                 assert a.getrandbits(32) == us[used]
         assert lst == want
+
