@@ -139,7 +139,7 @@ __device__ __forceinline__ void twist_regs(uint32_t (&x)[10], int lane) {
     // (the empty asm pins both sources in registers: folded into a select of
     // addresses, the array would be indexed per lane and live in scratch)
     auto pick = [&](bool lo, uint32_t a, uint32_t b) __attribute__((always_inline)) {
-        asm volatile("" : "+v"(a), "+v"(b));
+        asm("" : "+v"(a), "+v"(b));
         return lo ? a : b;
     };
     auto far_old = [&](int c) __attribute__((always_inline)) {
