@@ -277,6 +277,8 @@ int drl_reset(const drl_params* p, const drl_state* s, int32_t reseed, uint64_t 
         a.fy_serial = c ? atoi(c) : kFySerial;
         a.fy_bwords = drl::lay::fy_bitmap_words(GG);
         a.wave_lds += (a.fy_bwords + 64) * 4;
+        const char* pad = getenv("DRL_RESET_LDS_PAD");  // diagnostic: fewer waves per CU
+        if (pad) a.wave_lds += atoi(pad) / 16 * 16;
     }
     a.div_side = drl::make_fastdiv((uint32_t)p->side);
     hipError_t e = drl::launch_reset(a, stream);

@@ -5,7 +5,8 @@ python tools/reset_rate.py --configs c3,c4,c5 --variants lane,wave,wave_fy64,wav
 lane = drl_reset_kernel (lane per env); wave = drl_reset_wave_kernel with the
 batched shuffle (default: down to si = 1; wave_fyN: only while si >= N;
 wave_fy99999 = one draw at a time; wave_serN: at most N i-range writers per
-chunk by readlanes, more by the slot table).  Knobs are env variables read per
+chunk by readlanes, more by the slot table; wave_padN: N more LDS bytes per
+wave, a diagnostic of how the rate scales with waves per CU).  Knobs are env variables read per
 drl_reset call.  The streams are seeded once with the lane kernel (so a
 profiler filtered on drl_reset_wave sees only continuing resets); variants are
 timed in interleaved rounds after warm-up resets, and every variant's ground /
@@ -24,7 +25,7 @@ import torch  # noqa: E402
 from bench import CONFIGS  # noqa: E402
 from dronerl_amd import BatchedDeliveryDrones, EnvParams  # noqa: E402
 
-KNOBS = ("DRL_RESET_WAVE", "DRL_FY_BATCH_MIN", "DRL_FY_SERIAL")
+KNOBS = ("DRL_RESET_WAVE", "DRL_FY_BATCH_MIN", "DRL_FY_SERIAL", "DRL_RESET_LDS_PAD")
 
 
 def set_knobs(v):
@@ -38,6 +39,8 @@ def set_knobs(v):
             os.environ["DRL_FY_BATCH_MIN"] = v.split("_fy")[1].split("_")[0]
         if "_ser" in v:
             os.environ["DRL_FY_SERIAL"] = v.split("_ser")[1].split("_")[0]
+        if "_pad" in v:
+            os.environ["DRL_RESET_LDS_PAD"] = v.split("_pad")[1].split("_")[0]
 
 
 def snap(env):
