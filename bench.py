@@ -90,6 +90,14 @@ def min_over_ranks(v: float, world: int) -> float:
     return -max_over_ranks(-v, world)
 
 
+def under_profiler():
+    """True inside a rocprofv3 run: its preloaded tool has initialised the GPU
+    in this process, so a nested rocprofv3 child (which execs its target) must
+    not start; the committed profile is reported instead."""
+    pre = os.environ.get("LD_PRELOAD", "")
+    return "rocprof" in pre or any(k.startswith("ROCPROF") for k in os.environ)
+
+
 def measure_traffic(args):
     """HBM bytes per drl_step launch from rocprofv3 PMC passes of this same
     bench command (MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE in
@@ -104,7 +112,7 @@ def measure_traffic(args):
     import tempfile
     prof = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3")
                                          else None)
-    if prof is None:
+    if prof is None or under_profiler():
         return None
     child = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", "20", "--warmup", "3",
              "--no-cpu-baseline", "--no-reset-bench", "--no-dqn", "--rollout-chunk", "0", "--loop-segments", "0",

@@ -59,3 +59,19 @@ def test_cli_help_lists_contract_flags():
                          text=True, timeout=120, check=True).stdout
     for flag in ("--gpus", "--steps", "--warmup", "--config", "--cached-steps", "--no-pmc-traffic"):
         assert flag in out
+
+
+def test_no_nested_profiler_inside_a_rocprofv3_run(monkeypatch):
+    """Inside a rocprofv3 run the GPU is already initialised by its tool, so
+    bench.py must not start its own rocprofv3 children (they exec their
+    target): the in-run traffic passes are skipped."""
+    for k in [k for k in os.environ if k.startswith("ROCPROF")]:
+        monkeypatch.delenv(k)
+    monkeypatch.setenv("LD_PRELOAD", "")
+    assert not bench.under_profiler()
+    monkeypatch.setenv("ROCPROF_OUTPUT_PATH", "/tmp/x")
+    assert bench.under_profiler()
+    monkeypatch.delenv("ROCPROF_OUTPUT_PATH")
+    monkeypatch.setenv("LD_PRELOAD", "/opt/rocm/lib/librocprofiler-sdk-tool.so")
+    assert bench.under_profiler()
+    assert bench.measure_traffic(None) is None  # returns before reading any argument

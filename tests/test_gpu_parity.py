@@ -151,7 +151,9 @@ CONFIGS = {
 RESET_KERNELS = {
     "wave": {},                                                  # default: wave per env, batched shuffle
     "wave_serial": {"DRL_FY_BATCH_MIN": "1000000"},              # wave per env, one draw at a time
-    "wave_fy64": {"DRL_FY_BATCH_MIN": "64"},                     # batched only while si >= 64
+    "wave_fy64": {"DRL_FY_BATCH_MIN": "64"},                     # batched only while si >= 64 (no hot loop)
+    "wave_ser0": {"DRL_FY_SERIAL": "0"},                         # i-range writers: slot table + pointer jumps
+    "wave_ser64": {"DRL_FY_SERIAL": "64"},                       # i-range writers: readlane pass only
     "lane": {"DRL_RESET_WAVE": "0"},                             # lane per env
 }
 

@@ -2,7 +2,7 @@ set -u
 cd /root/repo
 export TMPDIR=/tmp
 OUT=gpurun_out/pmcq${TAG:-}; mkdir -p $OUT
-A="--config ${CFG:-c3} --steps 20 --warmup 2 --no-cpu-baseline --no-reset-bench ${EXTRA:-}"
+A="--config ${CFG:-c3} --steps 20 --warmup 2 --no-cpu-baseline --no-reset-bench --no-pmc-traffic ${EXTRA:-}"
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_INSTS_SMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA" ${EXTRA_PMC:-}; do
   i=$((i+1))
