@@ -1481,14 +1481,16 @@ __device__ __forceinline__ void fy_swaps(const FyLds& f, uint64_t S, int m, bool
     const uint32_t old = __hip_atomic_fetch_or(pw, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     uint64_t W = bal(slot < m);  // writers into the i range (self-swaps included: a no-op below)
     uint32_t A = a0;
-    if (popc(W) <= f.serial_chains) {
-        while (W) {  // ascending: the lane owning i = j takes this lane's A (rejected lanes' A is never stored)
+    if (W == 0) {
+        // no lane writes into the chunk's own i range (most chunks of a large list)
+    } else if (popc(W) <= f.serial_chains) {
+        do {  // ascending: the lane owning i = j takes this lane's A (rejected lanes' A is never stored)
             const int k = lobit(W);
             W &= W - 1;
             const int sk = __builtin_amdgcn_readlane(slot, k);
             const uint32_t ak = (uint32_t)__builtin_amdgcn_readlane((int)A, k);
             if (t == sk) A = ak;
-        }
+        } while (W);
     } else {  // many (small lists): last writer per i slot, then pointer jumping to the chain roots
         const bool w = slot < m && slot != t;
         if (w) __hip_atomic_fetch_max(ptab + slot, (uint32_t)lane + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -1591,40 +1593,29 @@ __device__ __forceinline__ void fy_run(const FyLds& f, uint32_t (&x)[10], int& m
         twist_regs(x, lane);
         c = 0;
     }
-    for (;;) {
-        const int cnt = c == 9 ? MT_N - 576 : 64;
+    int cnt = c == 9 ? MT_N - 576 : 64;
+    // Acceptance as one fixed-point loop for every chunk (the scalar unit is
+    // the reset's bottleneck, the vector units are not): start from "every
+    // draw below was accepted" (s_k = si0 - k, the smallest s each can see)
+    // and re-evaluate with the ranks that gives, until the set repeats.  With
+    // one draw width over the chunk and no draw in the narrow band, the start
+    // is already exact and the loop runs twice.
+    while (si - cnt >= 1) {
         const int si0 = si;
-        if (si0 - cnt < 1) break;
-        const bool live = lane < cnt;  // chunk 9 holds 48 words
-        const uint64_t L = bal(live);
         const uint32_t u = temper(x[__builtin_amdgcn_readfirstlane(c)]);
-        const int sh = __builtin_clz((uint32_t)si0 + 1u);  // 32 - bitlen(si0 + 1)
-        uint32_t r = u >> sh;
-        uint64_t S;
-        int t;
+        const bool live = lane < cnt;  // chunk 9 holds 48 words
+        int t = lane;         // = mbcnt(S) for the starting S: every lane
+        uint64_t S = ~0ull;
         bool acc;
-        if (__builtin_clz((uint32_t)(si0 - cnt + 2)) == sh) {  // one draw width over the chunk
-            S = bal((int)r <= si0) & L;  // #accepted before a lane lies in [0, lane]
-            if ((bal((int)r + lane <= si0) & L) != S) {
-                for (;;) {
-                    const uint64_t S2 = bal((int)r + mbcnt64(S) <= si0) & L;
-                    if (S2 == S) break;
-                    S = S2;
-                }
-            }
+        uint32_t r;
+        for (;;) {
+            const int sk = si0 - t;  // >= 1 on every live lane
+            r = u >> __builtin_clz((uint32_t)sk + 1u);
+            acc = live & ((int)r <= sk);
+            const uint64_t S2 = bal(acc);
+            if (S2 == S) break;
+            S = S2;
             t = mbcnt64(S);
-            acc = live & ((int)r + t <= si0);
-        } else {  // the width drops inside the chunk (s >= 1 on every lane)
-            S = L;
-            for (;;) {
-                const int sk = si0 - mbcnt64(S);
-                const uint64_t S2 = bal((int)(u >> __builtin_clz((uint32_t)sk + 1u)) <= sk) & L;
-                if (S2 == S) break;
-                S = S2;
-            }
-            t = mbcnt64(S);
-            r = u >> __builtin_clz((uint32_t)(si0 - t) + 1u);
-            acc = live & ((int)r <= si0 - t);
         }
         const int m = popc(S);
         if (si0 >= swap_floor) fy_swaps(f, S, m, acc, t, r, si0, lane);
@@ -1633,6 +1624,7 @@ __device__ __forceinline__ void fy_run(const FyLds& f, uint32_t (&x)[10], int& m
             twist_regs(x, lane);
             c = 0;
         }
+        cnt = c == 9 ? MT_N - 576 : 64;
     }
     midx = 64 * c;
 }
