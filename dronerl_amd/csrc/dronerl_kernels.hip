@@ -1604,19 +1604,20 @@ __device__ __forceinline__ void fy_run(const FyLds& f, uint32_t (&x)[10], int& m
         const int si0 = si;
         const uint32_t u = temper(x[__builtin_amdgcn_readfirstlane(c)]);
         const bool live = lane < cnt;  // chunk 9 holds 48 words
-        int t = lane;         // = mbcnt(S) for the starting S: every lane
-        uint64_t S = ~0ull;
-        bool acc;
-        uint32_t r;
-        for (;;) {
-            const int sk = si0 - t;  // >= 1 on every live lane
-            r = u >> __builtin_clz((uint32_t)sk + 1u);
-            acc = live & ((int)r <= sk);
-            const uint64_t S2 = bal(acc);
-            if (S2 == S) break;
-            S = S2;
+        const uint64_t L = bal(live);
+        auto accept = [&](int tk) __attribute__((always_inline)) {  // tk: accepted draws below this lane
+            const int sk = si0 - tk;  // >= 1 on every live lane
+            return bal((int)(u >> __builtin_clz((uint32_t)sk + 1u)) <= sk) & L;
+        };
+        int t = lane;  // the start: every draw below accepted (= mbcnt of all lanes)
+        uint64_t S = accept(t), Sp = ~0ull;
+        while (S != Sp) {
+            Sp = S;
             t = mbcnt64(S);
+            S = accept(t);
         }
+        const uint32_t r = u >> __builtin_clz((uint32_t)(si0 - t) + 1u);
+        const bool acc = live & ((int)r <= si0 - t);
         const int m = popc(S);
         if (si0 >= swap_floor) fy_swaps(f, S, m, acc, t, r, si0, lane);
         si = si0 - m;
