@@ -191,8 +191,11 @@ struct QnetLayout {
     int n_bias;                   // floats of biases
     int lds_vec;                  // uint4s of the LDS image (fragments + biases)
     int precision;                // DRL_QNET_BF16 / DRL_QNET_F32
-    int frag_lo_off[QN_MAX_LAYERS];  // F32: uint4 offset of the layer's lo fragments (after the LDS image)
+    int frag_lo_off[QN_MAX_LAYERS];  // F32: uint4 offset of the layer's lo fragments
     int total_vec;                // uint4s of the whole packed net
+    int frag_src[QN_MAX_LAYERS];  // the pack kernel's contiguous element numbering of the hi fragments
+    int bias_vec;                 // uint4 offset of the biases
+    int lo0_lds;                  // F32: layer 0's hi and lo fragments are the LDS image (the rest is global)
 };
 
 struct QnetPack {
@@ -206,6 +209,7 @@ struct QnetPack {
     float* packed_b;
     int precision;
     int frag_lo_off[QN_MAX_LAYERS];  // F32: lo fragments, uint4 offsets from packed_w
+    int frag_src[QN_MAX_LAYERS];     // contiguous numbering of the hi elements (uint4 units) -> frag_off
 };
 
 struct QnetArgs {
@@ -213,7 +217,8 @@ struct QnetArgs {
     int nt[QN_MAX_LAYERS];
     int frag_off[QN_MAX_LAYERS], bias_off[QN_MAX_LAYERS];
     int frag_total, lds_vec, n_bias;
-    int frag_lo_off[QN_MAX_LAYERS];  // F32: lo fragments in global memory (uint4 offsets from packed)
+    int frag_lo_off[QN_MAX_LAYERS];  // F32: lo fragments (uint4 offsets from packed, or in LDS: lo0_lds)
+    int bias_vec, lo0_lds;           // biases' uint4 offset; F32 layout with layer 0 alone in LDS
     const uint4* packed;
     const float* obs;
     int64_t obs_stride, E;

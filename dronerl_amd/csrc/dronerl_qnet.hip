@@ -50,8 +50,8 @@ __global__ void drl_qnet_pack_kernel(QnetPack p) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < p.n_wfrag_elems) {
         int l = 0;
-        while (l + 1 < p.n_layers && i >= (int64_t)p.frag_off[l + 1] * 8) ++l;
-        const int64_t e = i - (int64_t)p.frag_off[l] * 8;  // element within the layer
+        while (l + 1 < p.n_layers && i >= (int64_t)p.frag_src[l + 1] * 8) ++l;
+        const int64_t e = i - (int64_t)p.frag_src[l] * 8;  // element within the layer
         const int j = (int)(e & 7), lane = (int)((e >> 3) & 63);
         const int64_t frag = e >> 9;                       // m * kt + t
         const int kt = p.kt[l];
@@ -62,11 +62,11 @@ __global__ void drl_qnet_pack_kernel(QnetPack p) {
         const float w = (row < p.out[l] && k < p.in[l]) ? p.w[l][(int64_t)row * p.in[l] + k] : 0.0f;
         if (p.precision == DRL_QNET_F32) {  // hi = fp16(w), lo = fp16((w - hi) * 2^11), lo after the LDS image
             const _Float16 hi = (_Float16)w;
-            reinterpret_cast<_Float16*>(p.packed_w)[i] = hi;
+            reinterpret_cast<_Float16*>(p.packed_w)[(int64_t)p.frag_off[l] * 8 + e] = hi;
             reinterpret_cast<_Float16*>(p.packed_w)[(int64_t)p.frag_lo_off[l] * 8 + e] =
                 (_Float16)((w - (float)hi) * 2048.0f);
         } else {
-            reinterpret_cast<__bf16*>(p.packed_w)[i] = (__bf16)w;
+            reinterpret_cast<__bf16*>(p.packed_w)[(int64_t)p.frag_off[l] * 8 + e] = (__bf16)w;
         }
     } else if (i < p.n_wfrag_elems + p.n_bias) {
         const int64_t bi = i - p.n_wfrag_elems;
@@ -323,7 +323,12 @@ __device__ __forceinline__ void split_f16(const float (&v)[8], f16x8& hi, f16x8&
 
 #define MFMA_F16 __builtin_amdgcn_mfma_f32_16x16x32_f16
 
-template <int NT0, int TP>
+// LO0 (the layout whenever layer 0's two fragment sets fit, as at 294->128):
+// layer 0's hi and lo fragments are the LDS image and the later layers'
+// fragments and the biases are read from global memory (L2) instead, which
+// moves a tile's L2 weight reads from 80 KB (layer 0's lo set) to the later
+// layers' few KB.
+template <int NT0, int TP, bool LO0>
 __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_f32_kernel(QnetArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint4 wl[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -364,7 +369,7 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_f32_kernel(QnetArg
     for (int h = 0; h < TP; ++h) row[h] = row_of(TP * (grp < ngroups ? grp : 0) + h);
     // layer-0 lo fragments (global, L2-resident): buffer loads with the lane's
     // 16-B offset in one VGPR and the fragment offset in an SGPR
-    const auto glo0 = __builtin_amdgcn_make_buffer_rsrc((void*)(a.packed + a.frag_lo_off[0]), 0,
+    const auto glo0 = __builtin_amdgcn_make_buffer_rsrc((void*)(a.packed + (LO0 ? 0 : a.frag_lo_off[0])), 0,
                                                          nt0 * KP * 1024, 0x00020000);
 #pragma unroll
     for (int i = 0; i < QN_RING; ++i)
@@ -376,8 +381,11 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_f32_kernel(QnetArg
                                              (__attribute__((address_space(3))) void*)(wl + v0), 16, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const float* bias = reinterpret_cast<const float*>(wl + a.frag_total);
+    const float* bias = LO0 ? reinterpret_cast<const float*>(a.packed + a.bias_vec)
+                            : reinterpret_cast<const float*>(wl + a.frag_total);
     const uint4* W0 = wl + a.frag_off[0];
+    const uint4* W0lo = wl + (LO0 ? a.frag_lo_off[0] : 0);
+    const uint4* Wsrc = LO0 ? a.packed : wl;  // the later layers' fragments
 
     for (; grp < ngroups; grp += gstride) {
         const int64_t ngrp = grp + gstride;
@@ -395,10 +403,12 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_f32_kernel(QnetArg
             for (int i = 0; i < QN_RING; ++i) {
                 const int t = rd * QN_RING + i;
                 uint4 wlo[NT0];  // the slice's lo fragments (L2), used after the hi products
+                if constexpr (!LO0) {
 #pragma unroll
-                for (int m = 0; m < nt0; ++m) {
-                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(glo0, lane * 16, (m * KP + t) * 1024, 0);
-                    __builtin_memcpy(&wlo[m], &v, 16);
+                    for (int m = 0; m < nt0; ++m) {
+                        const auto v = __builtin_amdgcn_raw_buffer_load_b128(glo0, lane * 16, (m * KP + t) * 1024, 0);
+                        __builtin_memcpy(&wlo[m], &v, 16);
+                    }
                 }
                 f16x8 bh[TP], bl[TP];
 #pragma unroll
@@ -418,7 +428,7 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_f32_kernel(QnetArg
                 }
 #pragma unroll
                 for (int m = 0; m < nt0; ++m) {
-                    const f16x8 wo = as_f16x8(wlo[m]);
+                    const f16x8 wo = as_f16x8(LO0 ? W0lo[(m * KP + t) * 64 + lane] : wlo[m]);
 #pragma unroll
                     for (int h = 0; h < TP; ++h) acl[h][m] = MFMA_F16(wo, bh[h], acl[h][m], 0, 0, 0);
                 }
@@ -455,8 +465,8 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_f32_kernel(QnetArg
             for (int h = 0; h < TP; ++h)
 #pragma unroll
                 for (int m = 0; m < QN_MAXT; ++m) acc[h][m] = acl[h][m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-            const uint4* Wl = wl + a.frag_off[l];
-            const uint4* Wlo = wl + a.frag_lo_off[l];
+            const uint4* Wl = Wsrc + a.frag_off[l];
+            const uint4* Wlo = Wsrc + a.frag_lo_off[l];
 #pragma unroll
             for (int t = 0; t < QN_MAXT / 2; ++t) {
                 if (t < kt) {
@@ -581,13 +591,17 @@ hipError_t launch_qnet_act(const QnetArgs& a, int num_cus, hipStream_t s) {
         if (nb > num_cus) nb = num_cus;
         const dim3 grid((unsigned)nb), block(64 * QN_WAVES);
         const size_t lds = (size_t)a.lds_vec * 16;
+#define QN_F32_LAUNCH(NT)                                                                     \
+    if (a.lo0_lds) hipLaunchKernelGGL((drl_qnet_act_f32_kernel<NT, TP, true>), grid, block, lds, s, a); \
+    else hipLaunchKernelGGL((drl_qnet_act_f32_kernel<NT, TP, false>), grid, block, lds, s, a)
         switch (a.nt[0]) {
-            case 2: hipLaunchKernelGGL((drl_qnet_act_f32_kernel<2, TP>), grid, block, lds, s, a); break;
-            case 4: hipLaunchKernelGGL((drl_qnet_act_f32_kernel<4, TP>), grid, block, lds, s, a); break;
-            case 6: hipLaunchKernelGGL((drl_qnet_act_f32_kernel<6, TP>), grid, block, lds, s, a); break;
-            case 8: hipLaunchKernelGGL((drl_qnet_act_f32_kernel<8, TP>), grid, block, lds, s, a); break;
+            case 2: QN_F32_LAUNCH(2); break;
+            case 4: QN_F32_LAUNCH(4); break;
+            case 6: QN_F32_LAUNCH(6); break;
+            case 8: QN_F32_LAUNCH(8); break;
             default: return hipErrorInvalidValue;
         }
+#undef QN_F32_LAUNCH
         return hipGetLastError();
     }
     const int64_t ngroups = ((a.E + 15) / 16 + QN_TILES - 1) / QN_TILES;

@@ -43,22 +43,49 @@ int qnet_layout(const drl_qnet_desc* d, drl::QnetLayout* L) {
         constexpr int R = drl::lay::qn_ring;
         L->kt[l] = l == 0 ? ((d->in_features + 31) / 32 + R - 1) / R * R : L->in[l] / 32;
         L->frag_off[l] = frag * 64;
+        L->frag_src[l] = frag * 64;
         L->bias_off[l] = bias;
         frag += L->nt[l] * L->kt[l];
         bias += 16 * L->nt[l];
     }
     L->frag_total = frag * 64;
     L->n_bias = bias;
+    L->bias_vec = L->frag_total;
     L->lds_vec = L->frag_total + (bias + 3) / 4;
     if (d->precision == DRL_QNET_F32) {
-        // lo fragments: the hidden and output layers' after the biases (LDS
-        // image), layer 0's after the image (read from global memory / L2)
-        for (int l = 1; l < L->n_layers; ++l) {
-            L->frag_lo_off[l] = L->lds_vec;
-            L->lds_vec += L->nt[l] * L->kt[l] * 64;
+        const int f0 = L->nt[0] * L->kt[0] * 64;
+#ifndef DRL_QNET_LO0_LDS
+#define DRL_QNET_LO0_LDS 1
+#endif
+        if (DRL_QNET_LO0_LDS && 2 * f0 * 16 <= kQnetLdsMax) {
+            // layer 0's hi and lo fragments are the LDS image (160 KB at
+            // 294->128); the later layers' fragments and the biases follow in
+            // global memory (L2-resident, a few KB per 16-env tile)
+            L->lo0_lds = 1;
+            L->frag_lo_off[0] = f0;
+            int pos = 2 * f0;
+            L->lds_vec = pos;
+            for (int l = 1; l < L->n_layers; ++l) {
+                L->frag_off[l] = pos;
+                pos += L->nt[l] * L->kt[l] * 64;
+            }
+            L->bias_vec = pos;
+            pos += (bias + 3) / 4;
+            for (int l = 1; l < L->n_layers; ++l) {
+                L->frag_lo_off[l] = pos;
+                pos += L->nt[l] * L->kt[l] * 64;
+            }
+            L->total_vec = pos;
+        } else {
+            // lo fragments: the hidden and output layers' after the biases (LDS
+            // image), layer 0's after the image (read from global memory / L2)
+            for (int l = 1; l < L->n_layers; ++l) {
+                L->frag_lo_off[l] = L->lds_vec;
+                L->lds_vec += L->nt[l] * L->kt[l] * 64;
+            }
+            L->frag_lo_off[0] = L->lds_vec;
+            L->total_vec = L->lds_vec + f0;
         }
-        L->frag_lo_off[0] = L->lds_vec;
-        L->total_vec = L->lds_vec + L->nt[0] * L->kt[0] * 64;
     } else {
         L->total_vec = L->lds_vec;
     }
@@ -110,6 +137,7 @@ int drl_qnet_pack(const drl_qnet_desc* d, const float* const* d_weights, const f
     for (int l = 0; l < L.n_layers; ++l) {
         if (!d_weights[l] || !d_biases[l]) return fail("a weight or bias pointer is NULL");
         p.frag_off[l] = L.frag_off[l];
+        p.frag_src[l] = L.frag_src[l];
         p.kt[l] = L.kt[l];
         p.in[l] = L.in[l];
         p.out[l] = L.out[l];
@@ -122,7 +150,7 @@ int drl_qnet_pack(const drl_qnet_desc* d, const float* const* d_weights, const f
     p.n_wfrag_elems = (int64_t)L.frag_total * 8;
     p.n_bias = L.n_bias;
     p.packed_w = static_cast<uint16_t*>(d_packed);
-    p.packed_b = reinterpret_cast<float*>(static_cast<uint8_t*>(d_packed) + (size_t)L.frag_total * 16);
+    p.packed_b = reinterpret_cast<float*>(static_cast<uint8_t*>(d_packed) + (size_t)L.bias_vec * 16);
     hipError_t e = drl::launch_qnet_pack(p, stream);
     return e == hipSuccess ? 0 : hip_fail(e, "drl_qnet_pack launch");
 }
@@ -155,6 +183,8 @@ static int qnet_act_impl(const drl_qnet_desc* d, const void* d_packed, const flo
     }
     a.precision = L.precision;
     a.frag_total = L.frag_total;
+    a.bias_vec = L.bias_vec;
+    a.lo0_lds = L.lo0_lds;
     a.lds_vec = L.lds_vec;
     a.n_bias = L.n_bias;
     a.packed = static_cast<const uint4*>(d_packed);

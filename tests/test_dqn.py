@@ -55,8 +55,13 @@ def test_qnet_packed_size_formula():
     assert nb.value == 2 * frags * 1024 + biases
     assert L.drl_qnet_packed_bytes(ctypes.byref(_desc(294, (128, 64), precision=2)), ctypes.byref(nb)) != 0
     assert b"precision" in L.drl_last_error()
-    # hi + lo fragments of three 128-wide hidden layers exceed the LDS in f32 mode
-    assert L.drl_qnet_packed_bytes(ctypes.byref(_desc(294, (128, 128, 128), precision=1)), ctypes.byref(nb)) != 0
+    # f32 with layer 0's hi + lo fragments alone in LDS (160 KB at 294 -> 128), the later layers in global
+    # memory: three 128-wide hidden layers pack (same total bytes, another order)
+    assert L.drl_qnet_packed_bytes(ctypes.byref(_desc(294, (128, 128, 128), precision=1)), ctypes.byref(nb)) == 0
+    frags3 = 8 * 10 + 8 * 4 + 8 * 4 + 1 * 4
+    assert nb.value == 2 * frags3 * 1024 + (128 * 3 + 16) * 4
+    # 486 inputs (radius 4) at 128 units: neither layout fits the LDS
+    assert L.drl_qnet_packed_bytes(ctypes.byref(_desc(486, (128, 128), precision=1)), ctypes.byref(nb)) != 0
 
 
 def _hash_explore(seed, step, genv, n_actions, eps):
@@ -116,12 +121,17 @@ def test_qnet_greedy_matches_torch_reference(hidden, E):
 Q_TOL_EXACT = 1e-5
 
 
+# Layouts: layer 0's hi + lo fragments fit the LDS (every 294-input net here,
+# and 486 inputs at 64 units) -> layer 0 alone in LDS, the rest from L2; at 486
+# inputs with 96 units they do not -> layer 0's lo fragments from L2.
 @gpu
-@pytest.mark.parametrize("hidden,E", [((128, 64), 65536), ((128, 64), 1000), ((32, 32), 4096), ((64,), 31),
-                                      ((96, 32), 4096), ((128, 128), 333), ((64, 64, 32), 4096)])
-def test_qnet_f32_matches_fp32_forward(hidden, E):
+@pytest.mark.parametrize("hidden,E,radius", [((128, 64), 65536, 3), ((128, 64), 1000, 3), ((32, 32), 4096, 3),
+                                             ((64,), 31, 3), ((96, 32), 4096, 3), ((128, 128), 333, 3),
+                                             ((64, 64, 32), 4096, 3), ((128, 128, 128), 2048, 3), ((96, 32), 2048, 4),
+                                             ((64, 32), 777, 4)])
+def test_qnet_f32_matches_fp32_forward(hidden, E, radius):
     from dronerl_amd.dqn import QNetwork
-    obs, _ = _obs_batch(E)
+    obs, _ = _obs_batch(E, radius=radius)
     g = torch.Generator().manual_seed(len(hidden) * 1000 + E)
     net = QNetwork(obs.shape[1], hidden, generator=g, precision="f32")
     for b in net.biases:
