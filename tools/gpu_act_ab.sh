@@ -1,6 +1,7 @@
 #!/bin/bash
 # GPU: DQN tests on the product library, then act timing A/B: the product
-# build against VARLIB (a tools/variants.py build), per precision, two rounds.
+# build against each of VARLIB (tools/variants.py builds, space-separated),
+# per precision, two rounds.
 set -u
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
@@ -12,8 +13,10 @@ for r in 1 2; do
   for p in ${PRECISIONS:-f32}; do
     echo "== round $r precision $p product" >> gpurun_out/time_act.log
     timeout -k 10 120 python tools/time_act.py --precision $p >> gpurun_out/time_act.log 2>&1 || exit $?
-    echo "== round $r precision $p $VARLIB" >> gpurun_out/time_act.log
-    timeout -k 10 120 python tools/time_act.py --precision $p --lib $VARLIB >> gpurun_out/time_act.log 2>&1 || exit $?
+    for v in $VARLIB; do
+      echo "== round $r precision $p $v" >> gpurun_out/time_act.log
+      timeout -k 10 120 python tools/time_act.py --precision $p --lib $v >> gpurun_out/time_act.log 2>&1 || exit $?
+    done
   done
 done
 cat gpurun_out/time_act.log
