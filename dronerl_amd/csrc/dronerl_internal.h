@@ -56,11 +56,17 @@ constexpr int step_draws(int P) {
 // narrower groups roll out as drl_step launches (the 64-VGPR cap of their
 // 8-waves-per-SIMD occupancy leaves no room for the rollout's carried state)
 constexpr int kRolloutMinLanes = 16;
-// DRL_ROLL_RING=0 builds a drl_rollout that discards the rings' entries and
-// draws every respawn from the stream (the round-1 rollout's registers: one
-// more wave per SIMD at C5); not yet measured against the default
+// drl_rollout takes the rings' entries at group widths P <= DRL_ROLL_RING_MAXP
+// and discards them at wider groups, drawing every respawn from the stream
+// (the round-1 rollout's registers: one more wave per SIMD at C5).  Measured
+// (profiles/r02_rollout_ring_ab/): C4 (P = 16) 27.95 vs 29.2 us/step with
+// the entries, C5 (P = 32) 119.0 vs 134.2 without.  DRL_ROLL_RING=0 discards
+// them at every width.
 #ifndef DRL_ROLL_RING
 #define DRL_ROLL_RING 1
+#endif
+#ifndef DRL_ROLL_RING_MAXP
+#define DRL_ROLL_RING_MAXP 16
 #endif
 constexpr int OBS_U = 1;        // observation cells per lane per pass (stage: OBS_U*1536 B per wave)
 

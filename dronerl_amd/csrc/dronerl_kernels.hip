@@ -613,12 +613,12 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     int midx = 0;
     l_u32* const stash = W.stash;  // ROLL: records between steps ([GPW][P], O order)
     // drl_rollout takes the rings' entries while they last, then draws from
-    // the stream.  DRL_ROLL_RING=0 discards the entries instead (they are a
-    // cache of the same draws; the refill at the end rebuilds them), which
-    // frees the ring code's registers: C5's rollout runs 3 waves per SIMD with
-    // it (126 -> 138 VGPRs) and measured 134-136 us/step against 119.5 for
-    // round 1's ring-less rollout.
-    constexpr bool kRing = !ROLL || DRL_ROLL_RING;
+    // the stream, at P <= DRL_ROLL_RING_MAXP (16).  Wider groups discard the
+    // entries instead (they are a cache of the same draws; the refill at the
+    // end rebuilds them), which frees the ring code's registers: C5's rollout
+    // runs 3 waves per SIMD with it (126 -> 138 VGPRs) and measured 134 us/step
+    // against 119 without; C4's gains from the entries (27.95 vs 29.2).
+    constexpr bool kRing = !ROLL || (DRL_ROLL_RING && P <= DRL_ROLL_RING_MAXP);
     uint32_t cq[QL];  // the step's ring entries
     auto ring_issue = [&](const uint32_t mw) __attribute__((always_inline)) {
         const uint32_t rbase = (uint32_t)(env_ok0 ? grp0 : 0) * MT_WORDS + MT_RING;
