@@ -87,13 +87,16 @@ int step_group_lanes(int n_drones, int gstride, int cells, int window) {
 // Steps between refills.  Ring entries used per env-step, measured at the
 // benchmark shapes with random actions (tools/ring_usage.py): mean 2.06 /
 // 2.56 / 3.44 and at most 17 at N = 8 / 16 / 32; over 16 steps at most 71 /
-// 71 / 93.  CAND_Q / (N/4 + 3) steps keep the worst env well inside the
-// ring: 25 at C3, 18 at C4, 11 at C5 (an env whose ring runs dry draws from
-// the stream in the step: slower, same results).  DRL_REFILL_EVERY overrides
+// 71 / 93, i.e. about 1.53 + 0.06 N.  A refill every CAND_Q / (1.53 + 0.06 N)
+// steps (at most 32) fills the ring about as fast as the mean env drains it:
+// 32 at C3, C4 and C5.  The worst envs then run dry and draw from the stream
+// in the step (slower, same results), but fewer, fuller refills win overall
+// (profiles/r02_refill_cadence/: C3 22.1-22.2 -> 21.7-22.0 us/step from 25
+// to 32, C5 154.8-155.3 -> 151.5 from 11 to 32).  DRL_REFILL_EVERY overrides
 // it (A/B runs).
 int refill_cadence(int n_drones) {
     if (const char* v = getenv("DRL_REFILL_EVERY")) return atoi(v) > 0 ? atoi(v) : 1;
-    const int r = (int)(DRL_CAND_SLOTS / (0.25 * n_drones + 3.0));
+    const int r = (int)(DRL_CAND_SLOTS / (1.53 + 0.06 * n_drones));
     return r < 1 ? 1 : (r > 32 ? 32 : r);
 }
 
@@ -371,7 +374,7 @@ int drl_rollout(const drl_params* p, const drl_state* s, int32_t num_steps, cons
     a.act_tstride = act_step_stride;
     a.out_tstride = out_step_stride;
     a.obs_tstride = d_obs ? obs_step_stride : 0;
-    if (L.step_group_lanes < drl::kRolloutMinLanes) {
+    if (L.step_group_lanes < (d_obs ? drl::kRolloutMinLanes : drl::kRolloutNoObsMinLanes)) {
         // narrow groups (the 64-VGPR kernels): one drl_step launch per step,
         // streaming observation stores, a refill every refill_every steps
         a.obs_nt = 1;

@@ -52,10 +52,15 @@ constexpr int step_cq(int P) { return P <= 16 ? 2 : 1; }
 constexpr int step_draws(int P) {
     return P == 8 ? DRL_DRAWS_P8 : P == 16 ? DRL_DRAWS_P16 : P == 32 ? DRL_DRAWS_P32 : 1;
 }
-// drl_rollout (several steps per launch, state on chip) runs at P >= 16;
-// narrower groups roll out as drl_step launches (the 64-VGPR cap of their
-// 8-waves-per-SIMD occupancy leaves no room for the rollout's carried state)
+// drl_rollout (several steps per launch, state on chip) runs at P >= 16, and
+// at P = 8 without observations; otherwise narrower groups roll out as
+// drl_step launches.  At C3 (P = 8) the on-chip kernel (85-100 VGPRs, 4-5
+// waves per SIMD instead of the step kernel's 8) measured 12.1-12.2 us/step
+// without obs against 13.7-13.8 for step launches, and 26.2 against 22.7-22.8
+// with obs, whose stores want the step kernel's occupancy
+// (profiles/r02_rollout_p8/).
 constexpr int kRolloutMinLanes = 16;
+constexpr int kRolloutNoObsMinLanes = 8;
 // drl_rollout takes the rings' entries at group widths P <= DRL_ROLL_RING_MAXP
 // and discards them at wider groups, drawing every respawn from the stream
 // (the round-1 rollout's registers: one more wave per SIMD at C5).  Measured

@@ -558,7 +558,7 @@ template <int P, class GEO, bool ROLL, bool NT>
 __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     using GMask = typename GMaskT<P>::type;
     constexpr int GPW = 64 / P;
-    static_assert(!ROLL || P >= kRolloutMinLanes, "narrow groups roll out as drl_step launches");
+    static_assert(!ROLL || P >= kRolloutNoObsMinLanes, "narrow groups roll out as drl_step launches");
     constexpr int D = step_draws(P);             // draws per lane per dry-ring respawn round
     constexpr int QL = step_cq(P);               // ring entries per lane per batch
     using CM = typename GMaskT<(P * D <= 32 ? 32 : 64)>::type;  // round-position masks
@@ -613,12 +613,12 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     int midx = 0;
     l_u32* const stash = W.stash;  // ROLL: records between steps ([GPW][P], O order)
     // drl_rollout takes the rings' entries while they last, then draws from
-    // the stream, at P <= DRL_ROLL_RING_MAXP (16).  Wider groups discard the
+    // the stream, at 16 <= P <= DRL_ROLL_RING_MAXP (16).  Other groups discard the
     // entries instead (they are a cache of the same draws; the refill at the
     // end rebuilds them), which frees the ring code's registers: C5's rollout
     // runs 3 waves per SIMD with it (126 -> 138 VGPRs) and measured 134 us/step
     // against 119 without; C4's gains from the entries (27.95 vs 29.2).
-    constexpr bool kRing = !ROLL || (DRL_ROLL_RING && P <= DRL_ROLL_RING_MAXP);
+    constexpr bool kRing = !ROLL || (DRL_ROLL_RING && P >= kRolloutMinLanes && P <= DRL_ROLL_RING_MAXP);
     uint32_t cq[QL];  // the step's ring entries
     auto ring_issue = [&](const uint32_t mw) __attribute__((always_inline)) {
         const uint32_t rbase = (uint32_t)(env_ok0 ? grp0 : 0) * MT_WORDS + MT_RING;
@@ -2179,7 +2179,7 @@ static hipError_t launch_step_t(const StepArgs& a, hipStream_t s, int mode) {
         if constexpr (GEO::kObs) hipLaunchKernelGGL((drl_obs_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
         else return hipErrorInvalidValue;
     } else if (mode == kRolloutMode) {
-        if constexpr (P >= kRolloutMinLanes) hipLaunchKernelGGL((drl_rollout_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
+        if constexpr (P >= kRolloutNoObsMinLanes) hipLaunchKernelGGL((drl_rollout_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
         else return hipErrorInvalidValue;
     } else if (GEO::kObs && a.obs && a.obs_nt) {
         hipLaunchKernelGGL((drl_step_kernel<P, GEO, GEO::kObs>), grid, block, a.wave_lds, s, a);

@@ -58,7 +58,7 @@ def test_layout_and_validation():
     assert (L.cells, L.ground_stride, L.drone_stride, L.mt_stride, L.obs_window, L.obs_floats) == \
         (256, 256, 8, 1408, 7, 294)
     assert L.step_group_lanes == 8
-    assert (L.cand_slots, L.refill_every) == (128, 25)
+    assert (L.cand_slots, L.refill_every) == (128, 32)
     L = EnvParams(n_drones=32, grid_size=64).layout()
     assert L.step_group_lanes in (32, 64) and L.step_lds_bytes <= 160 * 1024
     L = EnvParams(n_drones=1, grid_size=5).layout()
