@@ -624,6 +624,10 @@ def test_grid_obs_vs_oracle_state_and_compat_gridview():
     ("pool_5x5_n2", 100, 80, 1),
     ("dense_10x10_n8", 200, 60, 1),
     ("c2_16x16_n8|rt", 333, 30, 1),
+    # P = 8 without observations: the on-chip kernel (ring entries discarded),
+    # long enough for several MT twists per env
+    ("c2_16x16_n8", 129, 120, 0),
+    ("c2_16x16_n8|rt", 200, 40, 0),
 ])
 def test_rollout_equals_steps(name, E, T, k, monkeypatch):
     """drl_rollout (T steps per launch, state on chip) == T drl_step calls:
