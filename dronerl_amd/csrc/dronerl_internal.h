@@ -33,7 +33,11 @@ __host__ __device__ constexpr uint32_t ce_pack(int cell, int idx, int par) {
 }
 // ring entries each drl_step lane holds (P lanes per env: P * step_cq(P) candidates per step
 // without a second memory round trip; more come from the stream itself)
-constexpr int step_cq(int P) { return P <= 16 ? 2 : 1; }
+// (DRL_CQ_NARROW: the count at P <= 16, a tuning knob for tools/variants.py builds)
+#ifndef DRL_CQ_NARROW
+#define DRL_CQ_NARROW 2
+#endif
+constexpr int step_cq(int P) { return P <= 16 ? DRL_CQ_NARROW : 1; }
 // DRL_DPP8: P = 8 / 16 claim and crash-order scans by DPP lane swaps instead of ds_bpermute
 #ifndef DRL_DPP8
 #define DRL_DPP8 1
