@@ -274,17 +274,27 @@ def test_ragged_num_envs(E, k):
                                    (dict(n_drones=16, grid_size=32), 300), (dict(n_drones=6, grid_size=11), 129)])
 def test_streaming_obs_stores(cfg, E):
     """drl_step_ex(DRL_STEP_OBS_STREAM): identical observation, rewards and
-    state to the cached-store step, step after step."""
+    state to the cached-store step, step after step, and both equal to the
+    oracle (rewards and dones every step, the observation every 5th, the
+    final state)."""
     p = EnvParams(**cfg)
     envs = [Env(p, E), Env(p, E)]
     for env in envs:
         env.reset(seed=21)
+    o = OracleMulti(oparams(p), E)
+    o.reset(21 + np.arange(E))
     for t in range(1, 31):
         a = envs[0].synth_actions(seed=8, step=t)
         out = [env.step(a, obs_k=1, obs_stream=s) for env, s in zip(envs, (False, True))]
         for x, y in zip(out[0], out[1]):
             assert torch.equal(x, y), f"step {t}"
+        ro, do = o.step(a.cpu().numpy())
+        assert_rewards(out[1][0].cpu().numpy(), ro, f"streaming step {t}")
+        np.testing.assert_array_equal(out[1][1].cpu().numpy().astype(bool), np.asarray(do).astype(bool))
+        if t % 5 == 0:
+            np.testing.assert_array_equal(out[1][2].cpu().numpy(), o.obs(p.window_radius, 1))
     assert_state(gpu_state(envs[1]), gpu_state(envs[0]), "streaming vs cached")
+    assert_state(gpu_state(envs[1]), o.state(), "streaming vs oracle")
     envs[1].check_errors()
 
 
