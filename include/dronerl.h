@@ -322,7 +322,9 @@ typedef struct drl_qnet_desc {
 } drl_qnet_desc;
 
 /* Bytes of the packed network (weight fragments + f32 biases; DRL_QNET_F32
- * packs fp16 hi fragments where bf16 ones go, then the lo fragments). */
+ * packs fp16 hi and lo fragments: layer 0's hi and lo sets first when both
+ * fit the 160 KB LDS together, else the hi fragments where bf16 ones go and
+ * the lo fragments after them).  The layout is opaque to callers. */
 int drl_qnet_packed_bytes(const drl_qnet_desc* d, int64_t* bytes);
 /* Pack the network once per weight update.  d_weights / d_biases: host arrays
  * of n_hidden + 1 device pointers; layer l weights f32 [out][in] row-major
