@@ -119,8 +119,7 @@ def measure_traffic(args):
              "--no-pmc-traffic", "--cached-steps", "0"]
     if args.envs:
         child += ["--envs", str(args.envs)]
-    if args.obs_stream:
-        child.append("--obs-stream")
+    child.append("--obs-stream" if args.obs_stream else "--obs-cached")
     if args.obs_k >= 0:
         child += ["--obs-k", str(args.obs_k)]
     vals = {}
@@ -354,6 +353,11 @@ def rollout_bench(env, actions, K, warmup_steps, steps, chunk: int, R: int, Wb: 
                                  "read and written once per launch, so HBM traffic per step is lower"}}
 
 
+# diagnostic: the train loop's step with streaming observation stores (A/B of
+# env.step()'s store mode where the act kernel reads the observation next)
+LOOP_OBS_STREAM = {"0": False, "1": True}.get(os.environ.get("DRL_LOOP_OBS_STREAM", ""))
+
+
 class TrainSegment:
     """One segment of the train_jax.py:38-113 loop minus the learner (SURVEY.md
     §8 D2; C5: "multi-step loop, hipGraph of step+obs+act"): per step,
@@ -401,7 +405,8 @@ class TrainSegment:
         b, nb = t % self.NB, (t + 1) % self.NB
         self.net.act(self.obs[b].reshape(self.E, -1), 0.1, seed=7, step=t, env_offset=self.env.env_offset,
                      actions=self.acts[b], synth=(2024, t) if self.fused else None)
-        self.env.step(self.acts[b], obs_k=1, rewards=self.rewards[b], dones=self.dones[b], obs=self.obs[nb])
+        self.env.step(self.acts[b], obs_k=1, rewards=self.rewards[b], dones=self.dones[b], obs=self.obs[nb],
+                      obs_stream=LOOP_OBS_STREAM)  # None: env.step()'s default
 
     def _replay(self, t):
         b, nb = t % self.NB, (t + 1) % self.NB
@@ -499,8 +504,8 @@ def main():
                          "kernel fills every CU in one generation, and co-running kernels delay its waves)")
     ap.add_argument("--obs-stream", action="store_true",
                     help="write the per-step observation with streaming stores (DRL_STEP_OBS_STREAM); default: "
-                         "cached stores, env.step()'s default and what a train_jax-style caller gets")
-    ap.add_argument("--obs-cached", action="store_true", help="(the default; kept for old command lines)")
+                         "env.step()'s mode (cached at 8 lanes per env, streaming at >= 16)")
+    ap.add_argument("--obs-cached", action="store_true", help="write the per-step observation with cached stores")
     ap.add_argument("--obs-k", type=int, default=-1,
                     help="diagnostic: observed drones per step (default: the config's; 0 = step without obs)")
     ap.add_argument("--cached-steps", type=int, default=200,
@@ -536,6 +541,8 @@ def main():
     actions = torch.empty((T, E, N), dtype=torch.int32, device=dev)
     for t in range(T):
         env.synth_actions(seed=2024, step=t, out=actions[t])
+    if not args.obs_stream and not args.obs_cached:  # env.step()'s default store mode
+        args.obs_stream = env.default_obs_stream
     W = env.layout.obs_window
     rewards = torch.empty((E, N), dtype=torch.float32, device=dev)
     dones = torch.empty((E, N), dtype=torch.uint8, device=dev)
@@ -639,10 +646,9 @@ def main():
                   "ms_per_step": cwall / nc * 1e3, "avg_launch_us": c_launch * 1e6,
                   "frac": E * algorithmic_bytes(G, N, K, W)[0] / c_launch / 1e9 / PEAK_HBM_GBS,
                   "obs_stores": "cached" if args.obs_stream else "streaming",
-                  "note": ("env.step() / drl_step default (cached observation stores): what a train_jax-style "
-                           "caller whose policy reads the observation next gets") if args.obs_stream else
-                          ("drl_step_ex(DRL_STEP_OBS_STREAM): streaming observation stores, for an observation "
-                           "no kernel reads right away; same results")}
+                  "note": "the other observation store mode, same steps and results; `value` uses env.step()'s "
+                          "default (cached stores at 8 lanes per env, streaming at >= 16: the faster one in "
+                          "the train loop, profiles/r02_store_mode/)"}
 
     # resets (train_jax.py:101-113 resets every 100 steps in C5): timed separately
     resets_per_s = None

@@ -158,7 +158,9 @@ int drl_env_step_obs(drl_env* env, const int32_t* d_actions, float* d_rewards, u
     return on_device(env, [&]() -> int {
         if (!env->seeded) return drl_internal_fail("step before the first reset");
         if (!d_obs) return drl_internal_fail("obs is NULL");
-        return drl_step_ex(&env->p, &env->s, d_actions, d_rewards, d_dones, d_obs, k, env->err, refill_flag(env),
+        // store mode as env.step() picks it (drl_default_obs_stream)
+        const uint32_t st = env->L.step_group_lanes >= 16 ? DRL_STEP_OBS_STREAM : 0u;
+        return drl_step_ex(&env->p, &env->s, d_actions, d_rewards, d_dones, d_obs, k, env->err, refill_flag(env) | st,
                            stream);
     });
 }

@@ -97,6 +97,12 @@ class BatchedDeliveryDrones:
         # steps between drl_refill top-ups of the respawn-candidate rings (0: never;
         # the steps then draw every respawn from the MT stream themselves)
         self.refill_every = int(L.refill_every)
+        # step()'s default observation store mode: cached stores at P <= 8
+        # (C3: the act kernel that reads the observation next runs 64-66 us per
+        # loop step against 71 after streaming stores), streaming stores at
+        # P >= 16 (C4: 90 vs 93-94 us per loop step, 34.3 vs 36.6 per bare
+        # step; profiles/r02_store_mode/)
+        self.default_obs_stream = int(L.step_group_lanes) >= 16
         self._since_refill = 0
 
     # ------------------------------------------------------------ core API --
@@ -131,14 +137,17 @@ class BatchedDeliveryDrones:
         self._since_refill = 0
 
     def step(self, actions: torch.Tensor, obs_k: int = 0, rewards: Optional[torch.Tensor] = None,
-             dones: Optional[torch.Tensor] = None, obs: Optional[torch.Tensor] = None, obs_stream: bool = False):
+             dones: Optional[torch.Tensor] = None, obs: Optional[torch.Tensor] = None,
+             obs_stream: Optional[bool] = None):
         """env.py:112-215 for every env.  actions int32 [E, N] by drone index.
 
         Returns (rewards f32 [E,N], dones bool-as-uint8 [E,N]) and, when
         obs_k > 0, the fused observation f32 [E, obs_k, W, W, 6] of drone
         indices 0..obs_k-1 after the step (train_jax.py:55-56 uses obs_k=1).
         obs_stream: write the observation with streaming stores
-        (DRL_STEP_OBS_STREAM), for observations no kernel reads right away.
+        (DRL_STEP_OBS_STREAM) or cached ones; None (default) picks
+        ``default_obs_stream`` (streaming at step_group_lanes >= 16).  Results
+        are identical either way.
         """
         E, N = self.num_envs, self.n_drones
         actions = self._check(actions, torch.int32, (E, N), "actions")
@@ -154,6 +163,8 @@ class BatchedDeliveryDrones:
         if obs_k:
             self._check_out(obs, torch.float32, (E, obs_k, W, W, 6), "obs")
         s = self.state.c()
+        if obs_stream is None:
+            obs_stream = self.default_obs_stream
         flags = DRL_STEP_OBS_STREAM if obs_stream else 0
         if self.refill_every > 0:
             self._since_refill += 1
