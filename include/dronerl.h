@@ -274,7 +274,9 @@ int drl_env_seed(drl_env* env, uint64_t base_seed);
 int drl_env_reset(drl_env* env, const uint8_t* d_env_mask, hipStream_t stream);
 /* step() (env.py:112-215): actions i32, rewards f32, dones u8, [E][n_drones]. */
 int drl_env_step(drl_env* env, const int32_t* d_actions, float* d_rewards, uint8_t* d_dones, hipStream_t stream);
-/* step() + the WindowedGridView observation of drone indices 0..k-1 after it. */
+/* step() + the WindowedGridView observation of drone indices 0..k-1 after it
+ * (cached stores at layout.step_group_lanes 8 or less, streaming stores at 16
+ * and more: the faster mode when the policy reads the observation next). */
 int drl_env_step_obs(drl_env* env, const int32_t* d_actions, float* d_rewards, uint8_t* d_dones, int32_t k,
                      float* d_obs, hipStream_t stream);
 /* WindowedGridView observation (wrappers.py:55-73): f32 [E][k][W][W][6]. */
