@@ -98,13 +98,33 @@ def under_profiler():
     return "rocprof" in pre or any(k.startswith("ROCPROF") for k in os.environ)
 
 
-def measure_traffic(args):
-    """HBM bytes per drl_step launch from rocprofv3 PMC passes of this same
-    bench command (MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE in
-    separate passes, FETCH_SIZE doubled for gfx950, KiB -> bytes).  Runs as
-    child processes before this process touches the GPU; returns None when
-    rocprofv3 is absent or a pass fails (the caller then reports the committed
-    profile, labelled as such)."""
+# torchrun's per-rank variables: a rocprofv3 child started by rank 0 must run
+# as a plain single-process bench, not join the job's process group
+TORCHRUN_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                 "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+
+PMC_KERNELS = ("drl_step_kernel", "drl_refill_kernel")
+
+
+def child_env():
+    env = {k: v for k, v in os.environ.items() if k not in TORCHRUN_VARS and not k.startswith("TORCHELASTIC")}
+    env["TMPDIR"] = os.environ.get("TMPDIR", "/tmp")
+    local = os.environ.get("LOCAL_RANK")
+    if local not in (None, "0"):  # the rank's own GPU (rank 0 is normally local rank 0)
+        env["HIP_VISIBLE_DEVICES"] = local
+    return env
+
+
+def measure_traffic(args, names):
+    """HBM bytes per launch of drl_step_kernel and drl_refill_kernel for each
+    config in `names`, from rocprofv3 PMC passes of this same bench
+    (MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE in separate passes,
+    FETCH_SIZE doubled for gfx950, KiB -> bytes).  One child process per
+    counter runs every config's step loop (`--pmc-child`, same store mode,
+    same pre-roll and refill cadence as the timed loops) before this process
+    touches the GPU; the child reports each config's launch grid sizes, which
+    attribute the counter rows.  Returns None when rocprofv3 is absent or a
+    pass fails (the caller then reports the committed profile, labelled)."""
     import csv
     import glob
     import shutil
@@ -114,23 +134,26 @@ def measure_traffic(args):
                                          else None)
     if prof is None or under_profiler():
         return None
-    child = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", "20", "--warmup", "3",
-             "--no-cpu-baseline", "--no-reset-bench", "--no-dqn", "--rollout-chunk", "0", "--loop-segments", "0",
-             "--no-pmc-traffic", "--cached-steps", "0"]
-    if args.envs:
-        child += ["--envs", str(args.envs)]
-    child.append("--obs-stream" if args.obs_stream else "--obs-cached")
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", ",".join(names), "--config", args.config,
+             "--steps", "20", "--warmup", "3", "--envs", str(args.envs), "--c5-envs", str(args.c5_envs)]
+    # the store mode: forced flags pass through; otherwise the child resolves
+    # env.step()'s default itself, exactly as the timed loop does
+    if args.obs_stream:
+        child.append("--obs-stream")
+    elif args.obs_cached:
+        child.append("--obs-cached")
     if args.obs_k >= 0:
         child += ["--obs-k", str(args.obs_k)]
-    vals = {}
-    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    rows = {}
+    grids = None
+    env = child_env()
     with tempfile.TemporaryDirectory(prefix="drl_pmc_") as td:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(td, ctr)
-            cmd = [prof, "--pmc", ctr, "--kernel-include-regex", "drl_step_kernel", "-d", d, "-o", "run",
+            cmd = [prof, "--pmc", ctr, "--kernel-include-regex", "|".join(PMC_KERNELS), "-d", d, "-o", "run",
                    "--output-format", "csv", "--"] + child
             try:
-                r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=150, env=env,
+                r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=240, env=env,
                                    cwd=REPO)
             except subprocess.TimeoutExpired:
                 print(f"pmc pass {ctr}: timed out", file=sys.stderr)
@@ -139,20 +162,38 @@ def measure_traffic(args):
                 print(f"pmc pass {ctr}: rc={r.returncode} {r.stderr.decode(errors='replace')[-300:]}",
                       file=sys.stderr)
                 return None
-            xs = []
+            for ln in r.stdout.decode(errors="replace").splitlines():
+                if ln.startswith("{\"pmc_child\""):
+                    grids = json.loads(ln)["pmc_child"]
             for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
                 for row in csv.DictReader(open(f)):
-                    if "drl_step_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
-                        xs.append(float(row["Counter_Value"]))
-            if not xs:
-                return None
-            vals[ctr] = sum(xs) / len(xs)
-    read_b = 2 * vals["FETCH_SIZE"] * 1024
-    write_b = vals["WRITE_SIZE"] * 1024
-    return {"bytes_per_launch": read_b + write_b, "read_bytes_per_launch": read_b, "write_bytes_per_launch": write_b,
-            "fetch_size_kib": vals["FETCH_SIZE"], "write_size_kib": vals["WRITE_SIZE"],
-            "source": "measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate child runs "
-                      "of this bench, 20 steps), traffic = 2*FETCH_SIZE + WRITE_SIZE"}
+                    if row.get("Counter_Name") != ctr:
+                        continue
+                    kern = next((k for k in PMC_KERNELS if k in row.get("Kernel_Name", "")), None)
+                    if kern:
+                        rows.setdefault((ctr, kern, int(row["Grid_Size"])), []).append(float(row["Counter_Value"]))
+    if not grids:
+        return None
+    out = {}
+    for name, g in grids.items():
+        rec = {}
+        for kern, key in (("drl_step_kernel", "step_grid"), ("drl_refill_kernel", "refill_grid")):
+            f = rows.get(("FETCH_SIZE", kern, g[key]))
+            w = rows.get(("WRITE_SIZE", kern, g[key]))
+            if not f or not w:
+                continue
+            rd = 2 * sum(f) / len(f) * 1024
+            wr = sum(w) / len(w) * 1024
+            rec[kern] = {"bytes_per_launch": rd + wr, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+                         "read_bytes_per_env": rd / g["envs"], "write_bytes_per_env": wr / g["envs"],
+                         "launches": min(len(f), len(w))}
+        if "drl_step_kernel" in rec:
+            rec["envs"] = g["envs"]
+            rec["source"] = ("measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate child "
+                             "runs of this bench's step loop, 20 steps after a refill-cycle pre-roll), traffic = "
+                             "2*FETCH_SIZE + WRITE_SIZE per launch")
+            out[name] = rec
+    return out or None
 
 
 def load_traffic(cfg_name: str):
@@ -244,16 +285,18 @@ def cpu_baseline(G, N, K, seconds: float):
             "cpu_model": cpu_model()}
 
 
-def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream):
+def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream, precision="f32"):
     """the C3 loop's consumer of the observation, timed
     separately from the env step.  (1) drl_qnet_act alone on the resident obs
     (dense 294->128->64->5 on MFMA, epsilon-greedy, writes actions[:, 0]):
     HBM-bound on reading the obs (E * W*W*6 f32); (2) the train_jax.py:42-64
-    loop shape per step: act -> step + obs -> replay add_many (capacity 10000)."""
+    loop shape per step: act -> step + obs -> replay add_many (capacity 10000).
+    `precision` is the loop's (f32: the reference's nets); both acts are
+    timed alone."""
     from dronerl_amd.dqn import QNetwork, ReplayBuffer
     E = env.num_envs
     D = obs[0].numel()
-    net = QNetwork(D, (128, 64), device=env.device, generator=torch.Generator().manual_seed(0))
+    net = QNetwork(D, (128, 64), device=env.device, generator=torch.Generator().manual_seed(0), precision=precision)
     rb = ReplayBuffer(10000, D, env.device)
     flat = obs.reshape(E, -1)
     a0 = actions[0]
@@ -276,8 +319,9 @@ def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream)
     ev[3].record(stream)
     torch.cuda.synchronize()
     env.check_errors()
-    # the same act with the reference's f32 numerics (DRL_QNET_F32)
-    net32 = QNetwork(D, (128, 64), device=env.device, generator=torch.Generator().manual_seed(0), precision="f32")
+    # the act in the other precision
+    other = "bf16" if precision == "f32" else "f32"
+    net32 = QNetwork(D, (128, 64), device=env.device, generator=torch.Generator().manual_seed(0), precision=other)
     for t in range(warmup):
         net32.act(flat, 0.1, seed=1, step=t, actions=a0)
     f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -286,21 +330,23 @@ def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream)
         net32.act(flat, 0.1, seed=1, step=t, actions=a0)
     f1.record(stream)
     torch.cuda.synchronize()
-    act32_s = f0.elapsed_time(f1) / 1e3 / steps
+    act_o = f0.elapsed_time(f1) / 1e3 / steps
     act_s = ev[0].elapsed_time(ev[1]) / 1e3 / steps
     loop_s = ev[2].elapsed_time(ev[3]) / 1e3 / steps
     read = E * D * 4
-    return {"net": f"dense {D}->128->64->5, bf16 MFMA (f32 accumulate)", "act_us": act_s * 1e6,
-            "act_roofline": {"bound": "hbm", "achieved": read / act_s / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                             "frac": read / act_s / 1e9 / PEAK_HBM_GBS,
-                             "algorithmic_bytes_per_env": D * 4 + 4},
-            "act_f32_us": act32_s * 1e6,
-            "act_f32_roofline": {"bound": "hbm", "achieved": read / act32_s / 1e9, "peak": PEAK_HBM_GBS,
-                                 "unit": "GB/s", "frac": read / act32_s / 1e9 / PEAK_HBM_GBS},
+    t = {"bf16": (act_o, act_s), "f32": (act_s, act_o)}[other]
+    rl = lambda s: {"bound": "hbm", "achieved": read / s / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",  # noqa: E731
+                    "frac": read / s / 1e9 / PEAK_HBM_GBS, "algorithmic_bytes_per_env": D * 4 + 4}
+    return {"net": f"dense {D}->128->64->5", "precision": precision,
+            "act_f32_us": t[1] * 1e6, "act_f32_roofline": rl(t[1]),
             "act_f32_note": "precision='f32' (DRL_QNET_F32): fp16 hi/lo split operands, 3 MFMAs per product tile, "
                             "Q to f32 rounding (the reference's f32 nets)",
+            "act_bf16_us": t[0] * 1e6, "act_bf16_roofline": rl(t[0]),
+            "act_bf16_note": "precision='bf16': bf16 MFMA operands, f32 accumulate (a labelled extra; narrower than "
+                             "the reference)",
             "loop_us_per_step": loop_s * 1e6, "loop_env_steps_per_s": E / loop_s,
-            "loop": "act(obs_t) -> step + obs(K=1) -> replay add_many(obs_t, a, r, obs_t+1, done), capacity 10000"}
+            "loop": f"act(obs_t, {precision}) -> step + obs(K=1) -> replay add_many(obs_t, a, r, obs_t+1, done), "
+                    "capacity 10000"}
 
 
 def rollout_bench(env, actions, K, warmup_steps, steps, chunk: int, R: int, Wb: int, world: int):
@@ -347,10 +393,8 @@ def rollout_bench(env, actions, K, warmup_steps, steps, chunk: int, R: int, Wb: 
             "kernel": "drl_rollout_kernel", "avg_launch_us": ev_s / -(-steps // chunk) * 1e6,
             "roofline": {"bound": "hbm", "achieved": E * R / per_step / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": E * R / per_step / 1e9 / PEAK_HBM_GBS,
-                         "achieved_read_plus_write": E * (R + Wb) / per_step / 1e9,
-                         "frac_read_plus_write": E * (R + Wb) / per_step / 1e9 / PEAK_HBM_GBS,
-                         "note": "same per-env-step algorithmic bytes as drl_step (SURVEY.md §8 D3); the state is "
-                                 "read and written once per launch, so HBM traffic per step is lower"}}
+                         "note": "same per-env-step algorithmic read bytes R as drl_step (SURVEY.md §8 D3); the "
+                                 "state is read and written once per launch, so HBM traffic per step is lower"}}
 
 
 # diagnostic: the train loop's step with streaming observation stores (A/B of
@@ -378,7 +422,8 @@ class TrainSegment:
     stream with 2 buffers; both leave identical state and replay contents
     (tests/test_gpu_parity.py::test_train_segment_parallel_matches_serial)."""
 
-    def __init__(self, env, seg: int, parallel: bool = False, net=None, rb=None, fused: bool = True):
+    def __init__(self, env, seg: int, parallel: bool = False, net=None, rb=None, fused: bool = True,
+                 precision: str = "f32"):
         from dronerl_amd.dqn import QNetwork, ReplayBuffer
         E, N, dev = env.num_envs, env.n_drones, env.device
         W = env.layout.obs_window
@@ -389,7 +434,8 @@ class TrainSegment:
         # suffice, and the third 77 MB observation buffer costs MALL hits (C3
         # loop 79.4 vs 74.4 us per step)
         self.NB = 3 if parallel else 2
-        self.net = net or QNetwork(D, (128, 64), device=dev, generator=torch.Generator().manual_seed(0))
+        self.net = net or QNetwork(D, (128, 64), device=dev, generator=torch.Generator().manual_seed(0),
+                                   precision=precision)
         self.rb = rb or ReplayBuffer(10000, D, dev)
         self.acts = [torch.empty((E, N), dtype=torch.int32, device=dev) for _ in range(self.NB)]
         self.rewards = [torch.empty((E, N), dtype=torch.float32, device=dev) for _ in range(self.NB)]
@@ -447,13 +493,14 @@ class TrainSegment:
         self.env.get_obs(1, out=self.obs[0])
 
 
-def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fused: bool = True):
+def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fused: bool = True,
+                     precision: str = "f32"):
     """TrainSegment captured once as a HIP graph (no host work per step) and
     replayed.  Counters (action stream step, epsilon draws, replay cursor) are
     baked into the capture, so replays repeat them: the work per step is the
     same, the action stream repeats every segment."""
     dev = env.device
-    loop = TrainSegment(env, seg, parallel=parallel, fused=fused)
+    loop = TrainSegment(env, seg, parallel=parallel, fused=fused, precision=precision)
     side = torch.cuda.Stream(dev)
     side.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(side):
@@ -477,9 +524,189 @@ def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fus
     branches = ("synthetic actions and replay add_many on parallel graph branches, 3 rotating buffers"
                 if parallel else "one stream" + ("; synthetic actions inside the act launch" if fused else ""))
     return {"env_steps_per_s": E * seg * reps / dt, "us_per_step": dt / (seg * reps) * 1e6,
-            "segments": reps, "steps_per_segment": seg,
-            "loop": f"hipGraph of {seg} x [synth actions -> qnet act (drone 0) -> step + obs(K=1) -> "
+            "segments": reps, "steps_per_segment": seg, "precision": precision,
+            "loop": f"hipGraph of {seg} x [synth actions -> qnet act (drone 0, {precision}) -> step + obs(K=1) -> "
                     f"replay add_many] + reset + obs, replayed {reps}x ({branches}; learner not included)"}
+
+
+def refill_plan(pre: int, warmup: int, steps: int, every: int):
+    """env.step()'s refill cadence over one bench run: drl_refill follows
+    global step s when (s + 1) % every == 0, counting from the first pre-roll
+    step.  Returns the timed steps a refill follows and the share of a refill
+    still to charge the timed region, steps / every - (refills inside it):
+    every timed step then carries exactly 1/every of a refill whatever the
+    step count (a 20-step window holds no refill at every = 32; a 1000-step
+    one holds 31 and is charged 0.25 more)."""
+    if every <= 0:
+        return [], 0.0
+    first = pre + warmup
+    inside = [s for s in range(first, first + steps) if (s + 1) % every == 0]
+    return inside, steps / every - len(inside)
+
+
+class StepRunner:
+    """The timed loop of one config: drl_step_ex launches through a ctypes
+    fast path (arguments built once; only the actions pointer moves), with
+    drl_refill at env.step()'s cadence bracketed by HIP events on the launch
+    stream, so the step kernel's average duration and the refills' can be
+    told apart.  Actions are synthetic uniform {0..4} (counter hash),
+    generated before timing and resident in HBM."""
+
+    def __init__(self, env, K: int, n_actions: int, obs_stream: bool):
+        from dronerl_amd._native import DRL_STEP_OBS_STREAM, lib
+        E, N, dev = env.num_envs, env.n_drones, env.device
+        self.env, self.K, self.E = env, K, E
+        self.L = lib()
+        self.stream = torch.cuda.current_stream(dev)
+        self.actions = torch.empty((n_actions, E, N), dtype=torch.int32, device=dev)
+        for t in range(n_actions):
+            env.synth_actions(seed=2024, step=t, out=self.actions[t])
+        W = env.layout.obs_window
+        self.rewards = torch.empty((E, N), dtype=torch.float32, device=dev)
+        self.dones = torch.empty((E, N), dtype=torch.uint8, device=dev)
+        self.obs = torch.empty((E, max(K, 1), W, W, 6), dtype=torch.float32, device=dev)
+        self._cp = ctypes.byref(env._cp)
+        self._st = env.state.c()
+        self._sp = ctypes.byref(self._st)
+        self._a = [ctypes.c_void_p(self.actions[t].data_ptr()) for t in range(n_actions)]
+        self._r, self._d, self._o = (ctypes.c_void_p(x.data_ptr()) for x in (self.rewards, self.dones, self.obs))
+        if K == 0:
+            self._o = None
+        self._e = ctypes.c_void_p(env.err.data_ptr())
+        self._s = ctypes.c_void_p(self.stream.cuda_stream)
+        self.flag_stream = DRL_STEP_OBS_STREAM
+        self.obs_stream = obs_stream
+        self.every = env.refill_every
+        self.s = 0  # global step counter (refill cadence)
+        self.refill_ev = []  # (start, end, timed) events of every refill
+
+    def step(self, timed: bool):
+        t = self.s % len(self._a)
+        flags = self.flag_stream if self.obs_stream else 0
+        rc = self.L.drl_step_ex(self._cp, self._sp, self._a[t], self._r, self._d, self._o, self.K, self._e, flags,
+                                self._s)
+        if rc:
+            raise RuntimeError(self.L.drl_last_error().decode())
+        if self.every > 0 and (self.s + 1) % self.every == 0:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(self.stream)
+            rc = self.L.drl_refill(self._cp, self._sp, self._s)
+            if rc:
+                raise RuntimeError(self.L.drl_last_error().decode())
+            ev[1].record(self.stream)
+            self.refill_ev.append(ev + (timed,))
+        self.s += 1
+
+    def run(self, steps: int, warmup: int, world: int, pre: int = 0):
+        """pre + warmup untimed steps, then `steps` timed ones bracketed by a
+        barrier + synchronize on both sides, max over ranks.  The value
+        charges the timed region steps/every refills (refill_plan)."""
+        for _ in range(pre + warmup):
+            self.step(False)
+        torch.cuda.synchronize()
+        barrier(world)
+        torch.cuda.synchronize()
+        n_before = len(self.refill_ev)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(self.stream)
+        for _ in range(steps):
+            self.step(True)
+        ev1.record(self.stream)
+        torch.cuda.synchronize()
+        barrier(world)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        self.env.check_errors()
+        wall_max = max_over_ranks(wall, world)
+        inside = [e for e in self.refill_ev[n_before:] if e[2]]
+        plan, charge = refill_plan(0, self.s - steps, steps, self.every)
+        assert len(plan) == len(inside), (plan, len(inside))
+        ref_in_ms = sum(a.elapsed_time(b) for a, b, _ in inside)
+        all_ms = [a.elapsed_time(b) for a, b, _ in self.refill_ev]
+        refill_avg_s = max_over_ranks(sum(all_ms) / len(all_ms) / 1e3 if all_ms else 0.0, world)
+        charged = wall_max + charge * refill_avg_s
+        launch_s = (ev0.elapsed_time(ev1) - ref_in_ms) / 1e3 / steps  # drl_step kernel, on this stream
+        return {"value": self.E * world * steps / charged, "ms_per_step": charged / steps * 1e3,
+                "wall_ms_per_step": wall_max / steps * 1e3, "launch_s": launch_s,
+                "refill": {"every": self.every, "launches_in_region": len(inside),
+                           "launches_measured": len(all_ms), "avg_launch_us": refill_avg_s * 1e6,
+                           "per_step_us": refill_avg_s / self.every * 1e6 if self.every > 0 else 0.0,
+                           "charged_launches": steps / self.every if self.every > 0 else 0.0,
+                           "prorated_launches": charge,
+                           "note": "env.step()'s cadence (a refill after every `every`-th step, counted from the "
+                                   "pre-roll); the timed region is charged exactly steps/every refills: the ones "
+                                   "inside it (wall clock) plus prorated_launches x avg_launch_us (HIP events, "
+                                   "max over ranks), so value and ms_per_step carry the refill share at any step "
+                                   "count"}}
+
+
+def roofline(E, R, Wb, launch_s, refill, traffic):
+    """SURVEY.md §8 D3 roofline of the dominant kernel (drl_step_kernel):
+    achieved = E * R (algorithmic read bytes per env-step) / its average
+    launch duration (HIP events on the launch stream).  `traffic` = measured
+    HBM bytes per launch (PMC); frac_measured = traffic / launch / peak, the
+    fraction of the HBM peak the kernel actually moves (<= 1 by construction,
+    unlike a read+write figure whose W counts a full ground write-back the
+    kernel never does).  with_refill adds the refill share per step."""
+    achieved = E * R / launch_s / 1e9
+    out = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+           "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": "drl_step_kernel",
+           "avg_launch_us": launch_s * 1e6, "algorithmic_read_bytes_per_env_step": R,
+           "algorithmic_write_bytes_per_env_step": Wb, "frac_ceiling_read_only": R / (R + Wb),
+           "note": "frac counts SURVEY.md §8 D3's read bytes R only (achieved = E*R / avg drl_step launch); moving "
+                   "all R + W algorithmic bytes at the HBM peak would score frac_ceiling_read_only = R/(R+W). "
+                   "traffic = measured HBM bytes per drl_step launch (2*FETCH_SIZE + WRITE_SIZE), "
+                   "frac_measured = traffic / avg launch / peak"}
+    per_step_s = launch_s + refill["per_step_us"] / 1e6
+    out["with_refill"] = {"us_per_step": per_step_s * 1e6, "achieved": E * R / per_step_s / 1e9,
+                          "frac": E * R / per_step_s / 1e9 / PEAK_HBM_GBS}
+    if traffic:
+        st = traffic["drl_step_kernel"]
+        out["traffic"] = st["bytes_per_launch"]
+        out["frac_measured"] = st["bytes_per_launch"] / launch_s / 1e9 / PEAK_HBM_GBS
+        out["traffic_detail"] = dict(st, source=traffic.get("source"), envs=traffic.get("envs"))
+        rf = traffic.get("drl_refill_kernel")
+        if rf and refill["every"] > 0:
+            per_step_b = st["bytes_per_launch"] + rf["bytes_per_launch"] / refill["every"]
+            out["with_refill"].update({"traffic_per_step": per_step_b,
+                                       "frac_measured": per_step_b / per_step_s / 1e9 / PEAK_HBM_GBS,
+                                       "refill_traffic_per_launch": rf["bytes_per_launch"],
+                                       "refill_read_bytes_per_env": rf["read_bytes_per_env"],
+                                       "refill_write_bytes_per_env": rf["write_bytes_per_env"]})
+    return out
+
+
+def make_env(cfg: str, envs: int, rank: int, dev):
+    from dronerl_amd import BatchedDeliveryDrones, EnvParams
+    G, N, E, K = CONFIGS[cfg]
+    E = envs or E
+    env = BatchedDeliveryDrones(EnvParams(n_drones=N, grid_size=G), E, device=dev, env_offset=rank * E)
+    env.reset(seed=0)
+    return env, G, N, E, K
+
+
+def pmc_child(args):
+    """--pmc-child: the step loops the rocprofv3 counter passes of
+    measure_traffic profile (no timing, no extras); prints each config's
+    launch grid sizes (threads) so the parent can attribute the rows."""
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    grids = {}
+    for name in args.pmc_child.split(","):
+        envs = args.c5_envs if name == "c5" and args.config != "c5" else args.envs
+        env, G, N, E, K = make_env(name, envs, 0, dev)
+        if args.obs_k >= 0 and name == args.config:
+            K = args.obs_k
+        stream = args.obs_stream or (env.default_obs_stream and not args.obs_cached)
+        run = StepRunner(env, K, 8, stream)
+        run.run(args.steps, args.warmup, 1, pre=env.refill_every)
+        P = env.layout.step_group_lanes
+        grids[name] = {"envs": E, "step_grid": -(-E // (64 // P)) * 64, "refill_grid": -(-E // 4) * 64}
+        del run, env
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    print(json.dumps({"pmc_child": grids}), flush=True)
 
 
 def main():
@@ -489,10 +716,16 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--envs", type=int, default=0, help="override envs per GPU")
+    ap.add_argument("--c5-envs", type=int, default=CONFIGS["c5"][2],
+                    help="envs per GPU of the north-star sub-record (C5: 64x64 grid, 32 drones; 131072 per GPU = "
+                         "2^20 over 8 GPUs; 0 = skip)")
+    ap.add_argument("--c5-steps", type=int, default=200, help="timed steps of the north-star sub-record (>= 200)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-reset-bench", action="store_true")
     ap.add_argument("--no-dqn", action="store_true", help="skip the DQN-consumer measurement (SURVEY.md §8 F1)")
+    ap.add_argument("--loop-precision", default="f32", choices=("f32", "bf16"),
+                    help="Q-network arithmetic of the DQN loops (f32: the reference's nets; bf16 reported beside)")
     ap.add_argument("--rollout-chunk", type=int, default=100,
                     help="steps per drl_rollout launch for the rollout measurement (0 = skip)")
     ap.add_argument("--loop-segments", type=int, default=3,
@@ -513,142 +746,59 @@ def main():
                          "`streaming_obs` (or `cached_obs` with --obs-stream) (0 = skip)")
     ap.add_argument("--no-pmc-traffic", action="store_true",
                     help="do not run the rocprofv3 FETCH_SIZE / WRITE_SIZE passes for roofline.traffic")
+    ap.add_argument("--pmc-child", default="", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.pmc_child:
+        return pmc_child(args)
 
+    north = args.c5_envs > 0 and args.config != "c5"
+    names = [args.config] + (["c5"] if north else [])
     traffic_run = None
-    if (not args.no_pmc_traffic and int(os.environ.get("WORLD_SIZE", "1")) == 1
+    if (not args.no_pmc_traffic and int(os.environ.get("RANK", "0")) == 0
             and os.environ.get("DRL_BENCH_PMC", "1") != "0"):
-        traffic_run = measure_traffic(args)  # child processes, before this one touches the GPU
+        traffic_run = measure_traffic(args, names)  # child processes, before this one touches the GPU
 
     rank, world, local = dist_init()
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
-    from dronerl_amd import BatchedDeliveryDrones, EnvParams
-    from dronerl_amd._native import DRL_STEP_OBS_STREAM, lib
-
-    G, N, E, K = CONFIGS[args.config]
-    if args.envs:
-        E = args.envs
+    dev = torch.device("cuda", local)
+    env, G, N, E, K = make_env(args.config, args.envs, rank, dev)
     if args.obs_k >= 0:
         K = args.obs_k
-    p = EnvParams(n_drones=N, grid_size=G)
-    dev = torch.device("cuda", local)
-    env = BatchedDeliveryDrones(p, E, device=dev, env_offset=rank * E)
-    env.reset(seed=0)
-    T = args.warmup + args.steps
-    # synthetic actions for every step, resident in HBM before timing
-    actions = torch.empty((T, E, N), dtype=torch.int32, device=dev)
-    for t in range(T):
-        env.synth_actions(seed=2024, step=t, out=actions[t])
     if not args.obs_stream and not args.obs_cached:  # env.step()'s default store mode
         args.obs_stream = env.default_obs_stream
     W = env.layout.obs_window
-    rewards = torch.empty((E, N), dtype=torch.float32, device=dev)
-    dones = torch.empty((E, N), dtype=torch.uint8, device=dev)
-    obs = torch.empty((E, max(K, 1), W, W, 6), dtype=torch.float32, device=dev)
-
-    # fast path: ctypes arguments built once; only the actions pointer moves
-    L = lib()
-    cp = ctypes.byref(env._cp)
-    st = env.state.c()
-    sp = ctypes.byref(st)
-    a_ptrs = [ctypes.c_void_p(actions[t].data_ptr()) for t in range(T)]
-    r_p, d_p, o_p = (ctypes.c_void_p(x.data_ptr()) for x in (rewards, dones, obs))
-    if K == 0:
-        o_p = None
-    e_p = ctypes.c_void_p(env.err.data_ptr())
-    stream = torch.cuda.current_stream(dev)
-    s_p = ctypes.c_void_p(stream.cuda_stream)
-
-    # cached observation stores (env.step()'s default, what a train_jax-style
-    # caller gets) unless --obs-stream; the other mode is timed after it
-    flags = DRL_STEP_OBS_STREAM if args.obs_stream else 0
-
-    # the respawn-candidate rings are topped up every refill_every steps (what
-    # env.step() does), as a separate drl_refill launch bracketed by its own
-    # events, so the step kernel's average duration can be separated from it
-    refill_every = env.refill_every
-    refill_ev = []  # (start, end) event pairs of the timed region's refills
-
-    def run(t, timed=False):
-        rc = L.drl_step_ex(cp, sp, a_ptrs[t], r_p, d_p, o_p, K, e_p, flags, s_p)
-        if rc:
-            raise RuntimeError(L.drl_last_error().decode())
-        if refill_every > 0 and (t + 1) % refill_every == 0:
-            if timed:
-                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                ev[0].record(stream)
-            rc = L.drl_refill(cp, sp, s_p)
-            if rc:
-                raise RuntimeError(L.drl_last_error().decode())
-            if timed:
-                ev[1].record(stream)
-                refill_ev.append(ev)
-
-    for t in range(args.warmup):
-        run(t)
-    torch.cuda.synchronize()
-    barrier(world)
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for t in range(args.warmup, T):
-        run(t, timed=True)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    barrier(world)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    ev_ms = ev0.elapsed_time(ev1)
-    env.check_errors()
-    wall_max = max_over_ranks(wall, world)
-
-    total_env_steps = E * world * args.steps
-    value = total_env_steps / wall_max
-    refill_ms = sum(a.elapsed_time(b) for a, b in refill_ev)
-    launch_s = (ev_ms - refill_ms) / 1e3 / args.steps  # average drl_step duration on this stream
-    refill = {"every": refill_every, "launches": len(refill_ev),
-              "avg_launch_us": refill_ms / max(len(refill_ev), 1) * 1e3,
-              "per_step_us": refill_ms / args.steps * 1e3,
-              "note": "drl_refill (respawn-candidate rings) launches inside the timed region: in value and "
-                      "ms_per_step, not in roofline.avg_launch_us (the drl_step kernel alone)"}
     R, Wb = algorithmic_bytes(G, N, K, W)
-    achieved = E * R / launch_s / 1e9
-    achieved_rw = E * (R + Wb) / launch_s / 1e9
 
-    # the other observation store mode, same steps
-    cached = None
+    # ---- the headline: setup rolls one refill cycle (steady-state rings),
+    # then W warm-up and K timed steps
+    runner = StepRunner(env, K, args.warmup + args.steps + env.refill_every, args.obs_stream)
+    main_res = runner.run(args.steps, args.warmup, world, pre=env.refill_every)
+    actions, rewards, dones, obs, stream = runner.actions, runner.rewards, runner.dones, runner.obs, runner.stream
+
+    def traffic_of(name):
+        if traffic_run is not None and name in traffic_run:
+            return traffic_run[name]
+        t = load_traffic(name)
+        if t is None:
+            return None
+        return {"drl_step_kernel": {"bytes_per_launch": t},
+                "source": f"committed profiles/pmc_{name}.json (an earlier run; no rocprofv3 pass in this one)"}
+
+    # ---- the other observation store mode, same steps
+    other = None
     if args.cached_steps > 0 and K > 0:
-        flags_main = flags
-        flags = 0 if args.obs_stream else DRL_STEP_OBS_STREAM
+        runner.obs_stream = not args.obs_stream
         nc = min(args.cached_steps, args.steps)
-        for t in range(min(args.warmup, 20)):
-            run(t)
-        torch.cuda.synchronize()
-        barrier(world)
-        torch.cuda.synchronize()
-        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        tc = time.perf_counter()
-        c0.record(stream)
-        for t in range(args.warmup, args.warmup + nc):
-            run(t)
-        c1.record(stream)
-        torch.cuda.synchronize()
-        barrier(world)
-        torch.cuda.synchronize()
-        cwall = max_over_ranks(time.perf_counter() - tc, world)
-        env.check_errors()
-        flags = flags_main
-        c_launch = c0.elapsed_time(c1) / 1e3 / nc  # (refill share included)
-        cached = {"value": E * world * nc / cwall, "unit": "env-steps/s", "steps": nc,
-                  "ms_per_step": cwall / nc * 1e3, "avg_launch_us": c_launch * 1e6,
-                  "frac": E * algorithmic_bytes(G, N, K, W)[0] / c_launch / 1e9 / PEAK_HBM_GBS,
-                  "obs_stores": "cached" if args.obs_stream else "streaming",
-                  "note": "the other observation store mode, same steps and results; `value` uses env.step()'s "
-                          "default (cached stores at 8 lanes per env, streaming at >= 16: the faster one in "
-                          "the train loop, profiles/r02_store_mode/)"}
+        o = runner.run(nc, min(args.warmup, 20), world)
+        runner.obs_stream = args.obs_stream
+        other = {"value": o["value"], "unit": "env-steps/s", "steps": nc, "ms_per_step": o["ms_per_step"],
+                 "avg_launch_us": o["launch_s"] * 1e6, "frac": E * R / o["launch_s"] / 1e9 / PEAK_HBM_GBS,
+                 "obs_stores": "cached" if args.obs_stream else "streaming",
+                 "note": "the other observation store mode, same steps and results, refill share charged the same "
+                         "way; `value` uses env.step()'s default (cached stores at 8 lanes per env, streaming at "
+                         ">= 16: the faster one in the train loop, profiles/r02_store_mode/)"}
 
     # resets (train_jax.py:101-113 resets every 100 steps in C5): timed separately
     resets_per_s = None
@@ -666,7 +816,8 @@ def main():
 
     dqn = None
     if K >= 1 and not args.no_dqn:
-        dqn = dqn_consumer_bench(env, actions, rewards, dones, obs, args.warmup, min(args.steps, 200), stream)
+        dqn = dqn_consumer_bench(env, actions, rewards, dones, obs, args.warmup, min(args.steps, 200), stream,
+                                 args.loop_precision)
 
     roll = None
     if args.rollout_chunk > 0:
@@ -680,60 +831,69 @@ def main():
 
     loop = None
     if args.loop_segments > 0 and not args.no_dqn and K >= 1:
-        loop = train_loop_bench(env, args.loop_segments, parallel=args.parallel_loop, fused=not args.unfused_act)
+        loop = train_loop_bench(env, args.loop_segments, parallel=args.parallel_loop, fused=not args.unfused_act,
+                                precision=args.loop_precision)
         loop["env_steps_per_s"] = min_over_ranks(loop["env_steps_per_s"], world) * world
         loop["n_gpus"] = world
+    del runner, actions, rewards, dones, obs, env
+
+    # ---- the north-star configuration (BASELINE.json north_star, SURVEY.md
+    # §8 D2 C5): 64x64 grid, 32 drones, c5_envs per rank (2^20 over 8 GPUs),
+    # step + obs(K=1) with refills, >= 200 timed steps
+    c5 = None
+    if north:
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        env5, G5, N5, E5, K5 = make_env("c5", args.c5_envs, rank, dev)
+        st5 = env5.default_obs_stream
+        steps5 = max(args.c5_steps, 200)
+        run5 = StepRunner(env5, K5, steps5 + 20 + env5.refill_every, st5)
+        r5 = run5.run(steps5, 20, world, pre=env5.refill_every)
+        R5, W5 = algorithmic_bytes(G5, N5, K5, env5.layout.obs_window)
+        c5 = {"value": r5["value"], "unit": "env-steps/s", "n_gpus": world, "steps": steps5, "warmup": 20,
+              "ms_per_step": r5["ms_per_step"], "wall_ms_per_step": r5["wall_ms_per_step"],
+              "config": {"workload": f"C5 (north star): {G5}x{G5} grid, {N5} drones, {E5} envs/GPU, "
+                                     f"step + fused obs(K={K5})", "num_envs_per_gpu": E5,
+                         "num_envs_total": E5 * world, "obs_stores": "streaming" if st5 else "cached",
+                         "parallelism": f"env-shard x{world}"},
+              "roofline": roofline(E5, R5, W5, r5["launch_s"], r5["refill"], traffic_of("c5")),
+              "refill": r5["refill"],
+              "north_star": "BASELINE.json: >= 1e8 env-steps/s at num_envs=2^20 on 8 GPUs at >= 40% HBM-read "
+                            "roofline (roofline.frac)"}
+        del run5, env5
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(G, N, K, args.cpu_seconds)
 
-    traffic_src = None
-    if traffic_run is not None:
-        traffic, traffic_src = traffic_run["bytes_per_launch"], traffic_run
-    else:
-        traffic = load_traffic(args.config)
-        if traffic is not None:
-            traffic_src = {"source": f"committed profiles/pmc_{args.config}.json (an earlier run; no rocprofv3 pass "
-                                     "in this one)"}
     if rank == 0:
         with open(os.path.join(REPO, "BASELINE.json")) as f:
             metric = json.load(f)["metric"]
         out = {
             "metric": metric,
-            "value": value,
+            "value": main_res["value"],
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": wall_max / args.steps * 1e3,
+            "ms_per_step": main_res["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic uniform random actions (counter hash), envs seeded random.seed(env index)",
             "config": {"workload": f"{args.config.upper()}: {G}x{G} grid, {N} drones, {E} envs/GPU, "
-                                   f"step + fused obs(K={K})",
+                                   f"step + fused obs(K={K}) + the drl_refill share",
                        "grid": G, "n_drones": N, "num_envs_per_gpu": E, "num_envs_total": E * world,
                        "obs_k": K, "obs_stores": "streaming" if args.obs_stream else "cached",
-                       "parallelism": f"env-shard x{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS,
-                         "traffic": traffic,
-                         "kernel": "drl_step_kernel", "avg_launch_us": launch_s * 1e6,
-                         "algorithmic_read_bytes_per_env_step": R,
-                         "algorithmic_write_bytes_per_env_step": Wb,
-                         "achieved_read_plus_write": achieved_rw,
-                         "frac_read_plus_write": achieved_rw / PEAK_HBM_GBS,
-                         "frac_ceiling": R / (R + Wb),
-                         "note": "frac counts SURVEY.md §8 D3's read bytes R only: moving all R + W "
-                                 "algorithmic bytes at the HBM peak would score frac_ceiling = R / (R + W). W counts "
-                                 "a full ground write-back but the kernel writes only the changed cells, so the "
-                                 "read+write figure can exceed the peak at large grids (C5). Measured HBM bytes "
-                                 "per launch: traffic",
-                         "traffic_detail": traffic_src},
-            "refill": refill,
-            ("cached_obs" if args.obs_stream else "streaming_obs"): cached,
+                       "parallelism": f"env-shard x{world}",
+                       "setup": f"reset(seed=0), then {main_res['refill']['every']} pre-roll steps (one refill "
+                                "cycle: steady-state candidate rings) before the warm-up"},
+            "wall_ms_per_step": main_res["wall_ms_per_step"],
+            "roofline": roofline(E, R, Wb, main_res["launch_s"], main_res["refill"], traffic_of(args.config)),
+            "refill": main_res["refill"],
+            ("cached_obs" if args.obs_stream else "streaming_obs"): other,
+            "c5": c5,
             "cpu_baseline": cpu,
             "resets_per_s": resets_per_s,
             "dqn_consumer": dqn,

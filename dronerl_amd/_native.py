@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # DRL_LIB: an alternative build of the same library (tools/variants.py A/B runs)
 LIB_PATH = os.environ.get("DRL_LIB") or os.path.join(_HERE, "libdronerl.so")
 
-DRL_ABI_VERSION = 4  # include/dronerl.h
+DRL_ABI_VERSION = 5  # include/dronerl.h
 DRL_MT_WORDS = 1408  # per-env RNG row: two MT blocks + the respawn-candidate ring
 DRL_CAND_SLOTS = 128
 DRL_MAX_DRONES = 64
@@ -22,6 +22,7 @@ DRL_MAX_RADIUS = 8
 DRL_ERR_BAD_ACTION = 1
 DRL_ERR_NO_FREE_CELL = 2
 DRL_ERR_BAD_STATE = 4
+DRL_ERR_QNET_RANGE = 8  # drl_qnet_act (f32): an operand outside fp16's split range
 DRL_STEP_OBS_STREAM = 1  # drl_step_ex flag: streaming (non-temporal) observation stores
 DRL_STEP_REFILL = 2      # drl_step_ex flag: top up the respawn-candidate rings after the step
 

@@ -93,9 +93,15 @@ int step_group_lanes(int n_drones, int gstride, int cells, int window) {
 // in the step (slower, same results), but fewer, fuller refills win overall
 // (profiles/r02_refill_cadence/: C3 22.1-22.2 -> 21.7-22.0 us/step from 25
 // to 32, C5 154.8-155.3 -> 151.5 from 11 to 32).  DRL_REFILL_EVERY overrides
-// it (A/B runs).
+// it (A/B runs) with a positive step count; anything else is refused (0
+// would read as "never" in the Python env's refill_every), and
+// the cadence stays >= 1 for drl_rollout's narrow-group modulo.
 int refill_cadence(int n_drones) {
-    if (const char* v = getenv("DRL_REFILL_EVERY")) return atoi(v) > 0 ? atoi(v) : 1;
+    if (const char* v = getenv("DRL_REFILL_EVERY")) {
+        char* end = nullptr;
+        const long r = strtol(v, &end, 10);
+        return (end != v && *end == 0 && r > 0 && r <= 1 << 20) ? (int)r : -1;
+    }
     const int r = (int)(DRL_CAND_SLOTS / (1.53 + 0.06 * n_drones));
     return r < 1 ? 1 : (r > 32 ? 32 : r);
 }
@@ -134,6 +140,7 @@ int validate(const drl_params* p, drl_layout* L) {
         if (L->step_lds_bytes > kLdsMax) return fail("side %d needs %d B of LDS per block", p->side, L->step_lds_bytes);
         L->cand_slots = DRL_CAND_SLOTS;
         L->refill_every = refill_cadence(N);
+        if (L->refill_every < 1) return fail("DRL_REFILL_EVERY must be a positive integer step count");
     }
     return 0;
 }

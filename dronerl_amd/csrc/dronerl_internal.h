@@ -245,6 +245,7 @@ struct QnetArgs {
     float* q;
     int synth_n;                    // > 1: also write drl_synth_actions' columns 1..synth_n-1
     uint64_t synth_seed, synth_step;
+    int32_t* err;                   // F32: DRL_ERR_QNET_RANGE when an operand leaves fp16's range (nullable)
 };
 
 struct ReplayArgs {

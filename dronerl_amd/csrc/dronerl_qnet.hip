@@ -312,12 +312,16 @@ __device__ __forceinline__ f16x8 as_f16x8(const uint4 v) {
     return f;
 }
 
-__device__ __forceinline__ void split_f16(const float (&v)[8], f16x8& hi, f16x8& lo) {
+// `bad` collects operands outside fp16's range (|v| >= 65520 rounds hi to
+// inf; NaN stays NaN): the split would turn them into NaN Q values, so the
+// kernel flags DRL_ERR_QNET_RANGE instead of failing silently.
+__device__ __forceinline__ void split_f16(const float (&v)[8], f16x8& hi, f16x8& lo, bool& bad) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const _Float16 h = (_Float16)v[j];
         hi[j] = h;
         lo[j] = (_Float16)((v[j] - (float)h) * 2048.0f);
+        bad |= !(__builtin_fabsf(v[j]) < 65520.0f);
     }
 }
 
@@ -381,6 +385,7 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_f32_kernel(QnetArg
                                              (__attribute__((address_space(3))) void*)(wl + v0), 16, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    bool bad = false;  // an operand outside fp16's range (split_f16)
     const float* bias = LO0 ? reinterpret_cast<const float*>(a.packed + a.bias_vec)
                             : reinterpret_cast<const float*>(wl + a.frag_total);
     const uint4* W0 = wl + a.frag_off[0];
@@ -413,7 +418,7 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_f32_kernel(QnetArg
                 f16x8 bh[TP], bl[TP];
 #pragma unroll
                 for (int h = 0; h < TP; ++h) {
-                    split_f16(raw[h][i], bh[h], bl[h]);
+                    split_f16(raw[h][i], bh[h], bl[h], bad);
                     if constexpr (MODE == 0) load_slice(row[h], t + QN_RING, raw[h][i]);
                     else if constexpr (MODE == 1) load_slice(nrow[h], t + QN_RING - KP, raw[h][i]);
                 }
@@ -455,7 +460,7 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_f32_kernel(QnetArg
                             const int m = 2 * s2 + (j >> 2), i = j & 3;
                             v[j] = fmaxf((acc[h][m][i] + acl[h][m][i] * kLo) + bprev[16 * m + 4 * g + i], 0.0f);
                         }
-                        split_f16(v, ah[h][s2], al[h][s2]);
+                        split_f16(v, ah[h][s2], al[h][s2], bad);
                     }
                 }
             }
@@ -513,6 +518,7 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_f32_kernel(QnetArg
             }
         }
     }
+    if (__ballot(bad) && lane == 0 && a.err) atomicOr(a.err, DRL_ERR_QNET_RANGE);
     if (a.synth_n > 1) {  // as in drl_qnet_act_kernel
         const uint32_t nd = (uint32_t)a.synth_n - 1u;
         const uint32_t per = (uint32_t)(TP * 16) * nd;

@@ -158,7 +158,7 @@ int drl_qnet_pack(const drl_qnet_desc* d, const float* const* d_weights, const f
 static int qnet_act_impl(const drl_qnet_desc* d, const void* d_packed, const float* d_obs, int64_t num_envs,
                          int64_t obs_stride, float epsilon, uint64_t seed, uint64_t step, int64_t env_offset,
                          int32_t* d_actions, int64_t action_stride, float* d_q, int synth_n, uint64_t synth_seed,
-                         uint64_t synth_step, hipStream_t stream) {
+                         uint64_t synth_step, int32_t* d_err, hipStream_t stream) {
     drl::QnetLayout L;
     if (qnet_layout(d, &L)) return -1;
     if (num_envs < 0) return fail("num_envs < 0");
@@ -201,24 +201,25 @@ static int qnet_act_impl(const drl_qnet_desc* d, const void* d_packed, const flo
     a.synth_n = synth_n;
     a.synth_seed = synth_seed;
     a.synth_step = synth_step;
+    a.err = d_err;
     hipError_t e = drl::launch_qnet_act(a, num_cus(), stream);
     return e == hipSuccess ? 0 : hip_fail(e, "drl_qnet_act launch");
 }
 
 int drl_qnet_act(const drl_qnet_desc* d, const void* d_packed, const float* d_obs, int64_t num_envs,
                  int64_t obs_stride, float epsilon, uint64_t seed, uint64_t step, int64_t env_offset,
-                 int32_t* d_actions, int64_t action_stride, float* d_q, hipStream_t stream) {
+                 int32_t* d_actions, int64_t action_stride, float* d_q, int32_t* d_err, hipStream_t stream) {
     return qnet_act_impl(d, d_packed, d_obs, num_envs, obs_stride, epsilon, seed, step, env_offset, d_actions,
-                         action_stride, d_q, 0, 0, 0, stream);
+                         action_stride, d_q, 0, 0, 0, d_err, stream);
 }
 
 int drl_qnet_act_synth(const drl_qnet_desc* d, const void* d_packed, const float* d_obs, int64_t num_envs,
                        int64_t obs_stride, float epsilon, uint64_t seed, uint64_t step, int64_t env_offset,
                        int32_t* d_actions, int32_t n_drones, uint64_t synth_seed, uint64_t synth_step, float* d_q,
-                       hipStream_t stream) {
+                       int32_t* d_err, hipStream_t stream) {
     if (n_drones < 1 || n_drones > 255) return fail("n_drones must be in [1, 255]");
     return qnet_act_impl(d, d_packed, d_obs, num_envs, obs_stride, epsilon, seed, step, env_offset, d_actions,
-                         n_drones, d_q, n_drones, synth_seed, synth_step, stream);
+                         n_drones, d_q, n_drones, synth_seed, synth_step, d_err, stream);
 }
 
 int drl_replay_add(const drl_replay* r, int64_t cursor, int64_t n, const float* d_obs, int64_t obs_stride,

@@ -19,7 +19,7 @@ from typing import Optional, Sequence, Tuple
 
 import torch
 
-from ._native import DroneRLError, lib
+from ._native import DRL_ERR_QNET_RANGE, DroneRLError, lib
 
 NUM_ACTIONS = 5  # common/constants.py Action
 
@@ -50,8 +50,8 @@ def _bind(L):
     sig = {
         "drl_qnet_packed_bytes": [D, ctypes.POINTER(i64)],
         "drl_qnet_pack": [D, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp, _vp],
-        "drl_qnet_act": [D, _vp, _vp, i64, i64, f32, u64, u64, i64, _vp, i64, _vp, _vp],
-        "drl_qnet_act_synth": [D, _vp, _vp, i64, i64, f32, u64, u64, i64, _vp, i32, u64, u64, _vp, _vp],
+        "drl_qnet_act": [D, _vp, _vp, i64, i64, f32, u64, u64, i64, _vp, i64, _vp, _vp, _vp],
+        "drl_qnet_act_synth": [D, _vp, _vp, i64, i64, f32, u64, u64, i64, _vp, i32, u64, u64, _vp, _vp, _vp],
         "drl_replay_add": [ctypes.POINTER(DrlReplay), i64, i64, _vp, i64, _vp, i64, _vp, i64, _vp, i64, _vp, i64, _vp],
     }
     for name, args in sig.items():
@@ -109,6 +109,7 @@ class QNetwork:
         nb = ctypes.c_int64()
         _check(self.L, self.L.drl_qnet_packed_bytes(ctypes.byref(self.desc), ctypes.byref(nb)))
         self.packed = torch.empty(nb.value // 4, dtype=torch.int32, device=self.device)  # 16-B aligned
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)  # DRL_ERR_QNET_RANGE (f32 operand range)
         self.pack()
 
     def load(self, weights: Sequence[torch.Tensor], biases: Sequence[torch.Tensor]):
@@ -172,13 +173,26 @@ class QNetwork:
                 ctypes.byref(self.desc), _vp(self.packed.data_ptr()), _vp(flat.data_ptr()), E, flat.stride(0),
                 float(epsilon), seed & (2**64 - 1), step, env_offset, _vp(actions.data_ptr()), stride_a,
                 synth[0] & (2**64 - 1), synth[1], None if q_out is None else _vp(q_out.data_ptr()),
-                _stream(self.device)))
+                _vp(self.err.data_ptr()), _stream(self.device)))
             return actions
         _check(self.L, self.L.drl_qnet_act(ctypes.byref(self.desc), _vp(self.packed.data_ptr()), _vp(flat.data_ptr()),
                                            E, flat.stride(0), float(epsilon), seed & (2**64 - 1), step, env_offset,
                                            _vp(actions.data_ptr()), stride_a,
-                                           None if q_out is None else _vp(q_out.data_ptr()), _stream(self.device)))
+                                           None if q_out is None else _vp(q_out.data_ptr()), _vp(self.err.data_ptr()),
+                                           _stream(self.device)))
         return actions
+
+    def check_errors(self):
+        """Synchronise and raise if an f32 act met an operand outside fp16's
+        split range (|input or hidden activation| >= 65520, or NaN): its Q
+        values and greedy actions are then not valid (DRL_ERR_QNET_RANGE)."""
+        e = int(self.err.item())
+        if e:
+            self.err.zero_()
+            if e & DRL_ERR_QNET_RANGE:
+                raise DroneRLError("f32 act: an input or hidden activation is outside the fp16 split range "
+                                   "(|v| >= 65520 or NaN); Q values are not valid")
+            raise DroneRLError(f"qnet error bits {e:#x}")
 
 
 @dataclass

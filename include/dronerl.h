@@ -46,7 +46,7 @@ extern "C" {
 
 typedef struct ihipStream_t* hipStream_t;
 
-#define DRL_ABI_VERSION 4
+#define DRL_ABI_VERSION 5
 /* Per-env RNG row of `mt` (u32 words, 5376 B):
  *   [0, 624)     MT19937 block 0     the env's CPython stream lives in block
  *   [624, 1248)  MT19937 block 1     mt_index.par (the other block is scratch)
@@ -75,6 +75,8 @@ typedef struct ihipStream_t* hipStream_t;
 #define DRL_ERR_NO_FREE_CELL 2 /* respawn found no free cell (the reference loops forever) */
 #define DRL_ERR_BAD_STATE 4    /* drl_env_set_state: MT index outside [0, 624] (CPython setstate's ValueError);
                                   clamped to 624 */
+#define DRL_ERR_QNET_RANGE 8   /* drl_qnet_act (DRL_QNET_F32): an input or hidden activation at or beyond fp16's
+                                  range (|v| >= 65520) or NaN; that env's Q values are not valid */
 
 /* Env parameters: torch_impl DEFAULT_CONFIG (env.py:28-42) / jax DroneEnvParams
  * (jax env.py:11-26).  `side` is explicit; torch_impl derives it as
@@ -338,10 +340,10 @@ int drl_qnet_pack(const drl_qnet_desc* d, const float* const* d_weights, const f
  * for e < num_envs (first maximum on ties, like jnp.argmax).  obs f32 rows of
  * obs_stride floats (8-byte aligned).  u_e and the random action come from a
  * counter hash of (seed, step, env_offset + e).  d_q (nullable): Q f32
- * [num_envs][n_actions]. */
+ * [num_envs][n_actions].  d_err (nullable): OR-ed DRL_ERR_QNET_RANGE. */
 int drl_qnet_act(const drl_qnet_desc* d, const void* d_packed, const float* d_obs, int64_t num_envs,
                  int64_t obs_stride, float epsilon, uint64_t seed, uint64_t step, int64_t env_offset,
-                 int32_t* d_actions, int64_t action_stride, float* d_q, hipStream_t stream);
+                 int32_t* d_actions, int64_t action_stride, float* d_q, int32_t* d_err, hipStream_t stream);
 /* drl_qnet_act for column 0 of d_actions [num_envs][n_drones] (contiguous
  * rows), fused with drl_synth_actions(synth_seed, synth_step, env_offset,
  * num_envs, n_drones) for columns 1..n_drones-1: one launch for the
@@ -350,7 +352,7 @@ int drl_qnet_act(const drl_qnet_desc* d, const void* d_packed, const float* d_ob
 int drl_qnet_act_synth(const drl_qnet_desc* d, const void* d_packed, const float* d_obs, int64_t num_envs,
                        int64_t obs_stride, float epsilon, uint64_t seed, uint64_t step, int64_t env_offset,
                        int32_t* d_actions, int32_t n_drones, uint64_t synth_seed, uint64_t synth_step, float* d_q,
-                       hipStream_t stream);
+                       int32_t* d_err, hipStream_t stream);
 
 /* Replay ring buffer storage (device, caller-owned): obs/next_obs f32
  * [capacity][obs_floats], actions i32, rewards f32, dones u8 [capacity]. */

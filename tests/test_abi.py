@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol():
     exported = set(re.findall(r"\s(drl_\w+)$", out, re.M))
     missing = [f for f in fns if f not in exported]
     assert not missing, missing
-    assert lib().drl_abi_version() == 4
+    assert lib().drl_abi_version() == 5
 
 
 def test_library_is_gfx950_code_object():
@@ -121,3 +121,17 @@ def test_replay_add_rejects_short_rows():
     r0 = DrlReplay(16, 294, 8, 8, 8, 8, 8)
     assert L.drl_replay_add(ctypes.byref(r0), 0, 4, vp(8), 294, vp(8), 294, vp(8), 0, vp(8), 1, vp(8), 1, None) != 0
     assert b"strides" in L.drl_last_error()
+
+
+@pytest.mark.parametrize("val,ok", [("0", False), ("-3", False), ("x", False), ("", False), ("7", True)])
+def test_refill_cadence_override_must_be_positive(monkeypatch, val, ok):
+    """DRL_REFILL_EVERY=0 used to mean "after every step" in C but
+    "never" for the Python env's refill_every; non-positive or non-numeric
+    overrides are now refused."""
+    monkeypatch.setenv("DRL_REFILL_EVERY", val)
+    p = EnvParams(n_drones=8, grid_size=16)
+    if ok:
+        assert p.layout().refill_every == 7
+    else:
+        with pytest.raises(ValueError, match="DRL_REFILL_EVERY"):
+            p.layout()

@@ -57,7 +57,8 @@ def test_cpu_baseline_record():
 def test_cli_help_lists_contract_flags():
     out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--help"], capture_output=True,
                          text=True, timeout=120, check=True).stdout
-    for flag in ("--gpus", "--steps", "--warmup", "--config", "--cached-steps", "--no-pmc-traffic"):
+    for flag in ("--gpus", "--steps", "--warmup", "--config", "--cached-steps", "--no-pmc-traffic", "--c5-envs",
+                 "--loop-precision"):
         assert flag in out
 
 
@@ -74,4 +75,47 @@ def test_no_nested_profiler_inside_a_rocprofv3_run(monkeypatch):
     monkeypatch.delenv("ROCPROF_OUTPUT_PATH")
     monkeypatch.setenv("LD_PRELOAD", "/opt/rocm/lib/librocprofiler-sdk-tool.so")
     assert bench.under_profiler()
-    assert bench.measure_traffic(None) is None  # returns before reading any argument
+    assert bench.measure_traffic(None, ["c3"]) is None  # returns before reading any argument
+
+
+@pytest.mark.parametrize("pre,warmup,steps,every", [(32, 5, 20, 32), (32, 50, 1000, 32), (32, 50, 200, 32),
+                                                    (25, 5, 20, 25), (32, 0, 64, 32), (1, 0, 7, 1)])
+def test_refill_share_charged_at_any_step_count(pre, warmup, steps, every):
+    """the timed region carries exactly steps/every refills
+    (the ones inside it plus a prorated share), so the driver's 20-step run
+    is charged like a 1000-step one."""
+    inside, charge = bench.refill_plan(pre, warmup, steps, every)
+    first = pre + warmup
+    assert inside == [s for s in range(first, first + steps) if (s + 1) % every == 0]
+    assert len(inside) + charge == pytest.approx(steps / every)
+    assert -1.0 < charge < 1.0
+    if not inside:
+        assert charge > 0  # e.g. --steps 20 --warmup 5: no refill inside, 0.625 of one charged
+
+
+def test_driver_run_charges_a_refill():
+    inside, charge = bench.refill_plan(32, 5, 20, 32)
+    assert inside == [] and charge == pytest.approx(20 / 32)
+
+
+def test_roofline_fractions_stay_below_one():
+    """every reported fraction is a share of the HBM peak
+    that the kernel can reach: R-only, measured traffic / time (no read+write
+    figure whose W counts a ground write-back the kernel never does)."""
+    E, R, Wb = 131072, 4256, 5560
+    refill = {"every": 32, "per_step_us": 5.0}
+    traffic = {"drl_step_kernel": {"bytes_per_launch": 810e6, "read_bytes_per_launch": 600e6,
+                                   "write_bytes_per_launch": 210e6},
+               "drl_refill_kernel": {"bytes_per_launch": 400e6, "read_bytes_per_env": 2000.0,
+                                     "write_bytes_per_env": 1000.0}, "source": "test", "envs": E}
+    rl = bench.roofline(E, R, Wb, 143.6e-6, refill, traffic)
+
+    def fracs(d):
+        for k, v in d.items():
+            if isinstance(v, dict):
+                yield from fracs(v)
+            elif k.startswith("frac"):
+                yield k, v
+    found = dict(fracs(rl))
+    assert "frac_read_plus_write" not in found and "frac_measured" in found
+    assert all(0.0 < v <= 1.0 for v in found.values()), found

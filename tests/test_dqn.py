@@ -167,6 +167,35 @@ def test_qnet_f32_weight_range_checked():
 
 
 @gpu
+@pytest.mark.parametrize("where", ["input", "hidden", "nan", "ok"])
+def test_qnet_f32_activation_range_flagged(where):
+    """an input or hidden activation beyond fp16's split range
+    (|v| >= 65520) would become inf/NaN in the hi/lo split; the kernel flags
+    DRL_ERR_QNET_RANGE instead of returning an arbitrary action silently."""
+    from dronerl_amd._native import DroneRLError
+    from dronerl_amd.dqn import QNetwork
+    E = 100
+    obs, _ = _obs_batch(E)
+    net = QNetwork(obs.shape[1], (64, 32), generator=torch.Generator().manual_seed(5), precision="f32")
+    x = obs.clone()
+    if where == "input":
+        x[17, 3] = 1.0e5
+    elif where == "nan":
+        x[42, 0] = float("nan")
+    elif where == "hidden":  # weights in range, activations of layer 0 beyond it
+        w = [t.clone() for t in net.weights]
+        w[0][:, :] = 3000.0
+        net.load(w, net.biases)
+    net.act(x, epsilon=0.0)
+    if where == "ok":
+        net.check_errors()
+        return
+    with pytest.raises(DroneRLError, match="fp16 split range"):
+        net.check_errors()
+    net.check_errors()  # cleared
+
+
+@gpu
 def test_qnet_exploration_stream_and_column_write():
     from dronerl_amd.dqn import QNetwork
     E, N = 777, 8

@@ -113,7 +113,8 @@ def test_bench_two_ranks_gloo_whole_job_json():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
            "--gpus", "2", "--steps", "20", "--warmup", "5", "--envs", "4096", "--no-cpu-baseline", "--no-dqn",
-           "--no-reset-bench", "--rollout-chunk", "0", "--loop-segments", "0", "--cached-steps", "10"]
+           "--no-reset-bench", "--rollout-chunk", "0", "--loop-segments", "0", "--cached-steps", "10",
+           "--c5-envs", "1024"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -125,3 +126,7 @@ def test_bench_two_ranks_gloo_whole_job_json():
     # value = every rank's env-steps over the slowest rank's wall time
     assert d["value"] == pytest.approx(2 * 4096 * 20 / (d["ms_per_step"] * 20 / 1e3), rel=1e-6)
     assert d["streaming_obs"]["value"] > 0 and d["config"]["obs_stores"] == "cached"
+    # the north-star sub-record: whole-job envs over both ranks, the same timing rule
+    c5 = d["c5"]
+    assert c5["config"]["num_envs_total"] == 2 * 1024 and c5["steps"] >= 200 and c5["n_gpus"] == 2
+    assert c5["value"] == pytest.approx(2 * 1024 * c5["steps"] / (c5["ms_per_step"] * c5["steps"] / 1e3), rel=1e-6)

@@ -21,14 +21,30 @@ import shutil
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def per_wave(src: str):
+    """Mean counter values per dispatch, and per wave (SQ_WAVES), over every
+    pass under src/pmc*/ (tools/gpu.sh pmc)."""
+    agg = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(src, "pmc*", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    m = {k: sum(v) / len(v) for k, v in agg.items()}
+    w = m.get("SQ_WAVES", 1.0)
+    for k in sorted(m):
+        print(f"{k:24s} {m[k]:16.1f}   per-wave {m[k] / w:10.1f}")
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--per-wave", default="", help="print per-wave PMC means of a tools/gpu.sh pmc directory")
     ap.add_argument("--src", default=os.path.join(REPO, "gpurun_out", "prof"))
-    ap.add_argument("--tag", required=True)
+    ap.add_argument("--tag", default="")
     ap.add_argument("--config", default="c3")
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--kernel", default="drl_step_kernel")
     args = ap.parse_args()
+    if args.per_wave:
+        return per_wave(args.per_wave)
     out = os.path.join(REPO, "profiles", args.tag)
     os.makedirs(out, exist_ok=True)
     ks = os.path.join(args.src, "trace", "run_kernel_stats.csv")
