@@ -190,7 +190,7 @@ def measure_traffic(args, names):
         if "drl_step_kernel" in rec:
             rec["envs"] = g["envs"]
             rec["source"] = ("measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate child "
-                             "runs of this bench's step loop, 20 steps after a refill-cycle pre-roll), traffic = "
+                             "runs of this bench's step loop, 20 steps after a two-refill-cycle pre-roll), traffic = "
                              "2*FETCH_SIZE + WRITE_SIZE per launch")
             out[name] = rec
     return out or None
@@ -599,8 +599,12 @@ class StepRunner:
 
     def run(self, steps: int, warmup: int, world: int, pre: int = 0):
         """pre + warmup untimed steps, then `steps` timed ones bracketed by a
-        barrier + synchronize on both sides, max over ranks.  The value
-        charges the timed region steps/every refills (refill_plan)."""
+        barrier + synchronize on both sides, max over ranks.  The region's
+        time is the HIP-event time on the launch stream from its first launch
+        to its last (the host's wall clock of the same region, which adds the
+        queue's start and drain latency, ~1 us per step over 20 steps and
+        0.02 over 1000, is reported as wall_ms_per_step).  The value charges
+        the timed region steps/every refills (refill_plan)."""
         for _ in range(pre + warmup):
             self.step(False)
         torch.cuda.synchronize()
@@ -623,9 +627,13 @@ class StepRunner:
         plan, charge = refill_plan(0, self.s - steps, steps, self.every)
         assert len(plan) == len(inside), (plan, len(inside))
         ref_in_ms = sum(a.elapsed_time(b) for a, b, _ in inside)
+        # the refill's average launch: every one measured except the first
+        # after the reset (the pre-roll's, on a cold machine)
         all_ms = [a.elapsed_time(b) for a, b, _ in self.refill_ev]
-        refill_avg_s = max_over_ranks(sum(all_ms) / len(all_ms) / 1e3 if all_ms else 0.0, world)
-        charged = wall_max + charge * refill_avg_s
+        use = all_ms[1:] if len(all_ms) > 1 else all_ms
+        refill_avg_s = max_over_ranks(sum(use) / len(use) / 1e3 if use else 0.0, world)
+        region_s = max_over_ranks(ev0.elapsed_time(ev1) / 1e3, world)
+        charged = region_s + charge * refill_avg_s
         launch_s = (ev0.elapsed_time(ev1) - ref_in_ms) / 1e3 / steps  # drl_step kernel, on this stream
         return {"value": self.E * world * steps / charged, "ms_per_step": charged / steps * 1e3,
                 "wall_ms_per_step": wall_max / steps * 1e3, "launch_s": launch_s,
@@ -636,9 +644,9 @@ class StepRunner:
                            "prorated_launches": charge,
                            "note": "env.step()'s cadence (a refill after every `every`-th step, counted from the "
                                    "pre-roll); the timed region is charged exactly steps/every refills: the ones "
-                                   "inside it (wall clock) plus prorated_launches x avg_launch_us (HIP events, "
-                                   "max over ranks), so value and ms_per_step carry the refill share at any step "
-                                   "count"}}
+                                   "inside it plus prorated_launches x avg_launch_us (HIP events; the pre-roll's "
+                                   "first refill excluded), so value and ms_per_step carry the refill share at any "
+                                   "step count"}}
 
 
 def roofline(E, R, Wb, launch_s, refill, traffic):
@@ -700,7 +708,7 @@ def pmc_child(args):
             K = args.obs_k
         stream = args.obs_stream or (env.default_obs_stream and not args.obs_cached)
         run = StepRunner(env, K, 8, stream)
-        run.run(args.steps, args.warmup, 1, pre=env.refill_every)
+        run.run(args.steps, args.warmup, 1, pre=2 * env.refill_every)
         P = env.layout.step_group_lanes
         grids[name] = {"envs": E, "step_grid": -(-E // (64 // P)) * 64, "refill_grid": -(-E // 4) * 64}
         del run, env
@@ -773,8 +781,8 @@ def main():
 
     # ---- the headline: setup rolls one refill cycle (steady-state rings),
     # then W warm-up and K timed steps
-    runner = StepRunner(env, K, args.warmup + args.steps + env.refill_every, args.obs_stream)
-    main_res = runner.run(args.steps, args.warmup, world, pre=env.refill_every)
+    runner = StepRunner(env, K, args.warmup + args.steps + 2 * env.refill_every, args.obs_stream)
+    main_res = runner.run(args.steps, args.warmup, world, pre=2 * env.refill_every)
     actions, rewards, dones, obs, stream = runner.actions, runner.rewards, runner.dones, runner.obs, runner.stream
 
     def traffic_of(name):
@@ -847,8 +855,8 @@ def main():
         env5, G5, N5, E5, K5 = make_env("c5", args.c5_envs, rank, dev)
         st5 = env5.default_obs_stream
         steps5 = max(args.c5_steps, 200)
-        run5 = StepRunner(env5, K5, steps5 + 20 + env5.refill_every, st5)
-        r5 = run5.run(steps5, 20, world, pre=env5.refill_every)
+        run5 = StepRunner(env5, K5, steps5 + 20 + 2 * env5.refill_every, st5)
+        r5 = run5.run(steps5, 20, world, pre=2 * env5.refill_every)
         R5, W5 = algorithmic_bytes(G5, N5, K5, env5.layout.obs_window)
         c5 = {"value": r5["value"], "unit": "env-steps/s", "n_gpus": world, "steps": steps5, "warmup": 20,
               "ms_per_step": r5["ms_per_step"], "wall_ms_per_step": r5["wall_ms_per_step"],
@@ -887,8 +895,8 @@ def main():
                        "grid": G, "n_drones": N, "num_envs_per_gpu": E, "num_envs_total": E * world,
                        "obs_k": K, "obs_stores": "streaming" if args.obs_stream else "cached",
                        "parallelism": f"env-shard x{world}",
-                       "setup": f"reset(seed=0), then {main_res['refill']['every']} pre-roll steps (one refill "
-                                "cycle: steady-state candidate rings) before the warm-up"},
+                       "setup": f"reset(seed=0), then {2 * main_res['refill']['every']} pre-roll steps (two refill "
+                                "cycles: steady-state candidate rings) before the warm-up"},
             "wall_ms_per_step": main_res["wall_ms_per_step"],
             "roofline": roofline(E, R, Wb, main_res["launch_s"], main_res["refill"], traffic_of(args.config)),
             "refill": main_res["refill"],

@@ -13,9 +13,11 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # DRL_LIB: an alternative build of the same library (tools/variants.py A/B runs)
 LIB_PATH = os.environ.get("DRL_LIB") or os.path.join(_HERE, "libdronerl.so")
 
-DRL_ABI_VERSION = 5  # include/dronerl.h
-DRL_MT_WORDS = 1408  # per-env RNG row: two MT blocks + the respawn-candidate ring
-DRL_CAND_SLOTS = 128
+DRL_ABI_VERSION = 6  # include/dronerl.h
+DRL_MT_WORDS = 1776  # per-env RNG row: two MT blocks + the respawn-candidate ring
+DRL_MT_RING = 1248
+DRL_MT_RING_END = 1760
+DRL_CAND_SLOTS = 512
 DRL_MAX_DRONES = 64
 DRL_MAX_SIDE = 128
 DRL_MAX_RADIUS = 8

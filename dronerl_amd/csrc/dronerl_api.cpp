@@ -84,25 +84,28 @@ int step_group_lanes(int n_drones, int gstride, int cells, int window) {
     return P;
 }
 
-// Steps between refills.  Ring entries used per env-step, measured at the
-// benchmark shapes with random actions (tools/ring_usage.py): mean 2.06 /
-// 2.56 / 3.44 and at most 17 at N = 8 / 16 / 32; over 16 steps at most 71 /
-// 71 / 93, i.e. about 1.53 + 0.06 N.  A refill every CAND_Q / (1.53 + 0.06 N)
-// steps (at most 32) fills the ring about as fast as the mean env drains it:
-// 32 at C3, C4 and C5.  The worst envs then run dry and draw from the stream
-// in the step (slower, same results), but fewer, fuller refills win overall
-// (profiles/r02_refill_cadence/: C3 22.1-22.2 -> 21.7-22.0 us/step from 25
-// to 32, C5 154.8-155.3 -> 151.5 from 11 to 32).  DRL_REFILL_EVERY overrides
-// it (A/B runs) with a positive step count; anything else is refused (0
-// would read as "never" in the Python env's refill_every), and
-// the cadence stays >= 1 for drl_rollout's narrow-group modulo.
-int refill_cadence(int n_drones) {
+// Steps between refills.  A refill converts a whole MT block into ring
+// entries once an env's stream has moved into the block the ring ends in, so
+// the ring then holds that block's remaining entries: 312 * side / 2^kbits
+// pairs per block (_randbelow's acceptance; 156 at power-of-two sides).  Ring
+// entries used per env-step, measured at the benchmark shapes with random
+// actions (tools/ring_usage.py): mean 2.06 / 2.56 / 3.44 and at most 17 at N =
+// 8 / 16 / 32, i.e. about 1.53 + 0.06 N, and up to ~2.2x the mean over 16
+// steps.  A refill every half block's worth of mean use (at most 32 steps)
+// keeps the heaviest envs off the dry-ring path: 32 at C3 and C4, 22 at C5.
+// The bytes per step do not depend on the cadence (each block is converted
+// once); only the launch count and the dry-ring risk do.  DRL_REFILL_EVERY
+// overrides it (A/B runs) with a positive step count; anything else is
+// refused (0 would read as "never" in the Python env's refill_every, ADVICE
+// r2), and the cadence stays >= 1 for drl_rollout's narrow-group modulo.
+int refill_cadence(int n_drones, int side) {
     if (const char* v = getenv("DRL_REFILL_EVERY")) {
         char* end = nullptr;
         const long r = strtol(v, &end, 10);
         return (end != v && *end == 0 && r > 0 && r <= 1 << 20) ? (int)r : -1;
     }
-    const int r = (int)(DRL_CAND_SLOTS / (1.53 + 0.06 * n_drones));
+    const double per_block = (DRL_MT_BLOCK1 / 2.0) * side / (double)(1 << bit_length((uint32_t)side));
+    const int r = (int)(0.5 * per_block / (1.53 + 0.06 * n_drones));
     return r < 1 ? 1 : (r > 32 ? 32 : r);
 }
 
@@ -139,7 +142,7 @@ int validate(const drl_params* p, drl_layout* L) {
                            env_lds(L->ground_stride, GG, N, 1, L->obs_window, L->step_group_lanes), true);
         if (L->step_lds_bytes > kLdsMax) return fail("side %d needs %d B of LDS per block", p->side, L->step_lds_bytes);
         L->cand_slots = DRL_CAND_SLOTS;
-        L->refill_every = refill_cadence(N);
+        L->refill_every = refill_cadence(N, p->side);
         if (L->refill_every < 1) return fail("DRL_REFILL_EVERY must be a positive integer step count");
     }
     return 0;

@@ -14,15 +14,18 @@ constexpr int MT_ALT = DRL_MT_BLOCK1;  // word offset of MT block 1 in an env's 
 constexpr int MT_RING = DRL_MT_RING;   // word offset of the respawn-candidate ring
 constexpr int CAND_Q = DRL_CAND_SLOTS; // ring entries (power of two)
 constexpr int MT_RING_END = DRL_MT_RING_END;  // word: stream position after the ring's last entry
-static_assert((CAND_Q & (CAND_Q - 1)) == 0 && CAND_Q <= 128, "ring size");
+static_assert((CAND_Q & (CAND_Q - 1)) == 0 && CAND_Q <= 512, "ring size");
+static_assert(MT_RING_END < MT_WORDS && MT_RING + CAND_Q <= MT_RING_END && MT_WORDS % 16 == 0, "MT row layout");
 
-// mt_index word (include/dronerl.h): index | par << 10 | head << 16 | count << 24
+// mt_index word (include/dronerl.h): index | par << 10 | head << 11 | count << 20
 __host__ __device__ constexpr int mi_idx(uint32_t w) { return (int)(w & 0x3ffu); }
 __host__ __device__ constexpr int mi_par(uint32_t w) { return (int)((w >> 10) & 1u); }
-__host__ __device__ constexpr int mi_head(uint32_t w) { return (int)((w >> 16) & (uint32_t)(CAND_Q - 1)); }
-__host__ __device__ constexpr int mi_cnt(uint32_t w) { return (int)(w >> 24) < CAND_Q ? (int)(w >> 24) : CAND_Q; }
+__host__ __device__ constexpr int mi_head(uint32_t w) { return (int)((w >> 11) & (uint32_t)(CAND_Q - 1)); }
+__host__ __device__ constexpr int mi_cnt(uint32_t w) {
+    return (int)((w >> 20) & 0x3ffu) < CAND_Q ? (int)((w >> 20) & 0x3ffu) : CAND_Q;
+}
 __host__ __device__ constexpr uint32_t mi_pack(int idx, int par, int head, int cnt) {
-    return (uint32_t)idx | ((uint32_t)par << 10) | ((uint32_t)head << 16) | ((uint32_t)cnt << 24);
+    return (uint32_t)idx | ((uint32_t)par << 10) | ((uint32_t)head << 11) | ((uint32_t)cnt << 20);
 }
 // candidate ring entry: cell | MT index after the pair << 16 | that index's block << 26
 __host__ __device__ constexpr int ce_cell(uint32_t e) { return (int)(e & 0x3fffu); }

@@ -1914,233 +1914,106 @@ __global__ void drl_mt_set_kernel(uint32_t* __restrict__ mt, uint32_t* __restric
 }
 
 // ---------------------------------------------------------------- refill ---
-// drl_refill: top up each env's respawn-candidate ring (include/dronerl.h).
-// The candidates are the (y, x) pairs of consecutive accepted randint(0,
-// side-1) draws (_randbelow: the top kbits bits of a tempered word, kept if <
-// side; env.py:226-233 draws y then x), in stream order, starting at the end
-// of the ring's last entry (or at the stream position when it is empty).
-// They depend on the stream alone, so they can be drawn ahead of the steps
-// that consume them.
+// drl_refill: extend each env's respawn-candidate ring (include/dronerl.h)
+// through the end of the MT block after the stream's, converting that block
+// while its words are in registers.  The candidates are the (y, x) pairs of
+// consecutive accepted randint(0, side-1) draws (_randbelow: the top kbits
+// bits of a tempered word, kept if < side; env.py:226-233 draws y then x), in
+// stream order from the end of the ring's last entry (or from the stream
+// position when it is empty).  They depend on the stream alone, so they can be
+// drawn ahead of the steps that consume them.
 //
-// Layout: a wave serves kRefillEnvs envs, one after another, lane l taking
-// the l-th word of a 64-word pass of the env's stream: acceptance is one
-// ballot, a draw's accepted rank one mbcnt, and its pair partner comes back
-// through an LDS slot indexed by rank.  Every load of a pass (the 64 words of
-// each of the wave's envs) is issued before any is used, so a pass costs one
-// round trip; so does the first one (the mt_index words and the whole rings,
-// for the ring's last entry).  Per-env scalars live in lane e of a few VGPRs.
+// An env needs a conversion when its ring does not reach past the stream's
+// block s (after a reset or drl_mt_set, and once its stream has moved on into
+// block s+1, whose entries the ring then still holds).  The conversion loads
+// block s (2.5 KB, one round trip), converts its words from the ring's end on,
+// twists it into block s+1 in registers, stores s+1 to the other block's words
+// (the stream's own block is never written: get_state and every kernel that
+// draws from the stream directly see the state its index says), and converts
+// all of s+1.  Every MT word is thus read once, twisted once and written once
+// (~9 B per word with its entry), instead of being re-read by 64-word passes
+// after the twist that wrote it (round 2's refill: ~13 B per word).
 //
-// Positions are extended: [0, 624) is the block holding the stream (mt_index
-// par), [624, 1248) the next block, kept in the other block's words.  A pass
-// that reaches it first twists the stream's block into them (out of place:
-// the stream's own block stays as the state says), kTwistBatch envs at a time
-// with their blocks loaded together.
-#ifndef DRL_REFILL_ENVS
-#define DRL_REFILL_ENVS 4
-#endif
-#ifndef DRL_TWIST_BATCH
-#define DRL_TWIST_BATCH 2
-#endif
-constexpr int kRefillEnvs = DRL_REFILL_ENVS;
-constexpr int kTwistBatch = DRL_TWIST_BATCH;
+// One wave per env (its 624 words in x[10] as in twist_regs), four waves per
+// workgroup: waves never wait for one another, and envs that need nothing
+// leave after two scalar loads.  Within a 64-word chunk acceptance is one
+// ballot, a draw's accepted rank an mbcnt, and an x draw takes its y from the
+// previous accepted lane by ds_bpermute (the first of a chunk from the
+// pending y of the previous chunk).  A ring that would overflow stops at
+// DRL_CAND_SLOTS entries; its end then lies inside block s+1, whose words the
+// next conversion (after the stream moves into s+1) converts from registers.
+constexpr int kRefillWaves = 4;  // waves (envs) per workgroup
 
-__global__ void __launch_bounds__(64) drl_refill_kernel(RefillArgs a) {
-    constexpr int NE = kRefillEnvs;
-    __shared__ uint32_t rank_lds[65];  // a pass's accepted draws by accepted rank (+1: slot 0 = pending y)
+__global__ void __launch_bounds__(64 * kRefillWaves) drl_refill_kernel(RefillArgs a) {
     const int lane = threadIdx.x & 63;
-    const int64_t env0 = (int64_t)blockIdx.x * NE;
-    const int nenv_w = (int)min((int64_t)NE, a.E - env0);
-    if (nenv_w <= 0) return;
-    uint32_t* const wrow = a.mt + env0 * MT_WORDS;  // the wave's rows (scalar base)
+    const int64_t env = (int64_t)blockIdx.x * kRefillWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (env >= a.E) return;  // whole wave
+    uint32_t* const row = a.mt + env * MT_WORDS;
+    const uint32_t mw = a.mt_index[env];  // uniform: scalar loads
+    const uint32_t rend = row[MT_RING_END];
+    const int cnt = mi_cnt(mw), spar = mi_par(mw);
+    // where the unconverted stream starts, relative to the stream's block:
+    // the end of the ring's last entry (in the next block: + 624), or the
+    // stream position when the ring is empty
+    const int from = cnt > 0 ? min((int)(rend & 0x3ffu), MT_N) + ((int)((rend >> 10) & 1u) != spar ? MT_N : 0)
+                             : min(mi_idx(mw), MT_N);
+    if (from > MT_N) return;  // the ring reaches into the next block already
     const int G = a.side, shift = 32 - a.kbits;
-#ifdef DRL_STAMPS  // diagnostic build: per-wave clocks (tools/refill_stamps.py)
-    unsigned long long rs_t0, rs_t1, rs_a, rs_b, rs_tw = 0, rs_ps = 0, rs_ntw = 0, rs_np = 0;
-    DRL_SUBT(rs_t0);
-#endif
-    // ---- round trip 1: every env's mt_index word and ring-end position (lane e: env e)
-    uint32_t mi[NE];
-#pragma unroll
-    for (int e = 0; e < NE; ++e) mi[e] = a.mt_index[env0 + min(e, nenv_w - 1)];
-    const uint32_t gend = wrow[(uint32_t)min(lane, nenv_w - 1) * MT_WORDS + MT_RING_END];
-    // per-env state, env e in lane e: count, extended resume position (just
-    // after the ring's last entry, or the stream position for an empty ring),
-    // the last entry's end, pending y (-1: none), next block twisted
-    int v_cnt = CAND_Q, v_gext = 0, v_end = 0, v_y = -1, v_nval = 0, v_twisted = 0, v_par = 0;
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        if (lane == e) {
-            const int cnt = e < nenv_w ? mi_cnt(mi[e]) : CAND_Q;
-            v_cnt = cnt;
-            // gend: MT index | block << 10 after the last entry (absolute block, like an entry's)
-            const int tpar = mi_par(mi[e]);
-            const bool nxt = cnt > 0 && (int)((gend >> 10) & 1u) != tpar;  // in the next block: twisted already
-            v_gext = cnt > 0 ? min((int)(gend & 0x3ffu), MT_N) + (nxt ? MT_N : 0) : min(mi_idx(mi[e]), MT_N);
-            v_end = v_gext;
-            v_nval = nxt;
-            v_par = tpar;
-        }
-    }
-#ifdef DRL_STAMPS
-    DRL_SUBT(rs_t1);
-#endif
-    for (;;) {
-        const uint64_t work = __ballot(lane < NE && v_cnt < CAND_Q && v_gext < 2 * MT_N);
-        if (!work) break;
-#ifdef DRL_STAMPS
-        DRL_SUBT(rs_a);
-        ++rs_np;
-#endif
-        // ---- twists: envs whose pass reaches the next block.  The block is
-        // loaded, twisted in registers and stored to the other block's words
-        // without waiting for the stores: this pass takes its words from the
-        // registers, and a later pass that reads them from memory first
-        // waits (fence) for them.
-#ifdef DRL_DIAG_REFILL_NO_TWIST  // timing-only (wrong rings): as if every next block were twisted already
-        v_nval = 1;
-#endif
-        if (__ballot(lane < NE && (work >> lane) & 1ull && v_twisted)) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            wave_sync();
-        }
-        uint64_t tw = __ballot(lane < NE && v_cnt < CAND_Q && v_gext < 2 * MT_N && !v_nval && v_gext + 64 > MT_N);
-        v_nval |= (int)((tw >> lane) & 1ull);
-        v_twisted = (int)((tw >> lane) & 1ull);
-        // ---- one pass: 64 words of every env with work, all loads first
-        uint32_t w[NE];
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            const int gext = __builtin_amdgcn_readlane(v_gext, e);
-            const int par = mi_par(mi[e]);
-            const int p = gext + lane;
-            const uint32_t off = (uint32_t)e * MT_WORDS +
-                                 (p < MT_N ? (uint32_t)par * MT_ALT + (uint32_t)p
-                                           : (uint32_t)(1 - par) * MT_ALT + (uint32_t)min(p - MT_N, MT_N - 1));
-            // (the next block may have been written by this wave's previous pass: an L2 load)
-            w[e] = ((work >> e) & 1ull) && !((tw >> e) & 1ull) ? (gext + 64 > MT_N ? load_l2(wrow + off) : wrow[off])
-                                                                : 0u;
-        }
-#ifdef DRL_STAMPS
-        rs_ntw += __popcll(tw);
-#endif
-        while (tw) {
-            int te[kTwistBatch];
-            uint32_t x[kTwistBatch][10];
-#pragma unroll
-            for (int t = 0; t < kTwistBatch; ++t) {
-                te[t] = tw ? __ffsll((unsigned long long)tw) - 1 : -1;
-                if (tw) tw &= tw - 1ull;
-                if (te[t] >= 0) {
-                    // the stream's block: not written by this kernel, plain loads
-                    const uint32_t* src = wrow + (uint32_t)te[t] * MT_WORDS +
-                                          (uint32_t)__builtin_amdgcn_readlane(v_par, te[t]) * MT_ALT;
-#pragma unroll
-                    for (int c = 0; c < 10; ++c) x[t][c] = (64 * c + lane < MT_N) ? src[64 * c + lane] : 0u;
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < kTwistBatch; ++t) {
-                if (te[t] >= 0) {
-                    // the pass's words: positions g0 + lane, old block below 624, new block from 624 (its
-                    // first chunk: g0 <= 624 here)
-                    const int g0 = __builtin_amdgcn_readlane(v_gext, te[t]);
-                    const int c0 = g0 >> 6, sl = (g0 + lane) & 63;
-                    uint32_t xa = 0u, xb = 0u;
-#pragma unroll
-                    for (int c = 0; c < 10; ++c) {
-                        xa = c == c0 ? x[t][c] : xa;
-                        xb = c == c0 + 1 ? x[t][c] : xb;
-                    }
-                    const uint32_t oa = (uint32_t)__shfl((int)xa, sl), ob = (uint32_t)__shfl((int)xb, sl);
-                    const uint32_t wold = (g0 & 63) + lane < 64 ? oa : ob;
-                    twist_regs(x[t], lane);
-                    const uint32_t wnew = (uint32_t)__shfl((int)x[t][0], (g0 + lane - MT_N) & 63);  // new word p - 624
-                    const uint32_t wt = g0 + lane < MT_N ? wold : wnew;
-#pragma unroll
-                    for (int e = 0; e < NE; ++e) w[e] = te[t] == e ? wt : w[e];
-                    uint32_t* dst = wrow + (uint32_t)te[t] * MT_WORDS +
-                                    (uint32_t)(1 - __builtin_amdgcn_readlane(v_par, te[t])) * MT_ALT;
-#pragma unroll
-                    for (int c = 0; c < 10; ++c)
-                        if (64 * c + lane < MT_N) dst[64 * c + lane] = x[t][c];
-                }
-            }
-        }
-#ifdef DRL_STAMPS
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        DRL_SUBT(rs_b);
-        rs_tw += rs_b - rs_a;
-        rs_a = rs_b;
-#endif
-        // the pass's entries are kept in registers and stored after it: a
-        // store between two uses of w[] would make the next use wait for it
-        uint32_t ent[NE];
-        int eslot[NE];
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            eslot[e] = -1;
-            ent[e] = 0u;
-            if (!((work >> e) & 1ull)) continue;  // uniform
-            const int gext = __builtin_amdgcn_readlane(v_gext, e);
-            const int cnt = __builtin_amdgcn_readlane(v_cnt, e);
-            const int yv = __builtin_amdgcn_readlane(v_y, e);
-            const int head = mi_head(mi[e]), tpar = mi_par(mi[e]);
-            const int p = gext + lane;
-            const int r = p < 2 * MT_N ? (int)(temper(w[e]) >> shift) : G;
-            const bool acc = r < G;
-            const uint64_t M = __ballot(acc);
-            const int hy = yv >= 0 ? 1 : 0;
-            const int ar = hy + mbcnt64(M);  // accepted draws before this one (+ a pending y)
-            if (lane == 0 && hy) rank_lds[0] = (uint32_t)yv;
-            if (acc) rank_lds[ar] = (uint32_t)r;
-            wave_sync();
-            const int slot = cnt + (ar >> 1);
-            if (acc && (ar & 1) && slot < CAND_Q) {
-                const int ycell = (int)rank_lds[ar - 1];
-                const int end = p + 1;  // extended position after the pair's second draw
-                eslot[e] = (head + slot) & (CAND_Q - 1);
-                ent[e] = ce_pack(ycell * G + r, end <= MT_N ? end : end - MT_N, end <= MT_N ? tpar : 1 - tpar);
-            }
-            const int tot = hy + __popcll(M);
-            const int ny = (tot & 1) ? (int)rank_lds[tot - 1] : -1;
-            const int ncnt = min(cnt + (tot >> 1), CAND_Q);
-            // the end of the pass's last entry (the ring's end from now on)
-            const uint64_t L = __ballot(acc && (ar & 1) && slot == ncnt - 1);
-            const int lend = L ? gext + (__ffsll((unsigned long long)L) - 1) + 1 : -1;
-            wave_sync();
-            if (lane == e) {
-                v_cnt = ncnt;
-                v_y = ny;
-                v_gext = gext + 64;
-                v_end = lend >= 0 ? lend : v_end;
-            }
-        }
-#pragma unroll
-        for (int e = 0; e < NE; ++e)
-            if (eslot[e] >= 0) wrow[(uint32_t)e * MT_WORDS + MT_RING + (uint32_t)eslot[e]] = ent[e];
-#ifdef DRL_STAMPS
-        DRL_SUBT(rs_b);
-        rs_ps += rs_b - rs_a;
-#endif
-    }
-#ifdef DRL_STAMPS
+    const int room = CAND_Q - cnt;
+    const int ring0 = mi_head(mw) + cnt;  // slot of the first new entry (mod CAND_Q)
+    uint32_t x[10];
     {
-        unsigned long long t_end;
-        DRL_SUBT(t_end);
-        if (lane == 0 && g_stamps) {
-            unsigned long long* r = g_stamps + (int64_t)blockIdx.x * 16;
-            r[0] = rs_t0; r[1] = rs_t1 - rs_t0; r[2] = rs_tw; r[3] = rs_ps; r[4] = t_end - rs_t0; r[5] = rs_ntw;
-            r[6] = rs_np; r[7] = __builtin_amdgcn_s_memrealtime();
-        }
-    }
-#endif
-    // (a pending y at the end is dropped: the next refill re-reads it)
-    uint32_t wout = mi[0];
+        const uint32_t* src = row + (uint32_t)spar * MT_ALT;  // not written by this kernel: plain loads
 #pragma unroll
-    for (int e = 1; e < NE; ++e) wout = lane == e ? mi[e] : wout;
-    if (lane < nenv_w) {
-        a.mt_index[env0 + lane] = (wout & 0x00ffffffu) | ((uint32_t)v_cnt << 24);
-        wrow[(uint32_t)lane * MT_WORDS + MT_RING_END] =
-            v_end <= MT_N ? (uint32_t)v_end | ((uint32_t)v_par << 10) : (uint32_t)(v_end - MT_N) | ((uint32_t)(1 - v_par) << 10);
+        for (int c = 0; c < 10; ++c) x[c] = (64 * c + lane < MT_N) ? src[64 * c + lane] : 0u;
+    }
+    uint32_t* const ring = row + MT_RING;
+    const uint64_t lower = (1ull << lane) - 1ull;
+    int made = 0;             // entries written (uniform)
+    int carry = 0, yv = 0;    // a pending y (accepted draw without its x yet)
+    uint32_t end_word = rend; // ring-end word: MT index | block << 10 after the last entry
+    // convert chunk c of block bp (positions >= f0 only)
+    auto chunk = [&](uint32_t word, int c, int bp, int f0) __attribute__((always_inline)) {
+        const int pos = 64 * c + lane;
+        const bool valid = pos >= f0 && pos < MT_N;
+        const int r = (int)(temper(word) >> shift);
+        const bool acc = valid && r < G;
+        const uint64_t M = __ballot(acc);
+        const int k = mbcnt64(M);  // accepted draws of this chunk below this lane
+        const int ar = carry + k;  // accepted rank within the pairing
+        const uint64_t below = M & lower;
+        const int yl = below ? 63 - __clzll((long long)below) : lane;
+        const int ry = __shfl(r, yl);
+        const int yy = k > 0 ? ry : yv;
+        const int slot = made + (ar >> 1);
+        const bool put = acc && (ar & 1) && slot < room;
+        if (put) ring[(uint32_t)(ring0 + slot) & (uint32_t)(CAND_Q - 1)] = ce_pack(yy * G + r, pos + 1, bp);
+        const uint64_t P = __ballot(put);
+        if (P) end_word = (uint32_t)(64 * c + (63 - __clzll((long long)P)) + 1) | ((uint32_t)bp << 10);
+        const int tot = carry + __popcll(M);
+        if (M && (tot & 1)) yv = __builtin_amdgcn_readlane(r, 63 - __clzll((long long)M));
+        made = min(made + (tot >> 1), room);
+        carry = tot & 1;
+    };
+    // ---- the rest of the stream's block, from `from`
+#pragma unroll
+    for (int c = 0; c < 10; ++c)
+        if (64 * c + 64 > from && made < room) chunk(x[c], c, spar, from);
+    // ---- block s+1: twisted in registers, stored to the other block, converted
+    twist_regs(x, lane);
+    {
+        uint32_t* dst = row + (uint32_t)(1 - spar) * MT_ALT;
+#pragma unroll
+        for (int c = 0; c < 10; ++c)
+            if (64 * c + lane < MT_N) dst[64 * c + lane] = x[c];
+    }
+#pragma unroll
+    for (int c = 0; c < 10; ++c)
+        if (made < room) chunk(x[c], c, 1 - spar, 0);
+    // (a pending y at the end is dropped: the next conversion re-reads it)
+    if (lane == 0) {
+        a.mt_index[env] = mi_pack(mi_idx(mw), spar, mi_head(mw), cnt + made);
+        row[MT_RING_END] = end_word;
     }
 }
 
@@ -2261,8 +2134,8 @@ hipError_t launch_encode(uint32_t* drones, int64_t E, int N, const int32_t* orde
 }
 
 hipError_t launch_refill(const RefillArgs& a, hipStream_t s) {
-    const int64_t blocks = (a.E + kRefillEnvs - 1) / kRefillEnvs;
-    hipLaunchKernelGGL(drl_refill_kernel, dim3((unsigned)blocks), dim3(64), 0, s, a);
+    const int64_t blocks = (a.E + kRefillWaves - 1) / kRefillWaves;
+    hipLaunchKernelGGL(drl_refill_kernel, dim3((unsigned)blocks), dim3(64 * kRefillWaves), 0, s, a);
     return hipGetLastError();
 }
 

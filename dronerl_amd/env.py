@@ -36,9 +36,9 @@ class DroneEnvState:
 
     ground : uint8 [E, ground_stride]  object code per cell, row-major (first side*side bytes)
     drones : int32 [E, n_drones]       packed u32 records in dict order O
-    mt     : int32 [E, 1408]           two MT19937 blocks + the respawn-candidate ring
+    mt     : int32 [E, 1776]           two MT19937 blocks + the respawn-candidate ring
     mt_index: int32 [E]                CPython's MT index (bits 0-9), the block holding the
-                                       stream (bit 10), ring head / count (bits 16-22 / 24-31)
+                                       stream (bit 10), ring head / count (bits 11-19 / 20-29)
     (the stream's CPython getstate() words: BatchedDeliveryDrones.mt_words())
     """
     ground: torch.Tensor

@@ -46,19 +46,20 @@ extern "C" {
 
 typedef struct ihipStream_t* hipStream_t;
 
-#define DRL_ABI_VERSION 5
-/* Per-env RNG row of `mt` (u32 words, 5376 B):
+#define DRL_ABI_VERSION 6
+/* Per-env RNG row of `mt` (u32 words, 7104 B):
  *   [0, 624)     MT19937 block 0     the env's CPython stream lives in block
- *   [624, 1248)  MT19937 block 1     mt_index.par (the other block is scratch)
- *   [1248, 1376) respawn-candidate ring (DRL_CAND_SLOTS entries, see drl_refill)
- *   1376         the stream position just after the ring's last entry: MT
+ *   [624, 1248)  MT19937 block 1     mt_index.par; the other block holds the
+ *                                    next block (twisted by drl_refill) or scratch
+ *   [1248, 1760) respawn-candidate ring (DRL_CAND_SLOTS entries, see drl_refill)
+ *   1760         the stream position just after the ring's last entry: MT
  *                index | block << 10 (valid while the ring holds entries)
- *   [1377, 1408) padding (rows 64-B aligned) */
-#define DRL_MT_WORDS 1408
+ *   [1761, 1776) padding (rows 64-B aligned) */
+#define DRL_MT_WORDS 1776
 #define DRL_MT_BLOCK1 624
 #define DRL_MT_RING 1248
-#define DRL_MT_RING_END 1376
-#define DRL_CAND_SLOTS 128
+#define DRL_MT_RING_END 1760
+#define DRL_CAND_SLOTS 512
 #define DRL_MAX_DRONES 64
 #define DRL_MAX_SIDE 128
 #define DRL_MAX_RADIUS 8
@@ -120,7 +121,7 @@ typedef struct drl_layout {
  *  mt     : u32 [E][DRL_MT_WORDS]   two MT19937 blocks + the candidate ring (above)
  *  mt_index: u32 [E]                bits 0-9 CPython's MT index (next word; 624 =
  *                                   twist first), bit 10 `par` (the block holding
- *                                   the stream), bits 16-22 ring head, bits 24-31
+ *                                   the stream), bits 11-19 ring head, bits 20-29
  *                                   ring count; kept apart so a wave's envs share
  *                                   one cache line.  A plain CPython index (0..624,
  *                                   upper bits 0) is a valid word: block 0, empty ring.
@@ -195,10 +196,12 @@ int drl_rollout(const drl_params* p, const drl_state* s, int32_t num_steps, cons
                 int64_t act_step_stride, float* d_rewards, uint8_t* d_dones, int64_t out_step_stride, float* d_obs,
                 int32_t obs_k, int64_t obs_step_stride, int32_t* d_err, hipStream_t stream);
 
-/* Top up every env's respawn-candidate ring (see drl_state) from its MT
- * stream: draws ahead of the stream position, twisting the next MT block into
- * the scratch block when the ring crosses a block end.  Never changes the
- * env's observable state.  drl_reset and drl_mt_set end with one. */
+/* Extend every env's respawn-candidate ring (see drl_state) through the end
+ * of the MT block after the stream's: an env whose ring does not reach past
+ * the stream's block gets the rest of that block's draws and, twisted into
+ * the other block's words, all of the next block's (up to DRL_CAND_SLOTS
+ * entries).  Never changes the env's observable state.  drl_reset and
+ * drl_mt_set end with one. */
 int drl_refill(const drl_params* p, const drl_state* s, hipStream_t stream);
 
 /* The envs' CPython getstate() words: d_words u32 [E][625] = the 624 state

@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol():
     exported = set(re.findall(r"\s(drl_\w+)$", out, re.M))
     missing = [f for f in fns if f not in exported]
     assert not missing, missing
-    assert lib().drl_abi_version() == 5
+    assert lib().drl_abi_version() == 6
 
 
 def test_library_is_gfx950_code_object():
@@ -56,11 +56,13 @@ def test_side_from_density_matches_reference_formula(n, density, side):
 def test_layout_and_validation():
     L = EnvParams(n_drones=8, grid_size=16).layout()
     assert (L.cells, L.ground_stride, L.drone_stride, L.mt_stride, L.obs_window, L.obs_floats) == \
-        (256, 256, 8, 1408, 7, 294)
+        (256, 256, 8, 1776, 7, 294)
     assert L.step_group_lanes == 8
-    assert (L.cand_slots, L.refill_every) == (128, 32)
+    assert (L.cand_slots, L.refill_every) == (512, 32)
     L = EnvParams(n_drones=32, grid_size=64).layout()
     assert L.step_group_lanes in (32, 64) and L.step_lds_bytes <= 160 * 1024
+    # half a block's worth of candidates (156 pairs at power-of-two sides) at ~1.53 + 0.06 N per step
+    assert L.refill_every == 22
     L = EnvParams(n_drones=1, grid_size=5).layout()
     assert L.ground_stride == 32
     with pytest.raises(ValueError, match="Not enough positions"):

@@ -739,44 +739,66 @@ def test_reset_states_fixture_on_gpu(name, kernel, monkeypatch):
         np.testing.assert_array_equal(mt_sha(g["mt"][e]), d[f"{name}__mtsha"][e], err_msg=f"{name} seed {e} MT")
 
 
-@pytest.mark.parametrize("name", ["c1_8x8_n4", "c2_16x16_n8", "c5_64x64_n32", "bigside_128_n4", "n6_11x11"])
+@pytest.mark.parametrize("name", ["c1_8x8_n4", "c2_16x16_n8", "c5_64x64_n32", "bigside_128_n4", "n6_11x11",
+                                  "n1_5x5"])
 def test_candidate_ring_holds_the_streams_randint_pairs(name):
-    """drl_refill's ring, entry by entry, against CPython's own generator: entry
-    k is the k-th (randint(0, side-1), randint(0, side-1)) pair drawn from the
-    env's stream (random.setstate of its getstate words), with the MT index
-    after the pair and its block (flipped once the stream passes a twist); the
-    ring-end word is the position after the last entry.  Checked after the
-    reset's fill and again mid-run (partly consumed, wrapped, topped up)."""
+    """drl_refill's ring, entry by entry, against CPython's own generator:
+    entry k is the k-th (randint(0, side-1), randint(0, side-1)) pair drawn
+    from the env's stream (random.setstate of its getstate words), with the MT
+    index after the pair and its block (flipped once the stream passes a
+    twist); the ring-end word is the position after the last entry; the ring
+    reaches through the end of the block after the stream's (the next pair
+    would end two blocks on) unless it is full; that next block sits twisted
+    in the other block's words.  Checked after the reset's conversion and
+    again mid-run (partly consumed, wrapped, converted again)."""
     import random
+    from dronerl_amd._native import DRL_CAND_SLOTS as CAP, DRL_MT_RING as RING, DRL_MT_RING_END as RING_END
     p = EnvParams(**CONFIGS[name])
     G, E = p.side, 48
+    kb = G.bit_length()
     env = Env(p, E)
     env.reset(seed=13)
-    for phase in range(2):
+    for phase in range(3):
         if phase:
-            for t in range(37):
-                env.step(env.synth_actions(seed=3, step=t))
+            for t in range(37 if phase == 1 else 160):
+                env.step(env.synth_actions(seed=3 + phase, step=t))
             env.refill()
         words = env.mt_words().numpy()
         mi = env.state.mt_index.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
         mt = env.state.mt.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
         for e in range(E):
-            head, cnt, tpar = (mi[e] >> 16) & 127, mi[e] >> 24, (mi[e] >> 10) & 1
-            assert cnt == 128, f"{name} env {e}: ring not full after a refill ({cnt})"
+            head, cnt, tpar = (mi[e] >> 11) & (CAP - 1), (mi[e] >> 20) & 0x3FF, (mi[e] >> 10) & 1
             r = random.Random()
             r.setstate((3, tuple(int(v) for v in words[e]), None))
-            prev, crossed = int(words[e, 624]), 0
+            pos = int(words[e, 624])  # absolute stream position (words drawn since block 0 of the stream's)
+
+            def randint():  # _randbelow(G) one getrandbits(kb) word at a time, counting words
+                nonlocal pos
+                while True:
+                    pos += 1
+                    v = r.getrandbits(kb)
+                    if v < G:
+                        return v
+            last = None
             for k in range(cnt):
-                y, x = r.randint(0, G - 1), r.randint(0, G - 1)
-                idx = r.getstate()[1][624]
-                crossed |= idx < prev
-                prev = idx
-                want = (y * G + x) | (idx << 16) | ((tpar ^ crossed) << 26)
-                got = mt[e, 1248 + (head + k) % 128]
-                assert got == want, f"{name} phase {phase} env {e} entry {k}: {got:#x} != {want:#x}"
-            assert mt[e, 1376] == (prev | ((tpar ^ crossed) << 10)), f"{name} env {e}: ring-end word"
-            if crossed:  # the other block holds the twisted next block: CPython's words after the twist
-                np.testing.assert_array_equal(mt[e, (1 - tpar) * 624:(2 - tpar) * 624],
-                                              np.array(r.getstate()[1][:624], dtype=np.int64),
-                                              err_msg=f"{name} env {e}: next block")
+                y, x = randint(), randint()
+                blk = (pos - 1) // 624  # block of the pair's last word (0: the stream's)
+                idx = pos - 624 * blk
+                want = (y * G + x) | (idx << 16) | ((tpar ^ (blk & 1)) << 26)
+                got = mt[e, RING + (head + k) % CAP]
+                assert got == want, f"{name} phase {phase} env {e} entry {k}/{cnt}: {got:#x} != {want:#x}"
+                last = idx | ((tpar ^ (blk & 1)) << 10)
+                assert blk <= 1
+            if last is not None:
+                assert mt[e, RING_END] == last, f"{name} env {e}: ring-end word"
+            if cnt < CAP:  # converted through the end of the next block: the next pair ends two blocks on
+                randint(), randint()
+                assert (pos - 1) // 624 >= 2, f"{name} phase {phase} env {e}: ring stops short ({cnt} entries)"
+            # the next block, twisted into the other block's words: CPython's words after the first twist
+            r2 = random.Random()
+            r2.setstate((3, tuple(int(v) for v in words[e][:624]) + (624,), None))
+            r2.getrandbits(1)
+            np.testing.assert_array_equal(mt[e, (1 - tpar) * 624:(2 - tpar) * 624],
+                                          np.array(r2.getstate()[1][:624], dtype=np.int64),
+                                          err_msg=f"{name} env {e}: next block")
     env.check_errors()

@@ -49,7 +49,7 @@ def main():
         for _ in range(args.reps):
             env.refill()
             env._since_refill = 0
-            cnt = (mi >> 24) & 255
+            cnt = (mi >> 20) & 1023
             newc = torch.clamp(cnt - k, min=0)
             mi.copy_((mi & 0x00FFFFFF) | (newc << 24))
             ts.append(timed_refill(env, s))

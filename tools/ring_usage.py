@@ -21,14 +21,14 @@ for name, (G, N, E) in CFG.items():
         env.step(env.synth_actions(seed=1, step=t))
     env.refill_every = 0
     env.refill()
-    c0 = ((env.state.mt_index >> 24) & 255).clone()
+    c0 = ((env.state.mt_index >> 20) & 1023).clone()
     out = {"config": name, "cadence": env.layout.refill_every, "start_mean": float(c0.float().mean())}
     t = 0
     for k in [1, 4, 8, 16, 24, 32, 48]:
         while t < k:
             env.step(env.synth_actions(seed=2, step=t))
             t += 1
-        c = (env.state.mt_index >> 24) & 255
+        c = (env.state.mt_index >> 20) & 1023
         used = (c0 - c).float()
         out[f"k{k}"] = {"mean": round(float(used.mean()), 2), "p99": float(used.quantile(0.99)),
                         "max": float(used.max()), "dry": float((c == 0).float().mean())}
