@@ -1934,39 +1934,32 @@ __global__ void drl_mt_set_kernel(uint32_t* __restrict__ mt, uint32_t* __restric
 // (~9 B per word with its entry), instead of being re-read by 64-word passes
 // after the twist that wrote it (round 2's refill: ~13 B per word).
 //
-// One wave per env (its 624 words in x[10] as in twist_regs), four waves per
-// workgroup: waves never wait for one another, and envs that need nothing
-// leave after two scalar loads.  Within a 64-word chunk acceptance is one
+// A wave serves kRefillEnvs envs (its 624 words each in x[e][10] as in
+// twist_regs): the mt_index and ring-end words of all of them are read at
+// once, then the blocks of those that need a conversion, and only then are
+// they converted one after another, so a wave pays its two memory round
+// trips once for all its envs (one env per wave left each wave a dependent
+// chain of scalar load -> block load -> conversion at 8 waves per SIMD: C3
+// 44 us per refill, 3.6 TB/s).  Within a 64-word chunk acceptance is one
 // ballot, a draw's accepted rank an mbcnt, and an x draw takes its y from the
 // previous accepted lane by ds_bpermute (the first of a chunk from the
 // pending y of the previous chunk).  A ring that would overflow stops at
 // DRL_CAND_SLOTS entries; its end then lies inside block s+1, whose words the
 // next conversion (after the stream moves into s+1) converts from registers.
-constexpr int kRefillWaves = 4;  // waves (envs) per workgroup
+#ifndef DRL_REFILL_ENVS
+#define DRL_REFILL_ENVS 2
+#endif
+constexpr int kRefillEnvs = DRL_REFILL_ENVS;  // envs per wave
+constexpr int kRefillWaves = 4;               // waves per workgroup
 
-__global__ void __launch_bounds__(64 * kRefillWaves) drl_refill_kernel(RefillArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int64_t env = (int64_t)blockIdx.x * kRefillWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (env >= a.E) return;  // whole wave
+// The conversion of one env whose stream block is in x (see above).
+__device__ __forceinline__ void refill_env(const RefillArgs& a, int64_t env, uint32_t mw, uint32_t rend, int from,
+                                           uint32_t (&x)[10], int lane) {
     uint32_t* const row = a.mt + env * MT_WORDS;
-    const uint32_t mw = a.mt_index[env];  // uniform: scalar loads
-    const uint32_t rend = row[MT_RING_END];
     const int cnt = mi_cnt(mw), spar = mi_par(mw);
-    // where the unconverted stream starts, relative to the stream's block:
-    // the end of the ring's last entry (in the next block: + 624), or the
-    // stream position when the ring is empty
-    const int from = cnt > 0 ? min((int)(rend & 0x3ffu), MT_N) + ((int)((rend >> 10) & 1u) != spar ? MT_N : 0)
-                             : min(mi_idx(mw), MT_N);
-    if (from > MT_N) return;  // the ring reaches into the next block already
     const int G = a.side, shift = 32 - a.kbits;
     const int room = CAND_Q - cnt;
     const int ring0 = mi_head(mw) + cnt;  // slot of the first new entry (mod CAND_Q)
-    uint32_t x[10];
-    {
-        const uint32_t* src = row + (uint32_t)spar * MT_ALT;  // not written by this kernel: plain loads
-#pragma unroll
-        for (int c = 0; c < 10; ++c) x[c] = (64 * c + lane < MT_N) ? src[64 * c + lane] : 0u;
-    }
     uint32_t* const ring = row + MT_RING;
     const uint64_t lower = (1ull << lane) - 1ull;
     int made = 0;             // entries written (uniform)
@@ -2015,6 +2008,49 @@ __global__ void __launch_bounds__(64 * kRefillWaves) drl_refill_kernel(RefillArg
         a.mt_index[env] = mi_pack(mi_idx(mw), spar, mi_head(mw), cnt + made);
         row[MT_RING_END] = end_word;
     }
+}
+
+__global__ void __launch_bounds__(64 * kRefillWaves) drl_refill_kernel(RefillArgs a) {
+    constexpr int NE = kRefillEnvs;
+    const int lane = threadIdx.x & 63;
+    const int64_t env0 = ((int64_t)blockIdx.x * kRefillWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * NE;
+    if (env0 >= a.E) return;  // whole wave
+    // ---- round trip 1: each env's mt_index word and ring-end word (uniform: scalar loads)
+    uint32_t mw[NE], rend[NE];
+    int from[NE];
+    bool need[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const int64_t ev = min(env0 + e, a.E - 1);
+        mw[e] = a.mt_index[ev];
+        rend[e] = a.mt[ev * MT_WORDS + MT_RING_END];
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        // where the unconverted stream starts, relative to the stream's block:
+        // the end of the ring's last entry (in the next block: + 624), or the
+        // stream position when the ring is empty; nothing to do once the ring
+        // reaches into the next block
+        const int cnt = mi_cnt(mw[e]), spar = mi_par(mw[e]);
+        from[e] = cnt > 0 ? min((int)(rend[e] & 0x3ffu), MT_N) + ((int)((rend[e] >> 10) & 1u) != spar ? MT_N : 0)
+                          : min(mi_idx(mw[e]), MT_N);
+        need[e] = env0 + e < a.E && from[e] <= MT_N;
+    }
+    // ---- round trip 2: the stream blocks of every env that needs a conversion
+    // (not written by this kernel: plain loads), all issued before any is used
+    uint32_t x[NE][10];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        if (need[e]) {
+            const uint32_t* src = a.mt + (env0 + e) * MT_WORDS + (uint32_t)mi_par(mw[e]) * MT_ALT;
+#pragma unroll
+            for (int c = 0; c < 10; ++c) x[e][c] = (64 * c + lane < MT_N) ? src[64 * c + lane] : 0u;
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int e = 0; e < NE; ++e)
+        if (need[e]) refill_env(a, env0 + e, mw[e], rend[e], from[e], x[e], lane);
 }
 
 // ------------------------------------------------------- synthetic actions ---
@@ -2134,7 +2170,7 @@ hipError_t launch_encode(uint32_t* drones, int64_t E, int N, const int32_t* orde
 }
 
 hipError_t launch_refill(const RefillArgs& a, hipStream_t s) {
-    const int64_t blocks = (a.E + kRefillWaves - 1) / kRefillWaves;
+    const int64_t blocks = (a.E + kRefillWaves * kRefillEnvs - 1) / (kRefillWaves * kRefillEnvs);
     hipLaunchKernelGGL(drl_refill_kernel, dim3((unsigned)blocks), dim3(64 * kRefillWaves), 0, s, a);
     return hipGetLastError();
 }

@@ -98,8 +98,9 @@ def test_qnet_greedy_matches_torch_reference(hidden, E):
     obs, _ = _obs_batch(E)
     g = torch.Generator().manual_seed(len(hidden) * 1000 + E)
     net = QNetwork(obs.shape[1], hidden, generator=g)
+    gb = torch.Generator(device="cuda").manual_seed(E + 3)
     for b in net.biases:
-        b.normal_(0, 0.1, generator=None)
+        b.normal_(0, 0.1, generator=gb)
     net.pack()
     q = torch.empty((E, 5), device="cuda")
     a = net.act(obs, epsilon=0.0, q_out=q)
@@ -134,8 +135,9 @@ def test_qnet_f32_matches_fp32_forward(hidden, E, radius):
     obs, _ = _obs_batch(E, radius=radius)
     g = torch.Generator().manual_seed(len(hidden) * 1000 + E)
     net = QNetwork(obs.shape[1], hidden, generator=g, precision="f32")
+    gb = torch.Generator(device="cuda").manual_seed(E + 7)
     for b in net.biases:
-        b.normal_(0, 0.1, generator=None)
+        b.normal_(0, 0.1, generator=gb)
     net.pack()
     q = torch.empty((E, 5), device="cuda")
     a = net.act(obs, epsilon=0.0, q_out=q)
@@ -152,8 +154,19 @@ def test_qnet_f32_matches_fp32_forward(hidden, E, radius):
     err = ((qc - ref32).abs() / scale).max().item()
     assert err <= Q_TOL_EXACT, err
     assert ((qc.double() - ref64).abs() / scale.double()).max().item() <= Q_TOL_EXACT
-    # greedy action == torch.argmax of the f32 reference (first maximum) on every env
-    assert torch.equal(a[:, 0].cpu().long(), torch.argmax(ref32, dim=1))
+    # greedy action == torch.argmax of the f32 reference (first maximum) on every env whose top two
+    # Q values are further apart than the tolerance (two f32 forwards that sum in different orders may
+    # order a closer pair either way); on the others the chosen action's reference Q is within the
+    # tolerance of the maximum
+    act = a[:, 0].cpu().long()
+    top2 = torch.topk(ref32, 2, dim=1).values
+    tol = 2 * Q_TOL_EXACT * scale[:, 0]
+    clear = (top2[:, 0] - top2[:, 1]) > tol
+    assert clear.float().mean() > 0.99
+    assert torch.equal(act[clear], torch.argmax(ref32, dim=1)[clear])
+    chosen = ref32.gather(1, act[:, None])[:, 0]
+    assert torch.all(chosen >= top2[:, 0] - tol)
+    assert torch.equal(act, torch.argmax(q.cpu(), dim=1))  # and always the first argmax of its own Q
 
 
 @gpu
