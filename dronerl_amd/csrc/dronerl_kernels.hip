@@ -597,7 +597,11 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     // them, so the wait counts stay exact); inactive lanes discard the values
     const uint32_t li0 = min(rl0 + (uint32_t)j0, (uint32_t)(nenv_w * N - 1));
     const uint32_t rec_ld = drones_w[li0];
+#ifdef DRL_DIAG_ACT_U8  // bytes-only diagnostic build (wrong actions): one byte per action
+    const int act_ld = reinterpret_cast<const uint8_t*>(a.actions)[wenv0 * N + li0] % 5;
+#else
     const int act_ld = a.actions[wenv0 * N + li0];
+#endif
     if constexpr (GEO::kGstride > 0) stage_ground_dma_n<GPW * GEO::kGstride / 16>(ground_w, nenv_w * gstride, W.gl, lane0);
     else stage_ground_dma(ground_w, nenv_w * gstride, W.gl, lane0);
     __builtin_amdgcn_sched_barrier(0);  // issue every load above before waiting for the MT index
@@ -624,7 +628,11 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         const uint32_t rbase = (uint32_t)(env_ok0 ? grp0 : 0) * MT_WORDS + MT_RING;
         const int qh = mi_head(mw);
 #pragma unroll
+#ifdef DRL_DIAG_RING_FIXED  // bytes-only diagnostic build (wrong results): every env reads the wave's first window
+        for (int r = 0; r < QL; ++r) cq[r] = mt_w[MT_RING + ((j0 + P * r) & (CAND_Q - 1))];
+#else
         for (int r = 0; r < QL; ++r) cq[r] = mt_w[rbase + ((qh + j0 + P * r) & (CAND_Q - 1))];
+#endif
     };
     int act_next = 4;
     const int T = ROLL ? a.steps : 1;
@@ -1935,19 +1943,21 @@ __global__ void drl_mt_set_kernel(uint32_t* __restrict__ mt, uint32_t* __restric
 // after the twist that wrote it (round 2's refill: ~13 B per word).
 //
 // A wave serves kRefillEnvs envs (its 624 words each in x[e][10] as in
-// twist_regs): the mt_index and ring-end words of all of them are read at
-// once, then the blocks of those that need a conversion, and only then are
-// they converted one after another, so a wave pays its two memory round
-// trips once for all its envs (one env per wave left each wave a dependent
-// chain of scalar load -> block load -> conversion at 8 waves per SIMD: C3
-// 44 us per refill, 3.6 TB/s).  Within a 64-word chunk acceptance is one
-// ballot, a draw's accepted rank an mbcnt, and an x draw takes its y from the
-// previous accepted lane by ds_bpermute (the first of a chunk from the
-// pending y of the previous chunk).  A ring that would overflow stops at
-// DRL_CAND_SLOTS entries; its end then lies inside block s+1, whose words the
-// next conversion (after the stream moves into s+1) converts from registers.
+// twist_regs), four waves per workgroup: the mt_index and ring-end words of
+// all of them are read at once, then the blocks of those that need a
+// conversion, then they are converted one after another.  One env per wave
+// measured best (C3 48.8 / 52.9 / 62.9 / 74.2 us per refill at 1 / 2 / 4 / 8
+// envs per wave with chained chunks, tools/refill_time.py): a conversion is a
+// latency chain, and more waves hide it better than shared round trips do.
+// Within a 64-word chunk acceptance is one ballot, a draw's accepted rank an
+// mbcnt, and an x draw takes its y from the previous accepted lane by
+// ds_bpermute (the first of a chunk from the pending y carried from earlier
+// chunks); the ten chunks of a block are independent after a scalar pass
+// over their ballots.  A ring that would overflow stops at DRL_CAND_SLOTS
+// entries; its end then lies inside block s+1, whose words the next
+// conversion (after the stream moves into s+1) converts from registers.
 #ifndef DRL_REFILL_ENVS
-#define DRL_REFILL_ENVS 2
+#define DRL_REFILL_ENVS 1
 #endif
 constexpr int kRefillEnvs = DRL_REFILL_ENVS;  // envs per wave
 constexpr int kRefillWaves = 4;               // waves per workgroup
@@ -1965,33 +1975,52 @@ __device__ __forceinline__ void refill_env(const RefillArgs& a, int64_t env, uin
     int made = 0;             // entries written (uniform)
     int carry = 0, yv = 0;    // a pending y (accepted draw without its x yet)
     uint32_t end_word = rend; // ring-end word: MT index | block << 10 after the last entry
-    // convert chunk c of block bp (positions >= f0 only)
-    auto chunk = [&](uint32_t word, int c, int bp, int f0) __attribute__((always_inline)) {
-        const int pos = 64 * c + lane;
-        const bool valid = pos >= f0 && pos < MT_N;
-        const int r = (int)(temper(word) >> shift);
-        const bool acc = valid && r < G;
-        const uint64_t M = __ballot(acc);
-        const int k = mbcnt64(M);  // accepted draws of this chunk below this lane
-        const int ar = carry + k;  // accepted rank within the pairing
-        const uint64_t below = M & lower;
-        const int yl = below ? 63 - __clzll((long long)below) : lane;
-        const int ry = __shfl(r, yl);
-        const int yy = k > 0 ? ry : yv;
-        const int slot = made + (ar >> 1);
-        const bool put = acc && (ar & 1) && slot < room;
-        if (put) ring[(uint32_t)(ring0 + slot) & (uint32_t)(CAND_Q - 1)] = ce_pack(yy * G + r, pos + 1, bp);
-        const uint64_t P = __ballot(put);
-        if (P) end_word = (uint32_t)(64 * c + (63 - __clzll((long long)P)) + 1) | ((uint32_t)bp << 10);
-        const int tot = carry + __popcll(M);
-        if (M && (tot & 1)) yv = __builtin_amdgcn_readlane(r, 63 - __clzll((long long)M));
-        made = min(made + (tot >> 1), room);
-        carry = tot & 1;
+    // Convert block bp's words from position f0 on.  Three passes keep the
+    // ten chunks independent (their bpermutes and stores overlap instead of
+    // forming one dependent chain): every chunk's draws and acceptance
+    // ballot; then, in scalar registers, each chunk's pairing state (pending
+    // y, entries made before it); then every chunk's pairs and stores.
+    auto convert = [&](const uint32_t (&xw)[10], int bp, int f0) __attribute__((always_inline)) {
+        int r[10];
+        uint64_t M[10];
+#pragma unroll
+        for (int c = 0; c < 10; ++c) {
+            const int pos = 64 * c + lane;
+            r[c] = (int)(temper(xw[c]) >> shift);
+            M[c] = __ballot(pos >= f0 && pos < MT_N && r[c] < G);
+        }
+        int carry_c[10], yv_c[10], base_c[10];
+#pragma unroll
+        for (int c = 0; c < 10; ++c) {
+            carry_c[c] = carry;
+            yv_c[c] = yv;
+            base_c[c] = made;
+            const int tot = carry + __popcll(M[c]);
+            if (M[c] && (tot & 1)) yv = __builtin_amdgcn_readlane(r[c], 63 - __clzll((long long)M[c]));
+            made = min(made + (tot >> 1), room);
+            carry = tot & 1;
+        }
+#pragma unroll
+        for (int c = 0; c < 10; ++c) {
+            if (M[c] && base_c[c] < room) {
+                const int pos = 64 * c + lane;
+                const bool acc = (M[c] >> lane) & 1ull;
+                const int k = mbcnt64(M[c]);  // accepted draws of this chunk below this lane
+                const int ar = carry_c[c] + k;  // accepted rank within the pairing
+                const uint64_t below = M[c] & lower;
+                const int yl = below ? 63 - __clzll((long long)below) : lane;
+                const int ry = __shfl(r[c], yl);
+                const int yy = k > 0 ? ry : yv_c[c];
+                const int slot = base_c[c] + (ar >> 1);
+                const bool put = acc && (ar & 1) && slot < room;
+                if (put) ring[(uint32_t)(ring0 + slot) & (uint32_t)(CAND_Q - 1)] = ce_pack(yy * G + r[c], pos + 1, bp);
+                const uint64_t P = __ballot(put);
+                if (P) end_word = (uint32_t)(64 * c + (63 - __clzll((long long)P)) + 1) | ((uint32_t)bp << 10);
+            }
+        }
     };
     // ---- the rest of the stream's block, from `from`
-#pragma unroll
-    for (int c = 0; c < 10; ++c)
-        if (64 * c + 64 > from && made < room) chunk(x[c], c, spar, from);
+    if (from < MT_N) convert(x, spar, from);
     // ---- block s+1: twisted in registers, stored to the other block, converted
     twist_regs(x, lane);
     {
@@ -2000,9 +2029,7 @@ __device__ __forceinline__ void refill_env(const RefillArgs& a, int64_t env, uin
         for (int c = 0; c < 10; ++c)
             if (64 * c + lane < MT_N) dst[64 * c + lane] = x[c];
     }
-#pragma unroll
-    for (int c = 0; c < 10; ++c)
-        if (made < room) chunk(x[c], c, 1 - spar, 0);
+    if (made < room) convert(x, 1 - spar, 0);
     // (a pending y at the end is dropped: the next conversion re-reads it)
     if (lane == 0) {
         a.mt_index[env] = mi_pack(mi_idx(mw), spar, mi_head(mw), cnt + made);

@@ -8,7 +8,7 @@
 # = test failures only: the later tasks still run).  Output goes under
 # gpurun_out/ (copy what should be kept to profiles/).
 #
-#   tests     pytest -m gpu                    PYTEST_ARGS, T_TESTS (s)
+#   tests     pytest -m gpu                    PYTEST_K (-k expression), PYTEST_ARGS, T_TESTS (s)
 #   smoke     __graft_entry__.smoke()
 #   bench     python bench.py $BENCH_ARGS      -> gpurun_out/bench$TAG.json
 #   configs   bench lines of CFGS (c4 c5)      -> gpurun_out/bench_<cfg>$TAG.json
@@ -52,8 +52,11 @@ LOOP_ONLY="--no-cpu-baseline --no-reset-bench --no-dqn --rollout-chunk 0 --loop-
 for task in "$@"; do
   case $task in
     tests)
+      # PYTEST_K: a -k expression (spaces kept); PYTEST_ARGS="-k <expr>" is read the same way
+      K=${PYTEST_K:-}; PA=${PYTEST_ARGS:-}
+      if [ -z "$K" ] && [ "${PA#-k }" != "$PA" ]; then K=${PA#-k }; PA=; fi
       step tests "${T_TESTS:-900}" gpurun_out/pytest_gpu$TAG.log \
-        python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} ;;
+        python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread ${K:+-k "$K"} $PA ;;
     smoke)
       step smoke 300 gpurun_out/smoke$TAG.log python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)
