@@ -1103,12 +1103,17 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     if (active) {
         if constexpr (!ROLL) drones_w[rl + newslot] = rec_out;
         a.rewards[t * a.out_tstride + wenv0 * N + (rl + idx)] = reward;
+#ifndef DRL_DIAG_NO_SMALL_WB  // bytes-only diagnostic build: no sub-line stores (dones, mt_index)
         a.dones[t * a.out_tstride + wenv0 * N + (rl + idx)] = crashed ? 1 : 0;
+#endif
         posidx[idx] = (uint16_t)pos;
     }
     if constexpr (ROLL) {  // a dry ring: the stream position after the draws, an empty ring
         if (rounds > 0) mword = mi_pack(midx, mrow != mt_w + (uint32_t)(env_ok ? grp : 0) * MT_WORDS ? 1 : 0, 0, 0);
     } else if (env_ok && j == 0) {
+#ifdef DRL_DIAG_NO_SMALL_WB
+        if (a.E < 0)
+#endif
         a.mt_index[wenv0 + grp] = rounds > 0 ? mi_pack(midx, mrow != mt_w + (uint32_t)grp * MT_WORDS ? 1 : 0, 0, 0)
                                              : W.cnt[grp * 4 + 1];
     }
@@ -1122,8 +1127,10 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         // list never overflows (chg_push drops past capacity regardless).  The
         // loop usually runs once: keep it rolled, unrolled/vectorised copies
         // cost registers the whole kernel pays for.
+#ifndef DRL_DIAG_NO_GROUND_WB  // bytes-only diagnostic build (wrong state): no changed-cell write-back
 #pragma clang loop unroll(disable) vectorize(disable)
         for (uint32_t q = j; q < min(nc, (uint32_t)nchg); q += P) gdst[ch[q]] = gl[ch[q]];
+#endif
     }
     DRL_STAMP(5);
     if (GEO::kObs && a.obs) {
