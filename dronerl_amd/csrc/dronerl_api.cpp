@@ -210,6 +210,12 @@ drl::StepArgs step_args(const drl_params* p, const drl_state* s, const drl_layou
     return a;
 }
 
+// dones as dwords (drl_step's write-back): whole dwords per env and per step,
+// and room for an env's flags in its (dead) LDS occupancy bitmap
+int dones_packed(const drl_params* p, const uint8_t* d_dones, int64_t step_stride, const drl::StepArgs& a) {
+    return p->n_drones % 4 == 0 && (uintptr_t)d_dones % 4 == 0 && step_stride % 4 == 0 && a.lds_bm >= p->n_drones;
+}
+
 int launch_refill(const drl_params* p, const drl_state* s, hipStream_t stream) {
     drl::RefillArgs a;
     a.side = p->side;
@@ -349,6 +355,7 @@ int drl_step_ex(const drl_params* p, const drl_state* s, const int32_t* d_action
     a.err = d_err;
     a.og = obs_geom(p, L, d_obs ? obs_k : 1);
     a.obs_nt = (flags & DRL_STEP_OBS_STREAM) ? 1 : 0;
+    a.dones_packed = dones_packed(p, d_dones, 0, a);
     hipError_t e = drl::launch_step(a, L.step_group_lanes, stream, drl::kStepMode);
     if (e != hipSuccess) return hip_fail(e, "drl_step launch");
     return (flags & DRL_STEP_REFILL) ? launch_refill(p, s, stream) : 0;
@@ -384,6 +391,7 @@ int drl_rollout(const drl_params* p, const drl_state* s, int32_t num_steps, cons
     a.act_tstride = act_step_stride;
     a.out_tstride = out_step_stride;
     a.obs_tstride = d_obs ? obs_step_stride : 0;
+    a.dones_packed = dones_packed(p, d_dones, out_step_stride, a);
     if (L.step_group_lanes < (d_obs ? drl::kRolloutMinLanes : drl::kRolloutNoObsMinLanes)) {
         // narrow groups (the 64-VGPR kernels): one drl_step launch per step,
         // streaming observation stores, a refill every refill_every steps

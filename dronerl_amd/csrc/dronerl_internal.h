@@ -159,6 +159,7 @@ struct StepArgs {
     int obs_wide;   // observation stores: 1 = 16-B via LDS transpose, 0 = 3 x 8-B per cell
     int obs_nt;     // drl_step: 1 = streaming (non-temporal) observation stores (DRL_STEP_OBS_STREAM)
     int specialize; // 1: use a compile-time-geometry instance when one matches (DRL_SPECIALIZE=0 disables)
+    int dones_packed; // 1: dones written as dwords (n_drones % 4 == 0, 4-B aligned rows and step strides)
     uint32_t max_rounds;
     FastDiv div_side;
     ObsGeom og;

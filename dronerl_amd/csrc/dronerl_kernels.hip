@@ -1100,11 +1100,18 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     const uint32_t py = g.div_side((uint32_t)(pos > 0 ? pos : 0));
     const uint32_t px = (uint32_t)(pos > 0 ? pos : 0) - py * (uint32_t)G;
     const uint32_t rec_out = pack_drone((int)py, (int)px, c, carry, idx);
+    // dones: byte stores make the L2 fetch the 128-B line they land in (PMC:
+    // ~16 B of reads per env-step at C3); when n_drones % 4 == 0 each env's
+    // flags are gathered by drone index in LDS (the occupancy bitmap is dead
+    // now) and written as dwords instead
+    const bool dpack = a.dones_packed;
+    l_u8* const dn = reinterpret_cast<l_u8*>(bm);
     if (active) {
         if constexpr (!ROLL) drones_w[rl + newslot] = rec_out;
         a.rewards[t * a.out_tstride + wenv0 * N + (rl + idx)] = reward;
 #ifndef DRL_DIAG_NO_SMALL_WB  // bytes-only diagnostic build: no sub-line stores (dones, mt_index)
-        a.dones[t * a.out_tstride + wenv0 * N + (rl + idx)] = crashed ? 1 : 0;
+        if (dpack) dn[idx] = crashed ? 1 : 0;
+        else a.dones[t * a.out_tstride + wenv0 * N + (rl + idx)] = crashed ? 1 : 0;
 #endif
         posidx[idx] = (uint16_t)pos;
     }
@@ -1118,6 +1125,9 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
                                              : W.cnt[grp * 4 + 1];
     }
     wave_sync();
+    if (dpack && env_ok && j < (N >> 2))
+        reinterpret_cast<uint32_t*>(a.dones + t * a.out_tstride + wenv0 * N + rl)[j] =
+            reinterpret_cast<const l_u32*>(dn)[j];
     if (!ROLL && env_ok) {
         const uint32_t nc = W.cnt[grp * 4];
         const l_u16* ch = W.chg + grp * nchg;
@@ -1958,11 +1968,13 @@ __global__ void drl_mt_set_kernel(uint32_t* __restrict__ mt, uint32_t* __restric
 // latency chain, and more waves hide it better than shared round trips do.
 // Within a 64-word chunk acceptance is one ballot, a draw's accepted rank an
 // mbcnt, and an x draw takes its y from the previous accepted lane by
-// ds_bpermute (the first of a chunk from the pending y carried from earlier
-// chunks); the ten chunks of a block are independent after a scalar pass
-// over their ballots.  A ring that would overflow stops at DRL_CAND_SLOTS
-// entries; its end then lies inside block s+1, whose words the next
-// conversion (after the stream moves into s+1) converts from registers.
+// ds_bpermute (the first of a chunk from the pending y carried from the
+// previous chunk).  (Three passes that made the ten chunks of a block
+// independent -- every ballot, then the pairing state in scalar registers,
+// then the pairs -- measured slower: C3 60 vs 48 us, C5 134 vs 102.)  A ring
+// that would overflow stops at DRL_CAND_SLOTS entries; its end then lies
+// inside block s+1, whose words the next conversion (after the stream moves
+// into s+1) converts from registers.
 #ifndef DRL_REFILL_ENVS
 #define DRL_REFILL_ENVS 1
 #endif
@@ -1982,52 +1994,33 @@ __device__ __forceinline__ void refill_env(const RefillArgs& a, int64_t env, uin
     int made = 0;             // entries written (uniform)
     int carry = 0, yv = 0;    // a pending y (accepted draw without its x yet)
     uint32_t end_word = rend; // ring-end word: MT index | block << 10 after the last entry
-    // Convert block bp's words from position f0 on.  Three passes keep the
-    // ten chunks independent (their bpermutes and stores overlap instead of
-    // forming one dependent chain): every chunk's draws and acceptance
-    // ballot; then, in scalar registers, each chunk's pairing state (pending
-    // y, entries made before it); then every chunk's pairs and stores.
-    auto convert = [&](const uint32_t (&xw)[10], int bp, int f0) __attribute__((always_inline)) {
-        int r[10];
-        uint64_t M[10];
-#pragma unroll
-        for (int c = 0; c < 10; ++c) {
-            const int pos = 64 * c + lane;
-            r[c] = (int)(temper(xw[c]) >> shift);
-            M[c] = __ballot(pos >= f0 && pos < MT_N && r[c] < G);
-        }
-        int carry_c[10], yv_c[10], base_c[10];
-#pragma unroll
-        for (int c = 0; c < 10; ++c) {
-            carry_c[c] = carry;
-            yv_c[c] = yv;
-            base_c[c] = made;
-            const int tot = carry + __popcll(M[c]);
-            if (M[c] && (tot & 1)) yv = __builtin_amdgcn_readlane(r[c], 63 - __clzll((long long)M[c]));
-            made = min(made + (tot >> 1), room);
-            carry = tot & 1;
-        }
-#pragma unroll
-        for (int c = 0; c < 10; ++c) {
-            if (M[c] && base_c[c] < room) {
-                const int pos = 64 * c + lane;
-                const bool acc = (M[c] >> lane) & 1ull;
-                const int k = mbcnt64(M[c]);  // accepted draws of this chunk below this lane
-                const int ar = carry_c[c] + k;  // accepted rank within the pairing
-                const uint64_t below = M[c] & lower;
-                const int yl = below ? 63 - __clzll((long long)below) : lane;
-                const int ry = __shfl(r[c], yl);
-                const int yy = k > 0 ? ry : yv_c[c];
-                const int slot = base_c[c] + (ar >> 1);
-                const bool put = acc && (ar & 1) && slot < room;
-                if (put) ring[(uint32_t)(ring0 + slot) & (uint32_t)(CAND_Q - 1)] = ce_pack(yy * G + r[c], pos + 1, bp);
-                const uint64_t P = __ballot(put);
-                if (P) end_word = (uint32_t)(64 * c + (63 - __clzll((long long)P)) + 1) | ((uint32_t)bp << 10);
-            }
-        }
+    // convert chunk c of block bp (positions >= f0 only)
+    auto chunk = [&](uint32_t word, int c, int bp, int f0) __attribute__((always_inline)) {
+        const int pos = 64 * c + lane;
+        const bool valid = pos >= f0 && pos < MT_N;
+        const int r = (int)(temper(word) >> shift);
+        const bool acc = valid && r < G;
+        const uint64_t M = __ballot(acc);
+        const int k = mbcnt64(M);  // accepted draws of this chunk below this lane
+        const int ar = carry + k;  // accepted rank within the pairing
+        const uint64_t below = M & lower;
+        const int yl = below ? 63 - __clzll((long long)below) : lane;
+        const int ry = __shfl(r, yl);
+        const int yy = k > 0 ? ry : yv;
+        const int slot = made + (ar >> 1);
+        const bool put = acc && (ar & 1) && slot < room;
+        if (put) ring[(uint32_t)(ring0 + slot) & (uint32_t)(CAND_Q - 1)] = ce_pack(yy * G + r, pos + 1, bp);
+        const uint64_t P = __ballot(put);
+        if (P) end_word = (uint32_t)(64 * c + (63 - __clzll((long long)P)) + 1) | ((uint32_t)bp << 10);
+        const int tot = carry + __popcll(M);
+        if (M && (tot & 1)) yv = __builtin_amdgcn_readlane(r, 63 - __clzll((long long)M));
+        made = min(made + (tot >> 1), room);
+        carry = tot & 1;
     };
     // ---- the rest of the stream's block, from `from`
-    if (from < MT_N) convert(x, spar, from);
+#pragma unroll
+    for (int c = 0; c < 10; ++c)
+        if (64 * c + 64 > from && made < room) chunk(x[c], c, spar, from);
     // ---- block s+1: twisted in registers, stored to the other block, converted
     twist_regs(x, lane);
     {
@@ -2036,7 +2029,9 @@ __device__ __forceinline__ void refill_env(const RefillArgs& a, int64_t env, uin
         for (int c = 0; c < 10; ++c)
             if (64 * c + lane < MT_N) dst[64 * c + lane] = x[c];
     }
-    if (made < room) convert(x, 1 - spar, 0);
+#pragma unroll
+    for (int c = 0; c < 10; ++c)
+        if (made < room) chunk(x[c], c, 1 - spar, 0);
     // (a pending y at the end is dropped: the next conversion re-reads it)
     if (lane == 0) {
         a.mt_index[env] = mi_pack(mi_idx(mw), spar, mi_head(mw), cnt + made);
