@@ -1166,6 +1166,21 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     }
 }
 
+// XCD-aware block order (cdna_hip_programming.md T1, bijective form): the
+// blocks that share an XCD (the same blockIdx % 8) take consecutive batches of
+// envs, so the lines that neighbouring waves share -- the mt_index words (32
+// envs per 128-B line), dones, the observation's boundary lines -- are
+// written and re-read in one L2 instead of being filled into up to eight.
+// Placement never affects results.  DRL_XCD_REMAP=0 restores blockIdx order.
+#ifndef DRL_XCD_REMAP
+#define DRL_XCD_REMAP 1
+#endif
+__device__ __forceinline__ uint32_t xcd_block(uint32_t orig, uint32_t n) {
+    if (!DRL_XCD_REMAP) return orig;
+    const uint32_t q = n / 8, r = n % 8, x = orig % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + orig / 8;
+}
+
 // One wave per batch of GPW envs.  (Persistent waves looping over 2-4 batches
 // were measured slower at C3/C4/C5: halving the resident waves costs more
 // latency hiding than the longer waves gain in balance.)
@@ -1173,13 +1188,13 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
 template <int P, class GEO, bool NT>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : 1, 8)))
 drl_step_kernel(StepArgs a) {
-    step_batch<P, GEO, false, NT>(a, (int64_t)blockIdx.x * (64 / P));
+    step_batch<P, GEO, false, NT>(a, (int64_t)xcd_block(blockIdx.x, gridDim.x) * (64 / P));
 }
 
 // drl_rollout: a.steps steps per launch, same wave layout (P >= 16).
 template <int P, class GEO>
 __global__ void __launch_bounds__(64) drl_rollout_kernel(StepArgs a) {
-    step_batch<P, GEO, true, true>(a, (int64_t)blockIdx.x * (64 / P));
+    step_batch<P, GEO, true, true>(a, (int64_t)xcd_block(blockIdx.x, gridDim.x) * (64 / P));
 }
 
 // ------------------------------------------------------------ observation ---
@@ -1191,7 +1206,7 @@ __global__ void __launch_bounds__(64) drl_obs_kernel(StepArgs a) {
     const int lane = threadIdx.x & 63;
     const int grp = lane / P;
     const int j = lane % P;
-    const int64_t wenv0 = (int64_t)blockIdx.x * GPW;
+    const int64_t wenv0 = (int64_t)xcd_block(blockIdx.x, gridDim.x) * GPW;
     const int nenv_w = (int)min((int64_t)GPW, a.E - wenv0);
     if (nenv_w <= 0) return;
     const bool env_ok = grp < nenv_w;
@@ -2042,7 +2057,8 @@ __device__ __forceinline__ void refill_env(const RefillArgs& a, int64_t env, uin
 __global__ void __launch_bounds__(64 * kRefillWaves) drl_refill_kernel(RefillArgs a) {
     constexpr int NE = kRefillEnvs;
     const int lane = threadIdx.x & 63;
-    const int64_t env0 = ((int64_t)blockIdx.x * kRefillWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * NE;
+    const int64_t env0 =
+        ((int64_t)xcd_block(blockIdx.x, gridDim.x) * kRefillWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * NE;
     if (env0 >= a.E) return;  // whole wave
     // ---- round trip 1: each env's mt_index word and ring-end word (uniform: scalar loads)
     uint32_t mw[NE], rend[NE];
