@@ -1171,9 +1171,12 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
 // envs, so the lines that neighbouring waves share -- the mt_index words (32
 // envs per 128-B line), dones, the observation's boundary lines -- are
 // written and re-read in one L2 instead of being filled into up to eight.
-// Placement never affects results.  DRL_XCD_REMAP=0 restores blockIdx order.
+// Placement never affects results.  Measured and OFF by default (A/B on one
+// box, two rounds each): C3 21.56 vs 21.56 us/step, C5 155.3 vs 151.5 (worse),
+// refill 50.0 vs 48.5 us; the step's PMC read bytes fell only 1.5 %.  Build
+// with -DDRL_XCD_REMAP=1 to turn it on.
 #ifndef DRL_XCD_REMAP
-#define DRL_XCD_REMAP 1
+#define DRL_XCD_REMAP 0
 #endif
 __device__ __forceinline__ uint32_t xcd_block(uint32_t orig, uint32_t n) {
     if (!DRL_XCD_REMAP) return orig;
