@@ -238,7 +238,6 @@ struct QnetArgs {
     int frag_total, lds_vec, n_bias;
     int frag_lo_off[QN_MAX_LAYERS];  // F32: lo fragments (uint4 offsets from packed, or in LDS: lo0_lds)
     int bias_vec, lo0_lds;           // biases' uint4 offset; F32 layout with layer 0 alone in LDS
-    int total_bytes;                 // bytes of the packed net (F32 kernel: buffer loads of the later layers)
     const uint4* packed;
     const float* obs;
     int64_t obs_stride, E;

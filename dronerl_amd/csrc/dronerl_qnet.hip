@@ -60,10 +60,11 @@ __global__ void drl_qnet_pack_kernel(QnetPack p) {
         const int row = 16 * m + c;
         const int k = 32 * t + frag_k(g, j);
         const float w = (row < p.out[l] && k < p.in[l]) ? p.w[l][(int64_t)row * p.in[l] + k] : 0.0f;
-        if (p.precision == DRL_QNET_F32) {  // hi = fp16(w), lo = bf16(w - hi) (drl_qnet_act_f32_kernel)
+        if (p.precision == DRL_QNET_F32) {  // hi = fp16(w), lo = fp16((w - hi) * 2^11), lo after the LDS image
             const _Float16 hi = (_Float16)w;
             reinterpret_cast<_Float16*>(p.packed_w)[(int64_t)p.frag_off[l] * 8 + e] = hi;
-            reinterpret_cast<__bf16*>(p.packed_w)[(int64_t)p.frag_lo_off[l] * 8 + e] = (__bf16)(w - (float)hi);
+            reinterpret_cast<_Float16*>(p.packed_w)[(int64_t)p.frag_lo_off[l] * 8 + e] =
+                (_Float16)((w - (float)hi) * 2048.0f);
         } else {
             reinterpret_cast<__bf16*>(p.packed_w)[(int64_t)p.frag_off[l] * 8 + e] = (__bf16)w;
         }
@@ -88,6 +89,10 @@ constexpr int QN_WAVES = lay::qn_waves;
 constexpr int QN_MAXT = 8;    // 16-unit tiles per hidden layer (hidden <= 128)
 constexpr int QN_RING = lay::qn_ring;  // K-slices in flight per wave
 constexpr int QN_TILES = lay::qn_tiles;  // env tiles per pass sharing each weight fragment
+#ifndef DRL_QN_TILES_F32
+#define DRL_QN_TILES_F32 1
+#endif
+constexpr int QN_TILES_F32 = DRL_QN_TILES_F32;  // the same for DRL_QNET_F32 (two accumulator sets)
 
 __device__ __forceinline__ bf16x8 lds_frag(const uint4* base, int frag, int lane) {
     const uint4 v = base[frag * 64 + lane];
@@ -289,23 +294,16 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_kernel(QnetArgs a)
 }
 
 // ---------------------------------------------------------- act, F32 ---
-// DRL_QNET_F32: the reference's f32 nets from fp16/bf16 MFMAs into ONE f32
-// accumulator per tile.  Every weight w is packed as hi = fp16(w) and lo =
-// bf16(w - hi) (|lo| <= 2^-11 |w|; bf16's exponent range keeps it normal),
-// every operand x as x_hi = fp16(x), x_lo = fp16(x - x_hi) and x_b = bf16(x).
-// Per tile and K-slice three MFMAs add into the same accumulator:
-//   v_mfma_f32_16x16x32_f16  (hi,  x_hi)     the bulk, exact products
-//   v_mfma_f32_16x16x32_f16  (hi,  x_lo)     x's low bits
-//   v_mfma_f32_16x16x32_bf16 (lo,  x_b)      w's low bits
-// The dropped terms are lo * (x - x_b) and (hi) * (x - x_hi - x_lo): below
-// 2^-20 of |w x| each, plus x_lo's fp16 subnormal rounding (absolute 2^-25)
-// for |x| < 2^-3; Q matches an f32 forward to ~1e-6 relative.  One
-// accumulator set (round 2's scheme kept hi*lo terms in a second one, 2^11
-// apart) leaves the registers for 4 waves per SIMD: the kernel is bound by
-// the latency of its observation reads, and 16 waves per CU keep twice as
-// many slices in flight as round 2's 8 did.  Layer 0's hi and lo fragments
-// are the LDS image (160 KB at 294 -> 128); the later layers' fragments and
-// the biases are read from global memory (L2-resident).
+// DRL_QNET_F32: the same dataflow with every operand v split into fp16
+// hi = fp16(v) and lo = fp16((v - hi) * 2^11) (exact up to 2^-23 |v|).
+// Per tile and K-slice three v_mfma_f32_16x16x32_f16: acc += Whi*xhi and
+// acl += Wlo*xhi + Whi*xlo; a layer's value is acc + 2^-11 * acl (+ bias).
+// bf16 products would need three pieces per operand (six MFMAs); fp16's
+// 11-bit significand needs two.  The hi fragments sit where the bf16 ones do
+// (LDS), the later layers' lo fragments after the biases (LDS); layer 0's lo
+// fragments stay in global memory (L2-resident, 1 KB per fragment) because
+// both sets of the 294->128 layer do not fit 160 KB of LDS.  A slice's lo
+// fragments are loaded at its start and used after its hi products.
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ f16x8 as_f16x8(const uint4 v) {
@@ -313,58 +311,40 @@ __device__ __forceinline__ f16x8 as_f16x8(const uint4 v) {
     __builtin_memcpy(&f, &v, 16);
     return f;
 }
-__device__ __forceinline__ bf16x8 as_bf16x8(const uint4 v) {
-    bf16x8 f;
-    __builtin_memcpy(&f, &v, 16);
-    return f;
-}
 
 // `bad` collects operands outside fp16's range (|v| >= 65520 rounds hi to
 // inf; NaN stays NaN): the split would turn them into NaN Q values, so the
 // kernel flags DRL_ERR_QNET_RANGE instead of failing silently.
-__device__ __forceinline__ void split3(const float (&v)[8], f16x8& hi, f16x8& lo, bf16x8& b, bool& bad) {
+__device__ __forceinline__ void split_f16(const float (&v)[8], f16x8& hi, f16x8& lo, bool& bad) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const _Float16 h = (_Float16)v[j];
         hi[j] = h;
-        lo[j] = (_Float16)(v[j] - (float)h);
-        b[j] = (__bf16)v[j];
+        lo[j] = (_Float16)((v[j] - (float)h) * 2048.0f);
         bad |= !(__builtin_fabsf(v[j]) < 65520.0f);
     }
 }
 
 #define MFMA_F16 __builtin_amdgcn_mfma_f32_16x16x32_f16
-#define MFMA_BF16 __builtin_amdgcn_mfma_f32_16x16x32_bf16
-#ifndef DRL_QN_WAVES_F32
-#define DRL_QN_WAVES_F32 8
-#endif
-#ifndef DRL_QN_RING_F32
-#define DRL_QN_RING_F32 2
-#endif
-#ifndef DRL_QN_SERIAL_M
-#define DRL_QN_SERIAL_M 0
-#endif
-constexpr int QN_WAVES_F32 = DRL_QN_WAVES_F32;
-constexpr int QN_SERIAL_M = DRL_QN_SERIAL_M;  // fragment reads of at most this many m-tiles ahead of their MFMAs (0: any)
-constexpr int QN_RING_F32 = DRL_QN_RING_F32;
 
-// LO0 (layer 0's hi and lo fragments fit the LDS together, as at 294 ->
-// 128): the LDS image is layer 0's two sets; the later layers' fragments and
-// the biases come from global memory.  Otherwise (e.g. 486 inputs at 96
-// units) the LDS image is every layer's hi fragments, the biases and the
-// later layers' lo fragments, and layer 0's lo fragments come from global
-// memory (L2).
-template <int NT0, bool LO0>
-__global__ void __launch_bounds__(64 * QN_WAVES_F32) drl_qnet_act_f32_kernel(QnetArgs a) {
+// LO0 (the layout whenever layer 0's two fragment sets fit, as at 294->128):
+// layer 0's hi and lo fragments are the LDS image and the later layers'
+// fragments and the biases are read from global memory (L2) instead, which
+// moves a tile's L2 weight reads from 80 KB (layer 0's lo set) to the later
+// layers' few KB.
+template <int NT0, int TP, bool LO0>
+__global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_f32_kernel(QnetArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint4 wl[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int c = lane & 15, g = lane >> 4;
     constexpr int nt0 = NT0;
     const int64_t ntiles = (a.E + 15) / 16;
-    const int64_t gstride = (int64_t)gridDim.x * QN_WAVES_F32;
+    const int64_t ngroups = (ntiles + TP - 1) / TP;
+    const int64_t gstride = (int64_t)gridDim.x * QN_WAVES;
     const int KP = a.kt0;
-    const int rounds = KP / QN_RING_F32;
-    float raw[QN_RING_F32][8];
+    const int rounds = KP / QN_RING;
+    constexpr float kLo = 1.0f / 2048.0f;
+    float raw[TP][QN_RING][8];
     // the observation rows by buffer loads (32-bit offsets; the host checks obs < 4 GiB)
     const auto obuf = __builtin_amdgcn_make_buffer_rsrc((void*)a.obs, 0, (int)(a.E * a.obs_stride * 4), 0x00020000);
     auto load_slice = [&](uint32_t rowb, int t, float (&dst)[8]) {  // as in drl_qnet_act_kernel
@@ -386,159 +366,166 @@ __global__ void __launch_bounds__(64 * QN_WAVES_F32) drl_qnet_act_f32_kernel(Qne
         const int64_t env = t * 16 + c;
         return (uint32_t)((env < a.E ? env : a.E - 1) * a.obs_stride * 4);
     };
-    const int64_t grp0 = (int64_t)blockIdx.x * QN_WAVES_F32 + wave;
+    const int64_t grp0 = (int64_t)blockIdx.x * QN_WAVES + wave;
     int64_t grp = grp0;
-    uint32_t row = row_of(grp < ntiles ? grp : 0);
+    uint32_t row[TP];
 #pragma unroll
-    for (int i = 0; i < QN_RING_F32; ++i) load_slice(row, i, raw[i]);
-    for (int v0 = wave * 64; v0 < a.lds_vec; v0 += 64 * QN_WAVES_F32)
+    for (int h = 0; h < TP; ++h) row[h] = row_of(TP * (grp < ngroups ? grp : 0) + h);
+    // layer-0 lo fragments (global, L2-resident): buffer loads with the lane's
+    // 16-B offset in one VGPR and the fragment offset in an SGPR
+    const auto glo0 = __builtin_amdgcn_make_buffer_rsrc((void*)(a.packed + (LO0 ? 0 : a.frag_lo_off[0])), 0,
+                                                         nt0 * KP * 1024, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < QN_RING; ++i)
+#pragma unroll
+        for (int h = 0; h < TP; ++h) load_slice(row[h], i, raw[h][i]);
+    for (int v0 = wave * 64; v0 < a.lds_vec; v0 += 64 * QN_WAVES)
         if (v0 + lane < a.lds_vec)
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(a.packed + v0 + lane),
                                              (__attribute__((address_space(3))) void*)(wl + v0), 16, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    bool bad = false;  // an operand outside fp16's range (split3)
-    // the later layers' fragments and the biases (global, L2-resident) by
-    // buffer loads: one VGPR of lane offset, the fragment offset in an SGPR
-    // (flat 64-bit per-lane addresses cost two VGPRs per load in flight)
-    const auto pbuf = __builtin_amdgcn_make_buffer_rsrc((void*)a.packed, 0, a.total_bytes, 0x00020000);
-    const int lane16 = lane * 16, bias_b = a.bias_vec * 16;
-    auto gfrag = [&](int frag_u4) __attribute__((always_inline)) {  // 64 lanes x 16 B at uint4 offset frag_u4
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(pbuf, lane16, frag_u4 * 16, 0);
-        uint4 r;
-        __builtin_memcpy(&r, &v, 16);
-        return r;
-    };
-    // the later layers' fragments: global (LO0) or the LDS image
-    auto frag_ld = [&](int frag_u4) __attribute__((always_inline)) {
-        if constexpr (LO0) return gfrag(frag_u4);
-        else return wl[frag_u4 + lane];
-    };
-    auto bias4 = [&](int off) __attribute__((always_inline)) {  // biases off + 4g .. + 3
-        f32x4 r;
-        if constexpr (LO0) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(pbuf, 16 * g, bias_b + off * 4, 0);
-            __builtin_memcpy(&r, &v, 16);
-        } else {
-            const uint4 v = wl[a.bias_vec + (off >> 2) + g];
-            __builtin_memcpy(&r, &v, 16);
-        }
-        return r;
-    };
+    bool bad = false;  // an operand outside fp16's range (split_f16)
+    const float* bias = LO0 ? reinterpret_cast<const float*>(a.packed + a.bias_vec)
+                            : reinterpret_cast<const float*>(wl + a.frag_total);
     const uint4* W0 = wl + a.frag_off[0];
-    auto w0lo = [&](int frag) __attribute__((always_inline)) {  // layer 0's lo fragment: LDS (LO0) or global
-        if constexpr (LO0) return wl[a.frag_lo_off[0] + frag * 64 + lane];
-        else return gfrag(a.frag_lo_off[0] + frag * 64);
-    };
+    const uint4* W0lo = wl + (LO0 ? a.frag_lo_off[0] : 0);
+    const uint4* Wsrc = LO0 ? a.packed : wl;  // the later layers' fragments
 
-    for (; grp < ntiles; grp += gstride) {
+    for (; grp < ngroups; grp += gstride) {
         const int64_t ngrp = grp + gstride;
-        const uint32_t nrow = row_of(ngrp < ntiles ? ngrp : grp);
-        f32x4 acc[QN_MAXT];
+        uint32_t nrow[TP];
 #pragma unroll
-        for (int m = 0; m < QN_MAXT; ++m) acc[m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        // layer 0 over the ring (refill mode per round as in drl_qnet_act_kernel)
+        for (int h = 0; h < TP; ++h) nrow[h] = row_of(TP * (ngrp < ngroups ? ngrp : grp) + h);
+        f32x4 acc[TP][QN_MAXT], acl[TP][QN_MAXT];
+#pragma unroll
+        for (int h = 0; h < TP; ++h)
+#pragma unroll
+            for (int m = 0; m < QN_MAXT; ++m) acc[h][m] = acl[h][m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         auto round = [&](int rd, auto mode) {
             constexpr int MODE = decltype(mode)::value;
 #pragma unroll
-            for (int i = 0; i < QN_RING_F32; ++i) {
-                const int t = rd * QN_RING_F32 + i;
-                f16x8 bh, bl;
-                bf16x8 bb;
-                split3(raw[i], bh, bl, bb, bad);
-                if constexpr (MODE == 0) load_slice(row, t + QN_RING_F32, raw[i]);
-                else if constexpr (MODE == 1) load_slice(nrow, t + QN_RING_F32 - KP, raw[i]);
+            for (int i = 0; i < QN_RING; ++i) {
+                const int t = rd * QN_RING + i;
+                uint4 wlo[NT0];  // the slice's lo fragments (L2), used after the hi products
+                if constexpr (!LO0) {
+#pragma unroll
+                    for (int m = 0; m < nt0; ++m) {
+                        const auto v = __builtin_amdgcn_raw_buffer_load_b128(glo0, lane * 16, (m * KP + t) * 1024, 0);
+                        __builtin_memcpy(&wlo[m], &v, 16);
+                    }
+                }
+                f16x8 bh[TP], bl[TP];
+#pragma unroll
+                for (int h = 0; h < TP; ++h) {
+                    split_f16(raw[h][i], bh[h], bl[h], bad);
+                    if constexpr (MODE == 0) load_slice(row[h], t + QN_RING, raw[h][i]);
+                    else if constexpr (MODE == 1) load_slice(nrow[h], t + QN_RING - KP, raw[h][i]);
+                }
 #pragma unroll
                 for (int m = 0; m < nt0; ++m) {
                     const f16x8 wh = as_f16x8(W0[(m * KP + t) * 64 + lane]);
-                    const bf16x8 wo = as_bf16x8(w0lo(m * KP + t));
-                    acc[m] = MFMA_F16(wh, bh, acc[m], 0, 0, 0);
-                    acc[m] = MFMA_F16(wh, bl, acc[m], 0, 0, 0);
-                    acc[m] = MFMA_BF16(wo, bb, acc[m], 0, 0, 0);
-                    if constexpr (QN_SERIAL_M > 0)
-                        if ((m + 1) % QN_SERIAL_M == 0) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int h = 0; h < TP; ++h) {
+                        acc[h][m] = MFMA_F16(wh, bh[h], acc[h][m], 0, 0, 0);
+                        acl[h][m] = MFMA_F16(wh, bl[h], acl[h][m], 0, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int m = 0; m < nt0; ++m) {
+                    const f16x8 wo = as_f16x8(LO0 ? W0lo[(m * KP + t) * 64 + lane] : wlo[m]);
+#pragma unroll
+                    for (int h = 0; h < TP; ++h) acl[h][m] = MFMA_F16(wo, bh[h], acl[h][m], 0, 0, 0);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
         };
         for (int rd = 0; rd + 1 < rounds; ++rd) round(rd, std::integral_constant<int, 0>{});
-        if (ngrp < ntiles) round(rounds - 1, std::integral_constant<int, 1>{});
+        if (ngrp < ngroups) round(rounds - 1, std::integral_constant<int, 1>{});
         else round(rounds - 1, std::integral_constant<int, 2>{});
-        row = nrow;
+#pragma unroll
+        for (int h = 0; h < TP; ++h) row[h] = nrow[h];
         int nt_prev = nt0;
-        int bprev = a.bias_off[0];
+        const float* bprev = bias + a.bias_off[0];
         for (int l = 1; l <= a.n_hidden; ++l) {
-            f16x8 ah[QN_MAXT / 2], al[QN_MAXT / 2];
-            bf16x8 ab[QN_MAXT / 2];
+            f16x8 ah[TP][QN_MAXT / 2], al[TP][QN_MAXT / 2];
 #pragma unroll
-            for (int s2 = 0; s2 < QN_MAXT / 2; ++s2) {
-                if (2 * s2 < nt_prev) {
-                    const f32x4 b0 = bias4(bprev + 32 * s2), b1 = bias4(bprev + 32 * s2 + 16);
-                    float v[8];
+            for (int h = 0; h < TP; ++h) {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const int i = j & 3;
-                        v[j] = fmaxf(acc[2 * s2 + (j >> 2)][i] + (j < 4 ? b0[i] : b1[i]), 0.0f);
+                for (int s2 = 0; s2 < QN_MAXT / 2; ++s2) {
+                    if (2 * s2 < nt_prev) {
+                        float v[8];
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const int m = 2 * s2 + (j >> 2), i = j & 3;
+                            v[j] = fmaxf((acc[h][m][i] + acl[h][m][i] * kLo) + bprev[16 * m + 4 * g + i], 0.0f);
+                        }
+                        split_f16(v, ah[h][s2], al[h][s2], bad);
                     }
-                    split3(v, ah[s2], al[s2], ab[s2], bad);
                 }
             }
             const int nt_l = (l < a.n_hidden) ? a.nt[l] : 1;
             const int kt = nt_prev / 2;
 #pragma unroll
-            for (int m = 0; m < QN_MAXT; ++m) acc[m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-            const int Wl = a.frag_off[l], Wlo = a.frag_lo_off[l];
+            for (int h = 0; h < TP; ++h)
+#pragma unroll
+                for (int m = 0; m < QN_MAXT; ++m) acc[h][m] = acl[h][m] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            const uint4* Wl = Wsrc + a.frag_off[l];
+            const uint4* Wlo = Wsrc + a.frag_lo_off[l];
 #pragma unroll
             for (int t = 0; t < QN_MAXT / 2; ++t) {
                 if (t < kt) {
 #pragma unroll
                     for (int m = 0; m < QN_MAXT; ++m) {
                         if (m < nt_l) {
-                            const f16x8 wh = as_f16x8(frag_ld(Wl + (m * kt + t) * 64));
-                            const bf16x8 wo = as_bf16x8(frag_ld(Wlo + (m * kt + t) * 64));
-                            acc[m] = MFMA_F16(wh, ah[t], acc[m], 0, 0, 0);
-                            acc[m] = MFMA_F16(wh, al[t], acc[m], 0, 0, 0);
-                            acc[m] = MFMA_BF16(wo, ab[t], acc[m], 0, 0, 0);
-                            if constexpr (QN_SERIAL_M > 0)
-                                if ((m + 1) % QN_SERIAL_M == 0) __builtin_amdgcn_sched_barrier(0);
+                            const f16x8 wh = as_f16x8(Wl[(m * kt + t) * 64 + lane]);
+                            const f16x8 wo = as_f16x8(Wlo[(m * kt + t) * 64 + lane]);
+#pragma unroll
+                            for (int h = 0; h < TP; ++h) {
+                                acc[h][m] = MFMA_F16(wh, ah[h][t], acc[h][m], 0, 0, 0);
+                                acl[h][m] = MFMA_F16(wh, al[h][t], acl[h][m], 0, 0, 0);
+                                acl[h][m] = MFMA_F16(wo, ah[h][t], acl[h][m], 0, 0, 0);
+                            }
                         }
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);  // fragment reads next to their MFMAs (register pressure)
             }
             nt_prev = nt_l;
-            bprev = a.bias_off[l];
+            bprev = bias + a.bias_off[l];
         }
-        float q[8];
-        const f32x4 bq = bias4(bprev);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float own = acc[0][i] + bq[i];
-            const float hi = __shfl(own, c + 16);
-            q[i] = own;
-            q[i + 4] = hi;
-        }
-        const int64_t env = grp * 16 + c;
-        if (g == 0 && env < a.E) {
-            int best = 0;
-            for (int i = 1; i < a.n_actions; ++i) best = q[i] > q[best] ? i : best;
-            const uint64_t ge = (uint64_t)(a.env_offset + env);
-            const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (ge << 8) ^ 0xa5ull));
-            const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
-            const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
-            a.actions[env * a.action_stride] = (u < a.epsilon) ? rnd : best;
-            if (a.q)
-                for (int i = 0; i < a.n_actions; ++i) a.q[env * a.n_actions + i] = q[i];
+        for (int h = 0; h < TP; ++h) {
+            float q[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float own = (acc[h][0][i] + acl[h][0][i] * kLo) + bprev[4 * g + i];
+                const float hi = __shfl(own, c + 16);
+                q[i] = own;
+                q[i + 4] = hi;
+            }
+            const int64_t env = (TP * grp + h) * 16 + c;
+            if (g == 0 && env < a.E) {
+                int best = 0;
+                for (int i = 1; i < a.n_actions; ++i) best = q[i] > q[best] ? i : best;
+                const uint64_t ge = (uint64_t)(a.env_offset + env);
+                const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (ge << 8) ^ 0xa5ull));
+                const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
+                const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
+                a.actions[env * a.action_stride] = (u < a.epsilon) ? rnd : best;
+                if (a.q)
+                    for (int i = 0; i < a.n_actions; ++i) a.q[env * a.n_actions + i] = q[i];
+            }
         }
     }
     if (__ballot(bad) && lane == 0 && a.err) atomicOr(a.err, DRL_ERR_QNET_RANGE);
-    if (a.synth_n > 1) {  // as in drl_qnet_act_kernel (one 16-env tile per group)
+    if (a.synth_n > 1) {  // as in drl_qnet_act_kernel
         const uint32_t nd = (uint32_t)a.synth_n - 1u;
-        const uint32_t per = 16u * nd;
-        for (int64_t gg = grp0; gg < ntiles; gg += gstride) {
+        const uint32_t per = (uint32_t)(TP * 16) * nd;
+        for (int64_t gg = grp0; gg < ngroups; gg += gstride) {
             for (uint32_t k = (uint32_t)lane; k < per; k += 64u) {
                 const uint32_t el = k / nd;
-                const int64_t env = 16 * gg + el;
+                const int64_t env = TP * 16 * gg + el;
                 const uint64_t drone = 1u + (k - el * nd);
                 if (env < a.E) {
                     const uint64_t ctr = (a.synth_step << 40) ^ ((uint64_t)(a.env_offset + env) << 8) ^ drone;
@@ -604,14 +591,15 @@ hipError_t launch_qnet_pack(const QnetPack& p, hipStream_t s) {
 
 hipError_t launch_qnet_act(const QnetArgs& a, int num_cus, hipStream_t s) {
     if (a.precision == DRL_QNET_F32) {
-        const int64_t nt = (a.E + 15) / 16;
-        int64_t nb = (nt + QN_WAVES_F32 - 1) / QN_WAVES_F32;
+        constexpr int TP = QN_TILES_F32;
+        const int64_t ng = ((a.E + 15) / 16 + TP - 1) / TP;
+        int64_t nb = (ng + QN_WAVES - 1) / QN_WAVES;
         if (nb > num_cus) nb = num_cus;
-        const dim3 grid((unsigned)nb), block(64 * QN_WAVES_F32);
+        const dim3 grid((unsigned)nb), block(64 * QN_WAVES);
         const size_t lds = (size_t)a.lds_vec * 16;
-#define QN_F32_LAUNCH(NT)                                                                               \
-    if (a.lo0_lds) hipLaunchKernelGGL((drl_qnet_act_f32_kernel<NT, true>), grid, block, lds, s, a);    \
-    else hipLaunchKernelGGL((drl_qnet_act_f32_kernel<NT, false>), grid, block, lds, s, a)
+#define QN_F32_LAUNCH(NT)                                                                     \
+    if (a.lo0_lds) hipLaunchKernelGGL((drl_qnet_act_f32_kernel<NT, TP, true>), grid, block, lds, s, a); \
+    else hipLaunchKernelGGL((drl_qnet_act_f32_kernel<NT, TP, false>), grid, block, lds, s, a)
         switch (a.nt[0]) {
             case 2: QN_F32_LAUNCH(2); break;
             case 4: QN_F32_LAUNCH(4); break;

@@ -185,7 +185,6 @@ static int qnet_act_impl(const drl_qnet_desc* d, const void* d_packed, const flo
     a.frag_total = L.frag_total;
     a.bias_vec = L.bias_vec;
     a.lo0_lds = L.lo0_lds;
-    a.total_bytes = L.total_vec * 16;
     a.lds_vec = L.lds_vec;
     a.n_bias = L.n_bias;
     a.packed = static_cast<const uint4*>(d_packed);
