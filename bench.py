@@ -285,14 +285,15 @@ def cpu_baseline(G, N, K, seconds: float):
             "cpu_model": cpu_model()}
 
 
-def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream, precision="f32"):
+def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream, precision="f32", input="obs"):
     """the C3 loop's consumer of the observation, timed
     separately from the env step.  (1) drl_qnet_act alone on the resident obs
     (dense 294->128->64->5 on MFMA, epsilon-greedy, writes actions[:, 0]):
     HBM-bound on reading the obs (E * W*W*6 f32); (2) the train_jax.py:42-64
     loop shape per step: act -> step + obs -> replay add_many (capacity 10000).
     `precision` is the loop's (f32: the reference's nets); both acts are
-    timed alone."""
+    timed alone, and the f32 act from the policy code (drl_qnet_act_code,
+    128 B per env read instead of 1,176).  `input` is the loop act's."""
     from dronerl_amd.dqn import QNetwork, ReplayBuffer
     E = env.num_envs
     D = obs[0].numel()
@@ -309,16 +310,46 @@ def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream,
     ev[1].record(stream)
     # loop shape: act on obs_t, step writing obs_t+1 into the other buffer, add the transition
     bufs = [obs, torch.empty_like(obs)]
+    lnet = net
+    if input == "code":  # the step writes drone 0's policy code alone; the replay holds code rows
+        lnet = QNetwork(D, (128, 64), device=env.device, generator=torch.Generator().manual_seed(0),
+                        precision="f32", input="code")
+        bufs = [env.new_code(), env.new_code()]
+        env.get_code(out=bufs[0])
+        rb = ReplayBuffer(10000, D, env.device, code_radius=env.params.window_radius)
     ev[2].record(stream)
     for t in range(steps):
         cur, nxt = bufs[t & 1], bufs[(t + 1) & 1]
         a = actions[t % actions.shape[0]]
-        net.act(cur.reshape(E, -1), 0.1, seed=1, step=t, actions=a)
-        env.step(a, obs_k=1, rewards=rewards, dones=dones, obs=nxt)
+        if input == "code":
+            lnet.act(cur, 0.1, seed=1, step=t, actions=a)
+            env.step(a, rewards=rewards, dones=dones, code=nxt)
+        else:
+            lnet.act(cur.reshape(E, -1), 0.1, seed=1, step=t, actions=a)
+            env.step(a, obs_k=1, rewards=rewards, dones=dones, obs=nxt)
         rb.add_many(cur, a, rewards, nxt, dones)
     ev[3].record(stream)
     torch.cuda.synchronize()
     env.check_errors()
+    # the f32 act from the policy code of the same state
+    act_code = None
+    W = env.layout.obs_window
+    if W in (5, 7, 9):
+        cnet = lnet if input == "code" else QNetwork(D, (128, 64), device=env.device,
+                                                     generator=torch.Generator().manual_seed(0),
+                                                     precision="f32", input="code")
+        code = env.new_code()
+        env.get_obs(1, out=obs, code=code)
+        for t in range(warmup):
+            cnet.act(code, 0.1, seed=1, step=t, actions=a0)
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record(stream)
+        for t in range(steps):
+            cnet.act(code, 0.1, seed=1, step=t, actions=a0)
+        c1.record(stream)
+        torch.cuda.synchronize()
+        act_code = c0.elapsed_time(c1) / 1e3 / steps
+        cnet.check_errors()
     # the act in the other precision
     other = "bf16" if precision == "f32" else "f32"
     net32 = QNetwork(D, (128, 64), device=env.device, generator=torch.Generator().manual_seed(0), precision=other)
@@ -344,9 +375,15 @@ def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream,
             "act_bf16_us": t[0] * 1e6, "act_bf16_roofline": rl(t[0]),
             "act_bf16_note": "precision='bf16': bf16 MFMA operands, f32 accumulate (a labelled extra; narrower than "
                              "the reference)",
+            "act_code_f32_us": None if act_code is None else act_code * 1e6,
+            "act_code_note": "f32 act from drone 0's policy code (drl_qnet_act_code; the step writes it beside the "
+                             "observation): inputs exact in fp16, 2 MFMAs per layer-0 product tile, Q to 1e-5 of "
+                             "the f32 forward",
             "loop_us_per_step": loop_s * 1e6, "loop_env_steps_per_s": E / loop_s,
-            "loop": f"act(obs_t, {precision}) -> step + obs(K=1) -> replay add_many(obs_t, a, r, obs_t+1, done), "
-                    "capacity 10000"}
+            "loop": (f"act(code_t, f32) -> step + drone 0 policy code -> replay add_many(code_t, a, r, "
+                     "code_t+1, done) of code rows (sample() decodes), capacity 10000") if input == "code" else
+                    (f"act(obs_t, {precision}) -> step + obs(K=1) -> replay add_many(obs_t, a, r, obs_t+1, done), "
+                     "capacity 10000")}
 
 
 def rollout_bench(env, actions, K, warmup_steps, steps, chunk: int, R: int, Wb: int, world: int):
@@ -423,36 +460,54 @@ class TrainSegment:
     (tests/test_gpu_parity.py::test_train_segment_parallel_matches_serial)."""
 
     def __init__(self, env, seg: int, parallel: bool = False, net=None, rb=None, fused: bool = True,
-                 precision: str = "f32"):
+                 precision: str = "f32", input: str = "obs"):
         from dronerl_amd.dqn import QNetwork, ReplayBuffer
         E, N, dev = env.num_envs, env.n_drones, env.device
         W = env.layout.obs_window
         D = W * W * 6
         self.env, self.seg, self.parallel, self.E = env, seg, parallel, E
+        # input "code": the step writes drone 0's policy code instead of the
+        # f32 observation (128 B per env instead of 1,176), the act reads it
+        # (f32 nets; Q to 1e-5 of the f32 forward) and the replay buffer
+        # stores code rows, decoding the rows it samples to the observation
+        self.input = input
         self.fused = fused and not parallel
         # parallel branches need 3 rotating buffers (see above); on one stream 2
         # suffice, and the third 77 MB observation buffer costs MALL hits (C3
         # loop 79.4 vs 74.4 us per step)
         self.NB = 3 if parallel else 2
         self.net = net or QNetwork(D, (128, 64), device=dev, generator=torch.Generator().manual_seed(0),
-                                   precision=precision)
-        self.rb = rb or ReplayBuffer(10000, D, dev)
+                                   precision=precision, input=input)
+        self.rb = rb or ReplayBuffer(10000, D, dev, code_radius=env.params.window_radius if input == "code" else 0)
         self.acts = [torch.empty((E, N), dtype=torch.int32, device=dev) for _ in range(self.NB)]
         self.rewards = [torch.empty((E, N), dtype=torch.float32, device=dev) for _ in range(self.NB)]
         self.dones = [torch.empty((E, N), dtype=torch.uint8, device=dev) for _ in range(self.NB)]
-        self.obs = [torch.empty((E, 1, W, W, 6), dtype=torch.float32, device=dev) for _ in range(self.NB)]
-        env.get_obs(1, out=self.obs[0])
+        if input == "code":
+            self.obs = self.code = [env.new_code() for _ in range(self.NB)]
+        else:
+            self.obs = [torch.empty((E, 1, W, W, 6), dtype=torch.float32, device=dev) for _ in range(self.NB)]
+        self._first_obs()
         self.s_syn, self.s_rep = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def _first_obs(self):
+        if self.input == "code":
+            self.env.get_code(out=self.code[0])
+        else:
+            self.env.get_obs(1, out=self.obs[0])
 
     def _synth(self, t):
         self.env.synth_actions(seed=2024, step=t, out=self.acts[t % self.NB])
 
     def _act_step(self, t):
         b, nb = t % self.NB, (t + 1) % self.NB
-        self.net.act(self.obs[b].reshape(self.E, -1), 0.1, seed=7, step=t, env_offset=self.env.env_offset,
+        x = self.code[b] if self.input == "code" else self.obs[b].reshape(self.E, -1)
+        self.net.act(x, 0.1, seed=7, step=t, env_offset=self.env.env_offset,
                      actions=self.acts[b], synth=(2024, t) if self.fused else None)
-        self.env.step(self.acts[b], obs_k=1, rewards=self.rewards[b], dones=self.dones[b], obs=self.obs[nb],
-                      obs_stream=LOOP_OBS_STREAM)  # None: env.step()'s default
+        if self.input == "code":
+            self.env.step(self.acts[b], rewards=self.rewards[b], dones=self.dones[b], code=self.code[nb])
+        else:
+            self.env.step(self.acts[b], obs_k=1, rewards=self.rewards[b], dones=self.dones[b], obs=self.obs[nb],
+                          obs_stream=LOOP_OBS_STREAM)  # None: env.step()'s default
 
     def _replay(self, t):
         b, nb = t % self.NB, (t + 1) % self.NB
@@ -490,17 +545,17 @@ class TrainSegment:
             main.wait_stream(self.s_syn)
             main.wait_stream(self.s_rep)
         self.env.reset(seed=None)
-        self.env.get_obs(1, out=self.obs[0])
+        self._first_obs()
 
 
 def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fused: bool = True,
-                     precision: str = "f32"):
+                     precision: str = "f32", input: str = "obs"):
     """TrainSegment captured once as a HIP graph (no host work per step) and
     replayed.  Counters (action stream step, epsilon draws, replay cursor) are
     baked into the capture, so replays repeat them: the work per step is the
     same, the action stream repeats every segment."""
     dev = env.device
-    loop = TrainSegment(env, seg, parallel=parallel, fused=fused, precision=precision)
+    loop = TrainSegment(env, seg, parallel=parallel, fused=fused, precision=precision, input=input)
     side = torch.cuda.Stream(dev)
     side.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(side):
@@ -524,9 +579,19 @@ def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fus
     branches = ("synthetic actions and replay add_many on parallel graph branches, 3 rotating buffers"
                 if parallel else "one stream" + ("; synthetic actions inside the act launch" if fused else ""))
     return {"env_steps_per_s": E * seg * reps / dt, "us_per_step": dt / (seg * reps) * 1e6,
-            "segments": reps, "steps_per_segment": seg, "precision": precision,
-            "loop": f"hipGraph of {seg} x [synth actions -> qnet act (drone 0, {precision}) -> step + obs(K=1) -> "
-                    f"replay add_many] + reset + obs, replayed {reps}x ({branches}; learner not included)"}
+            "segments": reps, "steps_per_segment": seg, "precision": precision, "input": input,
+            "loop": f"hipGraph of {seg} x [synth actions -> qnet act (drone 0, {precision}, input {input}) -> "
+                    f"step + {'drone 0 policy code' if input == 'code' else 'obs(K=1)'} -> "
+                    f"replay add_many{' (code rows)' if input == 'code' else ''}] + reset + obs, replayed {reps}x "
+                    f"({branches}; learner not included)"}
+
+
+def loop_input(args, env) -> str:
+    """--loop-input auto: the policy code wherever a code-input net applies
+    (f32 precision, a 5x5, 7x7 or 9x9 window)."""
+    if args.loop_input != "auto":
+        return args.loop_input
+    return "code" if args.loop_precision == "f32" and env.layout.obs_window in (5, 7, 9) else "obs"
 
 
 def refill_plan(pre: int, warmup: int, steps: int, every: int):
@@ -734,6 +799,9 @@ def main():
     ap.add_argument("--no-dqn", action="store_true", help="skip the DQN-consumer measurement (SURVEY.md §8 F1)")
     ap.add_argument("--loop-precision", default="f32", choices=("f32", "bf16"),
                     help="Q-network arithmetic of the DQN loops (f32: the reference's nets; bf16 reported beside)")
+    ap.add_argument("--loop-input", default="auto", choices=("auto", "obs", "code"),
+                    help="the DQN loops' act input: the f32 observation or drone 0's policy code (f32 nets, 5x5..9x9 "
+                         "windows); auto = code where it applies")
     ap.add_argument("--rollout-chunk", type=int, default=100,
                     help="steps per drl_rollout launch for the rollout measurement (0 = skip)")
     ap.add_argument("--loop-segments", type=int, default=3,
@@ -825,7 +893,7 @@ def main():
     dqn = None
     if K >= 1 and not args.no_dqn:
         dqn = dqn_consumer_bench(env, actions, rewards, dones, obs, args.warmup, min(args.steps, 200), stream,
-                                 args.loop_precision)
+                                 args.loop_precision, loop_input(args, env))
 
     roll = None
     if args.rollout_chunk > 0:
@@ -840,7 +908,7 @@ def main():
     loop = None
     if args.loop_segments > 0 and not args.no_dqn and K >= 1:
         loop = train_loop_bench(env, args.loop_segments, parallel=args.parallel_loop, fused=not args.unfused_act,
-                                precision=args.loop_precision)
+                                precision=args.loop_precision, input=loop_input(args, env))
         loop["env_steps_per_s"] = min_over_ranks(loop["env_steps_per_s"], world) * world
         loop["n_gpus"] = world
     del runner, actions, rewards, dones, obs, env

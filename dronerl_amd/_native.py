@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # DRL_LIB: an alternative build of the same library (tools/variants.py A/B runs)
 LIB_PATH = os.environ.get("DRL_LIB") or os.path.join(_HERE, "libdronerl.so")
 
-DRL_ABI_VERSION = 6  # include/dronerl.h
+DRL_ABI_VERSION = 7  # include/dronerl.h
 DRL_MT_WORDS = 1776  # per-env RNG row: two MT blocks + the respawn-candidate ring
 DRL_MT_RING = 1248
 DRL_MT_RING_END = 1760
@@ -31,12 +31,15 @@ DRL_STEP_REFILL = 2      # drl_step_ex flag: top up the respawn-candidate rings 
 # Every symbol include/dronerl.h declares (tests check the .so exports them all).
 EXPORTS = ["drl_abi_version", "drl_last_error", "drl_side_from_density", "drl_layout_query", "drl_reset",
            "drl_step", "drl_step_ex", "drl_rollout", "drl_refill", "drl_mt_get", "drl_mt_set", "drl_obs", "drl_grid_obs", "drl_decode", "drl_encode", "drl_synth_actions",
+           # the policy code (drone 0's window, one u16 per cell) for drl_qnet_act_code
+           "drl_policy_code_bytes", "drl_step_code", "drl_obs_code", "drl_code_decode",
            # library-owned env handles
            "drl_env_create", "drl_env_destroy", "drl_env_seed", "drl_env_reset", "drl_env_step",
            "drl_env_step_obs", "drl_env_obs", "drl_env_grid_obs", "drl_env_get_state", "drl_env_set_state", "drl_env_state",
            "drl_env_errors",
            # DQN consumer
-           "drl_qnet_packed_bytes", "drl_qnet_pack", "drl_qnet_act", "drl_qnet_act_synth", "drl_replay_add"]
+           "drl_qnet_packed_bytes", "drl_qnet_pack", "drl_qnet_act", "drl_qnet_act_synth", "drl_qnet_act_code",
+           "drl_replay_add"]
 
 
 class DrlParams(ctypes.Structure):
@@ -111,12 +114,17 @@ def lib():
     L.drl_mt_get.argtypes = [P, S, vp, vp]
     L.drl_mt_set.argtypes = [P, S, vp, vp, vp]
     L.drl_obs.argtypes = [P, S, i32, vp, vp]
+    L.drl_obs_code.argtypes = [P, S, i32, vp, vp, vp]
+    L.drl_step_code.argtypes = [P, S, vp, vp, vp, vp, i32, vp, vp, ctypes.c_uint32, vp]
+    L.drl_code_decode.argtypes = [i32, vp, i64, vp, vp]
+    L.drl_policy_code_bytes.argtypes = [i32]
+    L.drl_policy_code_bytes.restype = i32
     L.drl_grid_obs.argtypes = [P, S, vp, vp]
     L.drl_decode.argtypes = [P, S, vp, vp, vp, vp, vp, vp]
     L.drl_encode.argtypes = [P, S, vp, vp, vp, vp, vp, vp]
     L.drl_synth_actions.argtypes = [u64, u64, i64, i64, i32, vp, vp]
     for f in ["drl_layout_query", "drl_reset", "drl_step", "drl_step_ex", "drl_rollout", "drl_refill", "drl_mt_get", "drl_mt_set", "drl_obs", "drl_grid_obs", "drl_decode", "drl_encode",
-              "drl_synth_actions"]:
+              "drl_synth_actions", "drl_obs_code", "drl_step_code", "drl_code_decode"]:
         getattr(L, f).restype = ctypes.c_int
     if L.drl_abi_version() != DRL_ABI_VERSION:
         raise DroneRLError("libdronerl.so ABI version mismatch; rebuild it")

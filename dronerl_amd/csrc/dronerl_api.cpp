@@ -339,6 +339,38 @@ int drl_step(const drl_params* p, const drl_state* s, const int32_t* d_actions, 
 int drl_step_ex(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
                 uint8_t* d_dones, float* d_obs, int32_t obs_k, int32_t* d_err, uint32_t flags,
                 hipStream_t stream) {
+    return drl_step_code(p, s, d_actions, d_rewards, d_dones, d_obs, obs_k, nullptr, d_err, flags, stream);
+}
+
+// The policy code output of a step / obs launch: the wave's code rows are
+// staged in LDS (write_obs_wave<CODE>) -- in the scratch area, which holds
+// nothing else by then, when no f32 observation needs its transpose stage
+// there (no extra LDS: the C3 step keeps its 32 waves per CU), else after the
+// wave's LDS.
+static int set_code(const drl_params* p, drl::StepArgs* a, void* d_code, const drl_layout& L, bool with_obs) {
+    if ((uintptr_t)d_code % 16) return fail("code must be 16-byte aligned");
+    a->code = static_cast<uint4*>(d_code);
+    const int P = L.step_group_lanes, gpw = 64 / P;
+    const int need = gpw * drl::lay::code_bytes(L.obs_window);
+    const int stage = gpw * env_lds(L.ground_stride, L.cells, p->n_drones, 1, L.obs_window, P).fixed;
+    if (!with_obs && stage % 16 == 0 && a->wave_lds - stage >= need) {
+        a->code_lds = stage;
+    } else {
+        a->code_lds = (a->wave_lds + 15) / 16 * 16;  // (16-B LDS reads and writes)
+        a->wave_lds = a->code_lds + need;
+    }
+    if (a->wave_lds > kLdsMax) return fail("the policy code needs %d B of LDS per wave", a->wave_lds);
+    return 0;
+}
+
+int32_t drl_policy_code_bytes(int32_t window_radius) {
+    if (window_radius < 1 || window_radius > DRL_MAX_RADIUS) return -1;
+    return drl::lay::code_bytes(2 * window_radius + 1);
+}
+
+int drl_step_code(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
+                  uint8_t* d_dones, float* d_obs, int32_t obs_k, void* d_code, int32_t* d_err, uint32_t flags,
+                  hipStream_t stream) {
     drl_layout L;
     if (flags & ~(DRL_STEP_OBS_STREAM | DRL_STEP_REFILL)) return fail("unknown drl_step flags 0x%x", flags);
     if (validate(p, &L) || check_state(s, L)) return -1;
@@ -346,16 +378,19 @@ int drl_step_ex(const drl_params* p, const drl_state* s, const int32_t* d_action
     if (!d_actions || !d_rewards || !d_dones) return fail("actions/rewards/dones must be non-NULL");
     if (d_obs && (obs_k < 1 || obs_k > p->n_drones)) return fail("obs_k %d outside [1, n_drones]", obs_k);
     if (d_obs && ((uintptr_t)d_obs % 16)) return fail("obs must be 16-byte aligned");
-    drl::StepArgs a = step_args(p, s, L, d_obs ? obs_k : 0);
+    // (d_obs NULL with d_code: the code alone, drone index 0's window geometry)
+    const int k = d_obs ? obs_k : (d_code ? 1 : 0);
+    drl::StepArgs a = step_args(p, s, L, k);
     if (a.wave_lds > kLdsMax) return fail("obs_k %d needs %d B of LDS per wave", obs_k, a.wave_lds);
     a.actions = d_actions;
     a.rewards = d_rewards;
     a.dones = d_dones;
     a.obs = d_obs;
     a.err = d_err;
-    a.og = obs_geom(p, L, d_obs ? obs_k : 1);
+    a.og = obs_geom(p, L, k ? k : 1);
     a.obs_nt = (flags & DRL_STEP_OBS_STREAM) ? 1 : 0;
     a.dones_packed = dones_packed(p, d_dones, 0, a);
+    if (d_code && set_code(p, &a, d_code, L, d_obs != nullptr)) return -1;
     hipError_t e = drl::launch_step(a, L.step_group_lanes, stream, drl::kStepMode);
     if (e != hipSuccess) return hip_fail(e, "drl_step launch");
     return (flags & DRL_STEP_REFILL) ? launch_refill(p, s, stream) : 0;
@@ -421,16 +456,22 @@ int drl_rollout(const drl_params* p, const drl_state* s, int32_t num_steps, cons
 }
 
 int drl_obs(const drl_params* p, const drl_state* s, int32_t k, float* d_obs, hipStream_t stream) {
+    return drl_obs_code(p, s, k, d_obs, nullptr, stream);
+}
+
+int drl_obs_code(const drl_params* p, const drl_state* s, int32_t k, float* d_obs, void* d_code, hipStream_t stream) {
     drl_layout L;
     if (validate(p, &L) || check_state(s, L)) return -1;
     if (s->num_envs == 0) return 0;
-    if (!d_obs) return fail("obs is NULL");
+    if (!d_obs && !d_code) return fail("obs is NULL");
+    if (!d_obs) k = 1;  // the code alone: drone index 0's window
     if (k < 1 || k > p->n_drones) return fail("k %d outside [1, n_drones]", k);
     if ((uintptr_t)d_obs % 16) return fail("obs must be 16-byte aligned");
     drl::StepArgs a = step_args(p, s, L, k);
     if (a.wave_lds > kLdsMax) return fail("k %d needs %d B of LDS per wave", k, a.wave_lds);
     a.obs = d_obs;
     a.og = obs_geom(p, L, k);
+    if (d_code && set_code(p, &a, d_code, L, d_obs != nullptr)) return -1;
     hipError_t e = drl::launch_step(a, L.step_group_lanes, stream, drl::kObsMode);
     return e == hipSuccess ? 0 : hip_fail(e, "drl_obs launch");
 }
@@ -453,6 +494,16 @@ int drl_grid_obs(const drl_params* p, const drl_state* s, float* d_grid, hipStre
     hipError_t e = drl::launch_grid_obs(s->ground, s->drones, s->num_envs, p->side, p->n_drones, L.ground_stride, d_grid,
                                         stream);
     return e == hipSuccess ? 0 : hip_fail(e, "drl_grid_obs launch");
+}
+
+int drl_code_decode(int32_t window_radius, const void* d_code, int64_t n, float* d_obs, hipStream_t stream) {
+    if (window_radius < 1 || window_radius > DRL_MAX_RADIUS) return fail("window_radius outside [1, %d]", DRL_MAX_RADIUS);
+    if (n < 0) return fail("n < 0");
+    if (n == 0) return 0;
+    if (!d_code || !d_obs) return fail("code / obs is NULL");
+    if ((uintptr_t)d_code % 2 || (uintptr_t)d_obs % 8) return fail("code must be 2-byte and obs 8-byte aligned");
+    hipError_t e = drl::launch_code_decode(d_code, n, 2 * window_radius + 1, d_obs, stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_code_decode launch");
 }
 
 int drl_encode(const drl_params* p, const drl_state* s, const int32_t* d_order, const int32_t* d_y, const int32_t* d_x,

@@ -99,6 +99,14 @@ constexpr int bit_length(int v) { return v ? 1 + bit_length(v >> 1) : 0; }
 #ifndef DRL_QN_WAVES
 #define DRL_QN_WAVES 8
 #endif
+// policy code of a W x W window (write_code_wave, the DRL_QNET code input):
+// 4 groups of code_cpg cells, each padded to code_cpg8 u16 (16-B vectors)
+constexpr int code_cpg(int W) { return (W * W + 3) / 4; }
+constexpr int code_cpg8(int W) { return (code_cpg(W) + 7) / 8 * 8; }
+constexpr int code_bytes(int W) { return 4 * code_cpg8(W) * 2; }
+// layer 0's K-slices of a code-input net: 6 channels x code_cpg slots per lane group, 8 per slice, padded to the
+// act kernels' slice ring
+constexpr int code_kt(int W) { return ((6 * code_cpg(W) + 7) / 8 + DRL_QN_RING - 1) / DRL_QN_RING * DRL_QN_RING; }
 constexpr int qn_ring = DRL_QN_RING;    // act kernel: K-slices in flight per wave (layer-0 slices padded to a multiple)
 constexpr int qn_waves = DRL_QN_WAVES;  // act kernel: waves per workgroup (one workgroup per CU)
 #ifndef DRL_QN_TILES
@@ -160,6 +168,8 @@ struct StepArgs {
     int obs_nt;     // drl_step: 1 = streaming (non-temporal) observation stores (DRL_STEP_OBS_STREAM)
     int specialize; // 1: use a compile-time-geometry instance when one matches (DRL_SPECIALIZE=0 disables)
     int dones_packed; // 1: dones written as dwords (n_drones % 4 == 0, 4-B aligned rows and step strides)
+    uint4* code;      // nullable: drone 0's policy code (lay::code_bytes(W) per env), written with the observation
+    int code_lds;     // byte offset of the wave's code-row staging in its LDS (code non-NULL)
     uint32_t max_rounds;
     FastDiv div_side;
     ObsGeom og;
@@ -215,6 +225,7 @@ struct QnetLayout {
     int frag_src[QN_MAX_LAYERS];  // the pack kernel's contiguous element numbering of the hi fragments
     int bias_vec;                 // uint4 offset of the biases
     int lo0_lds;                  // F32: layer 0's hi and lo fragments are the LDS image (the rest is global)
+    int code_w;                   // > 0: DRL_QNET_INPUT_CODE net of a code_w x code_w window
 };
 
 struct QnetPack {
@@ -229,6 +240,7 @@ struct QnetPack {
     int precision;
     int frag_lo_off[QN_MAX_LAYERS];  // F32: lo fragments, uint4 offsets from packed_w
     int frag_src[QN_MAX_LAYERS];     // contiguous numbering of the hi elements (uint4 units) -> frag_off
+    int code_w;                      // > 0: layer 0 in the policy code's K order for a code_w x code_w window
 };
 
 struct QnetArgs {
@@ -250,6 +262,7 @@ struct QnetArgs {
     int synth_n;                    // > 1: also write drl_synth_actions' columns 1..synth_n-1
     uint64_t synth_seed, synth_step;
     int32_t* err;                   // F32: DRL_ERR_QNET_RANGE when an operand leaves fp16's range (nullable)
+    int total_bytes;                // bytes of the packed net (code act: buffer loads of the later layers)
 };
 
 struct ReplayArgs {
@@ -274,6 +287,7 @@ struct ReplayArgs {
 
 hipError_t launch_qnet_pack(const QnetPack& p, hipStream_t s);
 hipError_t launch_qnet_act(const QnetArgs& a, int num_cus, hipStream_t s);
+hipError_t launch_qnet_act_code(const QnetArgs& a, int window, int num_cus, hipStream_t s);
 hipError_t launch_replay_add(const ReplayArgs& a, hipStream_t s);
 
 enum StepMode : int { kStepMode = 0, kObsMode = 1, kRolloutMode = 2 };
@@ -281,6 +295,7 @@ hipError_t launch_step(const StepArgs& a, int P, hipStream_t s, int mode);
 hipError_t launch_reset(const ResetArgs& a, hipStream_t s);
 hipError_t launch_decode(const uint32_t* drones, int64_t E, int N, int32_t* order, int32_t* y, int32_t* x,
                          int32_t* c, uint8_t* k, hipStream_t s);
+hipError_t launch_code_decode(const void* code, int64_t n, int W, float* obs, hipStream_t s);
 hipError_t launch_grid_obs(const uint8_t* ground, const uint32_t* drones, int64_t E, int side, int N, int gstride,
                            float* out, hipStream_t s);
 hipError_t launch_encode(uint32_t* drones, int64_t E, int N, const int32_t* order, const int32_t* y,

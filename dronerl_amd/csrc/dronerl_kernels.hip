@@ -380,9 +380,17 @@ __device__ __forceinline__ void lds_zero(T* p, int nbytes, int lane) {
 // (true f32 division, == f32(double c/100)), ch5 skyscraper or wall.
 // `base` is the wave's first observation float (16-B aligned unless a wave
 // holds one env with an odd K*W*W).
-template <bool NT = false, class GEO>
+// CODE: also store drone 0's policy code (include/dronerl.h drl_step_code;
+// `code` = the wave's first env's code row): each lane of a k = 0 cell puts
+// its u16 (object | air << 3) at its group slot of an LDS copy of the wave's
+// code rows (`cst`, zeroed first: the padding), and the rows leave as 16-B
+// stores after the last pass.  F32 = false: the code alone (no f32
+// observation; `base` unused).
+template <bool NT = false, bool CODE = false, bool F32 = true, class GEO>
 __device__ __forceinline__ void write_obs_wave(float* __restrict__ base, int nenv_w, const GEO& g, const WaveLds& w,
-                                               bool obs_wide, int lane) {
+                                               bool obs_wide, int lane, uint16_t* __restrict__ code = nullptr,
+                                               l_u16* cst = nullptr) {
+    static_assert(CODE || F32, "nothing to write");
     const uint32_t W = g.W();
     const uint32_t win = W * W;
     const uint32_t env_cells = g.env_cells();  // K * W*W
@@ -390,6 +398,11 @@ __device__ __forceinline__ void write_obs_wave(float* __restrict__ base, int nen
     const int G = g.side(), R = g.radius();
     const uint32_t gstride = (uint32_t)g.gstride(), np = (uint32_t)g.np(), lpaint = (uint32_t)g.lds_paint();
     const bool wide = obs_wide && ((uintptr_t)base & 15u) == 0;
+    const int cpg = lay::code_cpg((int)W), cpg8 = lay::code_cpg8((int)W);
+    if constexpr (CODE) {
+        lds_zero(cst, nenv_w * 8 * cpg8, lane);
+        wave_sync();
+    }
     for (uint32_t q0 = 0; q0 < ncell; q0 += 64 * OBS_U) {
         uint32_t e[OBS_U], rem[OBS_U], wy[OBS_U], wx[OBS_U], pos[OBS_U];
 #pragma unroll
@@ -414,6 +427,13 @@ __device__ __forceinline__ void write_obs_wave(float* __restrict__ base, int nen
             const uint32_t o = w.gl[e[u] * gstride + (uint32_t)(in ? y * G + x : 0)];
             const uint32_t obj = in ? o : (uint32_t)OBJ_SKYSCRAPER;
             const uint32_t air = w.paint[e[u] * lpaint + rem[u]];
+            if constexpr (CODE) {
+                if (rem[u] < win) {  // drone index 0's window (k = 0)
+                    const uint32_t cl = rem[u], grpc = cl / (uint32_t)cpg;
+                    cst[e[u] * (uint32_t)(4 * cpg8) + grpc * (uint32_t)(cpg8 - cpg) + cl] = (uint16_t)(obj | (air << 3));
+                }
+            }
+            if constexpr (!F32) continue;
             v[u][0].x = air ? 1.0f : 0.0f;
             v[u][0].y = (obj == OBJ_PACKET || (air & 0x80u)) ? 1.0f : 0.0f;
             v[u][1].x = obj == OBJ_DROPZONE ? 1.0f : 0.0f;
@@ -421,6 +441,7 @@ __device__ __forceinline__ void write_obs_wave(float* __restrict__ base, int nen
             v[u][2].x = air ? div100((int)(air & 0x7fu) - 1) : 0.0f;
             v[u][2].y = obj == OBJ_SKYSCRAPER ? 1.0f : 0.0f;
         }
+        if constexpr (!F32) continue;
         if (wide) {
             // transpose through LDS: lane u*64+l's 24 B at stage[(u*64+l)*24], then 16-B stores
             l_f2* st = reinterpret_cast<l_f2*>(w.stage);
@@ -462,6 +483,28 @@ __device__ __forceinline__ void write_obs_wave(float* __restrict__ base, int nen
             }
         }
     }
+    if constexpr (CODE) {  // the wave's code rows: nenv_w * cpg8 / 2 16-B vectors
+        wave_sync();
+        const l_u4* cv = reinterpret_cast<const l_u4*>(cst);
+        uint4* dst = reinterpret_cast<uint4*>(code);
+        for (int v = lane; v < nenv_w * cpg8 / 2; v += 64) {
+            const u32x4 x = cv[v];
+            dst[v] = make_uint4(x[0], x[1], x[2], x[3]);
+        }
+    }
+}
+
+// Policy code (include/dronerl.h drl_step_code): drone index 0's window as one
+// u16 per cell -- object code (bits 0-2; walls read as skyscrapers) | air byte
+// << 3 ((charge+1) | carry << 7, 0 = no drone) -- in 4 groups of
+// lay::code_cpg(W) cells, each padded to code_cpg8 (zero codes), so an act
+// kernel lane group reads its group with 16-B loads.  The WindowedGridView
+// channels are the same functions of (object, air) the observation writer
+// uses (wrappers.py:10-31), so a policy that builds its inputs from the code
+// sees the observation's values exactly.  Written by write_obs_wave<CODE>.
+template <class GEO>
+__device__ __forceinline__ uint16_t* code_row(const StepArgs& a, int64_t wenv0, const GEO& g) {
+    return reinterpret_cast<uint16_t*>(a.code) + wenv0 * (int64_t)(4 * lay::code_cpg8((int)g.W()));
 }
 
 // Each drone paints its air byte into every observed window (drone indices
@@ -554,7 +597,9 @@ __device__ __forceinline__ void for_other_lanes(int v, F&& f) {
 // them -- ground in LDS, drone records in the scratch area (O order) and the
 // MT index in a register -- and written back once at the end; the actions of
 // step t+1 are loaded during step t.  NT: streaming observation stores.
-template <int P, class GEO, bool ROLL, bool NT>
+// CODE: also write drone 0's policy code (a separate instance: the code
+// writer's registers would otherwise spill in the plain step at 64 VGPRs).
+template <int P, class GEO, bool ROLL, bool NT, bool CODE = false>
 __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     using GMask = typename GMaskT<P>::type;
     constexpr int GPW = 64 / P;
@@ -589,7 +634,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
 #pragma unroll
     for (int e = 0; e < GPW; ++e) mi[e] = a.mt_index[wenv0 + min(e, nenv_w - 1)];
     lds_zero(W.bm, GPW * g.lds_bm(), lane0);
-    if (GEO::kObs && a.obs) lds_zero(W.paint, GPW * g.lds_paint(), lane0);
+    if (GEO::kObs && (a.obs || CODE)) lds_zero(W.paint, GPW * g.lds_paint(), lane0);
     if (lane0 < GPW) W.cnt[lane0 * 4] = 0u;
     wave_sync();
     const bool active0 = env_ok0 && j0 < N;
@@ -1143,12 +1188,19 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
 #endif
     }
     DRL_STAMP(5);
-    if (GEO::kObs && a.obs) {
+    if (GEO::kObs && (a.obs || (CODE && !ROLL))) {
         if (active) paint_windows(W.paint + grp * g.lds_paint(), posidx, (int)py, (int)px,
                                   (uint8_t)((c + 1) | (carry << 7)), g);
         wave_sync();
-        write_obs_wave<NT>(a.obs + t * a.obs_tstride + wenv0 * (int64_t)(6u * g.env_cells()), nenv_w, g, W,
-                             a.obs_wide, lane);
+        float* obase = a.obs + t * a.obs_tstride + wenv0 * (int64_t)(6u * g.env_cells());
+        if constexpr (CODE && !ROLL) {
+            uint16_t* crow = code_row(a, wenv0, g);
+            l_u16* cst = reinterpret_cast<l_u16*>((l_u8*)smem + a.code_lds);
+            if (a.obs) write_obs_wave<NT, true, true>(obase, nenv_w, g, W, a.obs_wide, lane, crow, cst);
+            else write_obs_wave<NT, true, false>(obase, nenv_w, g, W, a.obs_wide, lane, crow, cst);
+        } else {
+            write_obs_wave<NT>(obase, nenv_w, g, W, a.obs_wide, lane);
+        }
     }
     DRL_STAMP(6);
     if constexpr (ROLL) {  // records to the stash (the observation stage aliased it until here)
@@ -1187,11 +1239,12 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t orig, uint32_t n) {
 // One wave per batch of GPW envs.  (Persistent waves looping over 2-4 batches
 // were measured slower at C3/C4/C5: halving the resident waves costs more
 // latency hiding than the longer waves gain in balance.)
-// NT: streaming observation stores (DRL_STEP_OBS_STREAM).
-template <int P, class GEO, bool NT>
+// NT: streaming observation stores (DRL_STEP_OBS_STREAM).  CODE: with the
+// policy code (drl_step_code).
+template <int P, class GEO, bool NT, bool CODE = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : 1, 8)))
 drl_step_kernel(StepArgs a) {
-    step_batch<P, GEO, false, NT>(a, (int64_t)xcd_block(blockIdx.x, gridDim.x) * (64 / P));
+    step_batch<P, GEO, false, NT, CODE>(a, (int64_t)xcd_block(blockIdx.x, gridDim.x) * (64 / P));
 }
 
 // drl_rollout: a.steps steps per launch, same wave layout (P >= 16).
@@ -1228,7 +1281,12 @@ __global__ void __launch_bounds__(64) drl_obs_kernel(StepArgs a) {
     wave_sync();
     if (active) paint_windows(W.paint + grp * g.lds_paint(), posidx, y, x, (uint8_t)((c + 1) | (carry << 7)), g);
     wave_sync();
-    write_obs_wave(a.obs + wenv0 * (int64_t)(6u * g.env_cells()), nenv_w, g, W, a.obs_wide, lane);
+    float* obase = a.obs + wenv0 * (int64_t)(6u * g.env_cells());
+    uint16_t* crow = a.code ? code_row(a, wenv0, g) : nullptr;
+    l_u16* cst = reinterpret_cast<l_u16*>((l_u8*)smem + a.code_lds);
+    if (!a.code) write_obs_wave(obase, nenv_w, g, W, a.obs_wide, lane);
+    else if (a.obs) write_obs_wave<false, true, true>(obase, nenv_w, g, W, a.obs_wide, lane, crow, cst);
+    else write_obs_wave<false, true, false>(obase, nenv_w, g, W, a.obs_wide, lane, crow, cst);
 }
 
 // ------------------------------------------------------------------ reset ---
@@ -2138,6 +2196,9 @@ static hipError_t launch_step_t(const StepArgs& a, hipStream_t s, int mode) {
     } else if (mode == kRolloutMode) {
         if constexpr (P >= kRolloutNoObsMinLanes) hipLaunchKernelGGL((drl_rollout_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
         else return hipErrorInvalidValue;
+    } else if (GEO::kObs && a.code) {  // (obs NULL: the code alone)
+        if (a.obs_nt) hipLaunchKernelGGL((drl_step_kernel<P, GEO, GEO::kObs, GEO::kObs>), grid, block, a.wave_lds, s, a);
+        else hipLaunchKernelGGL((drl_step_kernel<P, GEO, false, GEO::kObs>), grid, block, a.wave_lds, s, a);
     } else if (GEO::kObs && a.obs && a.obs_nt) {
         hipLaunchKernelGGL((drl_step_kernel<P, GEO, GEO::kObs>), grid, block, a.wave_lds, s, a);
     } else {
@@ -2206,6 +2267,31 @@ hipError_t launch_grid_obs(const uint8_t* ground, const uint32_t* drones, int64_
                            float* out, hipStream_t s) {
     hipLaunchKernelGGL(drl_grid_obs_kernel, dim3((unsigned)E), dim3(256), (size_t)side * side, s, ground, drones, side,
                        N, gstride, out);
+    return hipGetLastError();
+}
+
+// Policy code -> observation (drl_code_decode): one thread per (row, cell),
+// the channels of write_obs_wave from (object, air).
+__global__ void __launch_bounds__(256) drl_code_decode_kernel(const uint16_t* __restrict__ code, int64_t n, int W,
+                                                              int64_t code_stride, float* __restrict__ obs) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int cells = W * W;
+    if (i >= n * cells) return;
+    const int64_t row = i / cells;
+    const int cl = (int)(i - row * cells);
+    const int cpg = lay::code_cpg(W), cpg8 = lay::code_cpg8(W), grp = cl / cpg;
+    const uint32_t h = code[row * code_stride + grp * cpg8 + (cl - grp * cpg)];
+    const uint32_t obj = h & 7u, air = h >> 3;
+    float2* o = reinterpret_cast<float2*>(obs + i * 6);
+    o[0] = make_float2(air ? 1.0f : 0.0f, (obj == OBJ_PACKET || (air & 0x80u)) ? 1.0f : 0.0f);
+    o[1] = make_float2(obj == OBJ_DROPZONE ? 1.0f : 0.0f, obj == OBJ_STATION ? 1.0f : 0.0f);
+    o[2] = make_float2(air ? div100((int)(air & 0x7fu) - 1) : 0.0f, obj == OBJ_SKYSCRAPER ? 1.0f : 0.0f);
+}
+
+hipError_t launch_code_decode(const void* code, int64_t n, int W, float* obs, hipStream_t s) {
+    const int64_t total = n * W * W;
+    hipLaunchKernelGGL(drl_code_decode_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                       static_cast<const uint16_t*>(code), n, W, (int64_t)(lay::code_bytes(W) / 2), obs);
     return hipGetLastError();
 }
 

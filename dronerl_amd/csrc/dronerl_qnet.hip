@@ -58,8 +58,18 @@ __global__ void drl_qnet_pack_kernel(QnetPack p) {
         const int m = (int)(frag / kt), t = (int)(frag % kt);
         const int c = lane & 15, g = lane >> 4;
         const int row = 16 * m + c;
-        const int k = 32 * t + frag_k(g, j);
-        const float w = (row < p.out[l] && k < p.in[l]) ? p.w[l][(int64_t)row * p.in[l] + k] : 0.0f;
+        int k = 32 * t + frag_k(g, j);
+        if (l == 0 && p.code_w > 0) {  // the policy code's K order (drl_qnet_act_code_kernel)
+            const int cpg = lay::code_cpg(p.code_w), cells = p.code_w * p.code_w, sl = 8 * t + j;
+            const int lc = sl < 5 * cpg ? sl / 5 : sl - 5 * cpg;
+            const int ch = sl < 5 * cpg ? (sl % 5 < 4 ? sl % 5 : 5) : 4;
+            const bool ok = sl < 6 * cpg && lc < cpg && g * cpg + lc < cells;
+            k = ok ? (g * cpg + lc) * 6 + ch : p.in[l];  // (in[l]: a zero weight)
+        }
+        float w = (row < p.out[l] && k < p.in[l]) ? p.w[l][(int64_t)row * p.in[l] + k] : 0.0f;
+        // the charge channel's 1/100 moves into its weights: the kernel feeds
+        // the integer charge (exact in fp16), so no input needs an x_lo product
+        if (l == 0 && p.code_w > 0 && k < p.in[l] && k % 6 == 4) w /= 100.0f;
         if (p.precision == DRL_QNET_F32) {  // hi = fp16(w), lo = fp16((w - hi) * 2^11), lo after the LDS image
             const _Float16 hi = (_Float16)w;
             reinterpret_cast<_Float16*>(p.packed_w)[(int64_t)p.frag_off[l] * 8 + e] = hi;
@@ -537,6 +547,238 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_f32_kernel(QnetArg
     }
 }
 
+// ----------------------------------------------------- act from the code ---
+// drl_qnet_act_code: the f32 act with its input built from the policy code
+// the step wrote (write_obs_wave<CODE>: drone 0's window, one u16 per cell, 128 B
+// per env at radius 3) instead of read from the f32 observation (1,176 B per
+// env, 8-B-aligned rows read as strided 128-B slices): the input of a 16-env
+// tile is 2 KB, contiguous, and the kernel is no longer bound by the latency
+// of observation reads (C3: 77 MB per step).  The channels are computed from
+// (object, air) exactly as the observation writer computes them, so every
+// input value equals the observation's.
+// K order: lane group g owns the window cells of code group g; its slot s =
+// 8t + j of K-slice t holds, for s < 5 cpg, channel (s % 5 < 4 ? s % 5 : 5) of
+// cell s / 5 (the 0/1 channels), and for s in [5 cpg, 6 cpg) channel 4 (charge
+// / 100) of cell s - 5 cpg.  drl_qnet_pack packs layer 0's weights in the same
+// order (drl_qnet_desc.input = DRL_QNET_INPUT_CODE), with the charge
+// weights divided by 100 in f32: the kernel feeds the integer charge, so every
+// input (0, 1 or a charge <= 100) is exact in fp16 and needs no x_lo product,
+// two MFMAs per tile and slice (hi and lo weights) instead of three.  The
+// products differ from W * fl(c / 100) by the rounding of fl(W / 100) and
+// fl(c / 100), ~1e-7 relative: far inside the f32 act's 1e-5 bound.
+// One workgroup per CU (the net fills the LDS); the kernel's ~140 VGPRs leave
+// room for 3 waves per SIMD, so a workgroup runs up to 12 waves (the obs act's
+// 4 hide its observation reads behind a register ring instead).
+constexpr int QN_CODE_MAXW = 12;
+#ifndef DRL_QN_CODE_WAVES
+#define DRL_QN_CODE_WAVES 8
+#endif
+constexpr int QN_CODE_WAVES = DRL_QN_CODE_WAVES;
+
+__device__ __forceinline__ float code_channel(uint32_t code, int ch) {
+    const uint32_t obj = code & 7u, air = code >> 3;
+    switch (ch) {
+        case 0: return air ? 1.0f : 0.0f;
+        case 1: return (obj == OBJ_PACKET || (air & 0x80u)) ? 1.0f : 0.0f;
+        case 2: return obj == OBJ_DROPZONE ? 1.0f : 0.0f;
+        case 3: return obj == OBJ_STATION ? 1.0f : 0.0f;
+        case 4:  // the charge c itself (the observation holds c / 100; the packed weights carry the 1/100)
+            return air ? (float)((int)(air & 0x7fu) - 1) : 0.0f;
+        default: return obj == OBJ_SKYSCRAPER ? 1.0f : 0.0f;
+    }
+}
+
+template <int NT0, bool LO0, int WN>
+__global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(QnetArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint4 wl[];
+    constexpr int CPG = lay::code_cpg(WN), CPG8 = lay::code_cpg8(WN), CELLS = WN * WN;
+    constexpr int NV = CPG8 / 8;                 // 16-B code vectors per lane group
+    constexpr int NB = 5 * CPG;                  // slots of the 0/1 channels
+    constexpr int KP = lay::code_kt(WN);         // layer 0's K-slices (host: QnetLayout::kt[0])
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int c = lane & 15, g = lane >> 4;
+    constexpr int nt0 = NT0;
+    const int64_t ntiles = (a.E + 15) / 16;
+    const int64_t gstride = (int64_t)gridDim.x * nw;
+    constexpr float kLo = 1.0f / 2048.0f;
+    const int ncell_g = min(CPG, CELLS - g * CPG);  // this lane group's cells (the last group may hold fewer)
+    const uint4* const code = reinterpret_cast<const uint4*>(a.obs);
+    auto load_codes = [&](int64_t tile, uint32_t (&dst)[4 * NV]) __attribute__((always_inline)) {
+        const int64_t env = min(tile * 16 + c, a.E - 1);
+        const uint4* src = code + env * (4 * NV) + g * NV;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const uint4 q = src[v];
+            dst[4 * v + 0] = q.x;
+            dst[4 * v + 1] = q.y;
+            dst[4 * v + 2] = q.z;
+            dst[4 * v + 3] = q.w;
+        }
+    };
+    const int64_t grp0 = (int64_t)blockIdx.x * nw + wave;
+    int64_t grp = grp0;
+    uint32_t cw[4 * NV];
+    load_codes(grp < ntiles ? grp : 0, cw);
+    for (int v0 = wave * 64; v0 < a.lds_vec; v0 += 64 * nw)
+        if (v0 + lane < a.lds_vec)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(a.packed + v0 + lane),
+                                             (__attribute__((address_space(3))) void*)(wl + v0), 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    bool bad = false;
+    const float* bias = LO0 ? reinterpret_cast<const float*>(a.packed + a.bias_vec)
+                            : reinterpret_cast<const float*>(wl + a.frag_total);
+    const uint4* W0 = wl + a.frag_off[0];
+    const uint4* W0lo = LO0 ? wl + a.frag_lo_off[0] : a.packed + a.frag_lo_off[0];
+    // the later layers' fragments and biases: global (LO0, L2-resident) by
+    // buffer loads -- one VGPR of lane offset, the fragment offset in an SGPR
+    // (flat loads cost a 64-bit per-lane address each) -- or the LDS image
+    const auto pbuf = __builtin_amdgcn_make_buffer_rsrc((void*)a.packed, 0, a.total_bytes, 0x00020000);
+    const int lane16 = lane * 16;
+    auto frag_ld = [&](int frag_u4) __attribute__((always_inline)) {  // 64 lanes x 16 B at uint4 offset frag_u4
+        if constexpr (LO0) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(pbuf, lane16, frag_u4 * 16, 0);
+            uint4 r;
+            __builtin_memcpy(&r, &v, 16);
+            return r;
+        } else {
+            return wl[frag_u4 + lane];
+        }
+    };
+    auto bias4 = [&](int off) __attribute__((always_inline)) {  // biases off + 4g .. off + 4g + 3
+        f32x4 r;
+        if constexpr (LO0) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(pbuf, 16 * g, a.bias_vec * 16 + off * 4, 0);
+            __builtin_memcpy(&r, &v, 16);
+        } else {
+            const float* bp = bias + off + 4 * g;
+            r = f32x4{bp[0], bp[1], bp[2], bp[3]};
+        }
+        return r;
+    };
+
+    for (; grp < ntiles; grp += gstride) {
+        const int64_t ngrp = grp + gstride;
+        uint32_t ncw[4 * NV];  // the next tile's codes, in flight while this tile runs
+        load_codes(ngrp < ntiles ? ngrp : grp, ncw);
+        // the first K-slice of each layer starts its accumulators from an
+        // inline zero (no zeroing moves)
+        f32x4 acc[QN_MAXT], acl[QN_MAXT];
+        const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int t = 0; t < KP; ++t) {
+            const uint32_t* cs = cw;
+            f16x8 bh;  // every input is 0, 1 or an integer charge <= 100: exact in fp16
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int sl = 8 * t + j;  // compile-time slot
+                const int l = sl < NB ? sl / 5 : sl - NB;
+                const int ch = sl < NB ? (sl % 5 < 4 ? sl % 5 : 5) : 4;
+                float x = 0.0f;
+                if (sl < 6 * CPG) {
+                    const uint32_t cd = (cs[l >> 1] >> (16 * (l & 1))) & 0xffffu;
+                    x = l < ncell_g ? code_channel(cd, ch) : 0.0f;
+                }
+                bh[j] = (_Float16)x;
+            }
+            // the slice index through an opaque SGPR: a compile-time one lets
+            // LLVM hoist every fragment address (lane offset + constant, 160 of
+            // them) out of the tile loop into its own VGPR
+            int ts = t;
+            asm volatile("" : "+s"(ts));
+#pragma unroll
+            for (int m = 0; m < nt0; ++m) {
+                const f16x8 wh = as_f16x8(W0[(m * KP + ts) * 64 + lane]);
+                const f16x8 wo = as_f16x8(W0lo[(m * KP + ts) * 64 + lane]);
+                acc[m] = MFMA_F16(wh, bh, t == 0 ? z4 : acc[m], 0, 0, 0);
+                acl[m] = MFMA_F16(wo, bh, t == 0 ? z4 : acl[m], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4 * NV; ++i) cw[i] = ncw[i];
+        // ---- hidden layers and the output layer: as drl_qnet_act_f32_kernel
+        int nt_prev = nt0;
+        int bprev = a.bias_off[0];
+        for (int l = 1; l <= a.n_hidden; ++l) {
+            f16x8 ah[QN_MAXT / 2], al[QN_MAXT / 2];
+#pragma unroll
+            for (int s2 = 0; s2 < QN_MAXT / 2; ++s2) {
+                ah[s2] = al[s2] = f16x8{};  // (not carried across layers and tiles as undefined values)
+                if (2 * s2 < nt_prev) {
+                    const f32x4 b0 = bias4(bprev + 32 * s2), b1 = bias4(bprev + 32 * s2 + 16);
+                    float v[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int m = 2 * s2 + (j >> 2), i = j & 3;
+                        v[j] = fmaxf((acc[m][i] + acl[m][i] * kLo) + (j < 4 ? b0[i] : b1[i]), 0.0f);
+                    }
+                    split_f16(v, ah[s2], al[s2], bad);
+                }
+            }
+            const int nt_l = (l < a.n_hidden) ? a.nt[l] : 1;
+            const int kt = nt_prev / 2, ms = kt * 64;  // (ms: the fragment stride of an output tile)
+            const int fl = a.frag_off[l], flo = a.frag_lo_off[l];
+#pragma unroll
+            for (int t = 0; t < QN_MAXT / 2; ++t) {
+                if (t < kt) {
+#pragma unroll
+                    for (int m = 0; m < QN_MAXT; ++m) {
+                        if (m < nt_l) {
+                            const f16x8 wh = as_f16x8(frag_ld(fl + m * ms + t * 64));
+                            const f16x8 wo = as_f16x8(frag_ld(flo + m * ms + t * 64));
+                            acc[m] = MFMA_F16(wh, ah[t], t == 0 ? z4 : acc[m], 0, 0, 0);
+                            acl[m] = MFMA_F16(wh, al[t], t == 0 ? z4 : acl[m], 0, 0, 0);
+                            acl[m] = MFMA_F16(wo, ah[t], acl[m], 0, 0, 0);
+                        }
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            nt_prev = nt_l;
+            bprev = a.bias_off[l];
+        }
+        const f32x4 bq = bias4(bprev);
+        float q[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float own = (acc[0][i] + acl[0][i] * kLo) + bq[i];
+            const float hi = __shfl(own, c + 16);
+            q[i] = own;
+            q[i + 4] = hi;
+        }
+        const int64_t env = grp * 16 + c;
+        if (g == 0 && env < a.E) {
+            int best = 0;
+            for (int i = 1; i < a.n_actions; ++i) best = q[i] > q[best] ? i : best;
+            const uint64_t ge = (uint64_t)(a.env_offset + env);
+            const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (ge << 8) ^ 0xa5ull));
+            const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
+            const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
+            a.actions[env * a.action_stride] = (u < a.epsilon) ? rnd : best;
+            if (a.q)
+                for (int i = 0; i < a.n_actions; ++i) a.q[env * a.n_actions + i] = q[i];
+        }
+    }
+    if (__ballot(bad) && lane == 0 && a.err) atomicOr(a.err, DRL_ERR_QNET_RANGE);
+    if (a.synth_n > 1) {  // as in drl_qnet_act_kernel (one 16-env tile per group)
+        const uint32_t nd = (uint32_t)a.synth_n - 1u;
+        const uint32_t per = 16u * nd;
+        for (int64_t gg = grp0; gg < ntiles; gg += gstride) {
+            for (uint32_t k = (uint32_t)lane; k < per; k += 64u) {
+                const uint32_t el = k / nd;
+                const int64_t env = 16 * gg + el;
+                const uint64_t drone = 1u + (k - el * nd);
+                if (env < a.E) {
+                    const uint64_t ctr = (a.synth_step << 40) ^ ((uint64_t)(a.env_offset + env) << 8) ^ drone;
+                    const uint64_t h = qn_splitmix64(a.synth_seed ^ qn_splitmix64(ctr));
+                    a.actions[env * a.action_stride + (int64_t)drone] = (int32_t)(((h >> 32) * 5ull) >> 32);
+                }
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------ add_many ---
 // Transition i of the batch goes to slot (cursor + i) % capacity; with more
 // transitions than slots only the last `capacity` are written (what a
@@ -622,6 +864,39 @@ hipError_t launch_qnet_act(const QnetArgs& a, int num_cus, hipStream_t s) {
         case 8: hipLaunchKernelGGL(drl_qnet_act_kernel<8>, grid, block, lds, s, a); break;
         default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_qnet_act_code(const QnetArgs& a, int window, int num_cus, hipStream_t s) {
+    static const int waves = [] {  // DRL_QN_CODE_WAVES: waves per workgroup (A/B knob)
+        const char* e = getenv("DRL_QN_CODE_WAVES");
+        const int w = e ? atoi(e) : QN_CODE_WAVES;
+        return w >= 1 && w <= QN_CODE_MAXW ? w : QN_CODE_WAVES;
+    }();
+    const int64_t nt = (a.E + 15) / 16;
+    int64_t nb = (nt + waves - 1) / waves;
+    if (nb > num_cus) nb = num_cus;
+    const dim3 grid((unsigned)nb), block(64 * waves);
+    const size_t lds = (size_t)a.lds_vec * 16;
+#define QN_CODE_LAUNCH(NT, W)                                                                               \
+    if (a.lo0_lds) hipLaunchKernelGGL((drl_qnet_act_code_kernel<NT, true, W>), grid, block, lds, s, a);    \
+    else hipLaunchKernelGGL((drl_qnet_act_code_kernel<NT, false, W>), grid, block, lds, s, a)
+#define QN_CODE_W(W)                             \
+    switch (a.nt[0]) {                            \
+        case 2: QN_CODE_LAUNCH(2, W); break;      \
+        case 4: QN_CODE_LAUNCH(4, W); break;      \
+        case 6: QN_CODE_LAUNCH(6, W); break;      \
+        case 8: QN_CODE_LAUNCH(8, W); break;      \
+        default: return hipErrorInvalidValue;     \
+    }
+    switch (window) {
+        case 5: QN_CODE_W(5) break;
+        case 7: QN_CODE_W(7) break;
+        case 9: QN_CODE_W(9) break;
+        default: return hipErrorInvalidValue;
+    }
+#undef QN_CODE_W
+#undef QN_CODE_LAUNCH
     return hipGetLastError();
 }
 

@@ -31,7 +31,17 @@ int qnet_layout(const drl_qnet_desc* d, drl::QnetLayout* L) {
     if (d->n_actions < 1 || d->n_actions > 8) return fail("n_actions must be in [1, 8]");
     if (d->precision != DRL_QNET_BF16 && d->precision != DRL_QNET_F32)
         return fail("precision must be DRL_QNET_BF16 or DRL_QNET_F32");
+    int code_w = 0;
+    if (d->input == DRL_QNET_INPUT_CODE) {
+        for (int w = 5; w <= 9; w += 2)
+            if (d->in_features == w * w * 6) code_w = w;
+        if (!code_w) return fail("a policy-code net takes a 5x5, 7x7 or 9x9 window (in_features W*W*6)");
+        if (d->precision != DRL_QNET_F32) return fail("a policy-code net runs DRL_QNET_F32");
+    } else if (d->input != DRL_QNET_INPUT_OBS) {
+        return fail("input must be DRL_QNET_INPUT_OBS or DRL_QNET_INPUT_CODE");
+    }
     memset(L, 0, sizeof *L);
+    L->code_w = code_w;
     L->precision = d->precision;
     L->n_layers = d->n_hidden + 1;
     int frag = 0, bias = 0;
@@ -41,7 +51,8 @@ int qnet_layout(const drl_qnet_desc* d, drl::QnetLayout* L) {
         L->nt[l] = (L->out[l] + 15) / 16;  // 16-row MFMA tiles
         // 32-wide K-slices; layer 0 padded to a multiple of the act kernel's slice ring
         constexpr int R = drl::lay::qn_ring;
-        L->kt[l] = l == 0 ? ((d->in_features + 31) / 32 + R - 1) / R * R : L->in[l] / 32;
+        L->kt[l] = l == 0 ? (code_w ? drl::lay::code_kt(code_w) : ((d->in_features + 31) / 32 + R - 1) / R * R)
+                          : L->in[l] / 32;
         L->frag_off[l] = frag * 64;
         L->frag_src[l] = frag * 64;
         L->bias_off[l] = bias;
@@ -146,6 +157,7 @@ int drl_qnet_pack(const drl_qnet_desc* d, const float* const* d_weights, const f
         p.b[l] = d_biases[l];
     }
     p.precision = L.precision;
+    p.code_w = L.code_w;
     for (int l = 0; l < L.n_layers; ++l) p.frag_lo_off[l] = L.frag_lo_off[l];
     p.n_wfrag_elems = (int64_t)L.frag_total * 8;
     p.n_bias = L.n_bias;
@@ -161,6 +173,7 @@ static int qnet_act_impl(const drl_qnet_desc* d, const void* d_packed, const flo
                          uint64_t synth_step, int32_t* d_err, hipStream_t stream) {
     drl::QnetLayout L;
     if (qnet_layout(d, &L)) return -1;
+    if (L.code_w) return fail("a DRL_QNET_INPUT_CODE net acts through drl_qnet_act_code");
     if (num_envs < 0) return fail("num_envs < 0");
     if (num_envs == 0) return 0;
     if (!d_packed || !d_obs || !d_actions) return fail("packed/obs/actions must be non-NULL");
@@ -220,6 +233,56 @@ int drl_qnet_act_synth(const drl_qnet_desc* d, const void* d_packed, const float
     if (n_drones < 1 || n_drones > 255) return fail("n_drones must be in [1, 255]");
     return qnet_act_impl(d, d_packed, d_obs, num_envs, obs_stride, epsilon, seed, step, env_offset, d_actions,
                          n_drones, d_q, n_drones, synth_seed, synth_step, d_err, stream);
+}
+
+int drl_qnet_act_code(const drl_qnet_desc* d, const void* d_packed, const void* d_code, int64_t num_envs,
+                      float epsilon, uint64_t seed, uint64_t step, int64_t env_offset, int32_t* d_actions,
+                      int64_t action_stride, int32_t synth_n, uint64_t synth_seed, uint64_t synth_step, float* d_q,
+                      int32_t* d_err, hipStream_t stream) {
+    drl::QnetLayout L;
+    if (qnet_layout(d, &L)) return -1;
+    if (!L.code_w) return fail("drl_qnet_act_code needs a DRL_QNET_INPUT_CODE net");
+    if (num_envs < 0) return fail("num_envs < 0");
+    if (num_envs == 0) return 0;
+    if (!d_packed || !d_code || !d_actions) return fail("packed/code/actions must be non-NULL");
+    if ((uintptr_t)d_packed % 16 || (uintptr_t)d_code % 16) return fail("packed and code must be 16-byte aligned");
+    if (action_stride < 1) return fail("action_stride must be >= 1");
+    if (synth_n > 1 && action_stride < synth_n) return fail("action_stride must be >= synth_n");
+    drl::QnetArgs a;
+    memset(&a, 0, sizeof a);
+    a.in_features = d->in_features;
+    a.kt0 = L.kt[0];
+    a.n_hidden = d->n_hidden;
+    a.n_actions = d->n_actions;
+    for (int l = 0; l < L.n_layers; ++l) {
+        a.nt[l] = L.nt[l];
+        a.frag_off[l] = L.frag_off[l];
+        a.bias_off[l] = L.bias_off[l];
+        a.frag_lo_off[l] = L.frag_lo_off[l];
+    }
+    a.precision = L.precision;
+    a.frag_total = L.frag_total;
+    a.bias_vec = L.bias_vec;
+    a.lo0_lds = L.lo0_lds;
+    a.lds_vec = L.lds_vec;
+    a.n_bias = L.n_bias;
+    a.packed = static_cast<const uint4*>(d_packed);
+    a.obs = static_cast<const float*>(d_code);
+    a.E = num_envs;
+    a.epsilon = epsilon;
+    a.seed = seed;
+    a.step = step;
+    a.env_offset = env_offset;
+    a.actions = d_actions;
+    a.action_stride = action_stride;
+    a.q = d_q;
+    a.synth_n = synth_n > 1 ? synth_n : 0;
+    a.synth_seed = synth_seed;
+    a.synth_step = synth_step;
+    a.err = d_err;
+    a.total_bytes = L.total_vec * 16;
+    hipError_t e = drl::launch_qnet_act_code(a, L.code_w, num_cus(), stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_qnet_act_code launch");
 }
 
 int drl_replay_add(const drl_replay* r, int64_t cursor, int64_t n, const float* d_obs, int64_t obs_stride,

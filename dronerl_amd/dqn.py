@@ -26,11 +26,14 @@ NUM_ACTIONS = 5  # common/constants.py Action
 
 DRL_QNET_BF16, DRL_QNET_F32 = 0, 1  # include/dronerl.h
 PRECISIONS = {"bf16": DRL_QNET_BF16, "f32": DRL_QNET_F32}
+DRL_QNET_INPUT_OBS, DRL_QNET_INPUT_CODE = 0, 1
+INPUTS = {"obs": DRL_QNET_INPUT_OBS, "code": DRL_QNET_INPUT_CODE}
 
 
 class DrlQnetDesc(ctypes.Structure):
     _fields_ = [("in_features", ctypes.c_int32), ("n_hidden", ctypes.c_int32),
-                ("hidden", ctypes.c_int32 * 3), ("n_actions", ctypes.c_int32), ("precision", ctypes.c_int32)]
+                ("hidden", ctypes.c_int32 * 3), ("n_actions", ctypes.c_int32), ("precision", ctypes.c_int32),
+                ("input", ctypes.c_int32)]
 
 
 class DrlReplay(ctypes.Structure):
@@ -52,6 +55,7 @@ def _bind(L):
         "drl_qnet_pack": [D, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp, _vp],
         "drl_qnet_act": [D, _vp, _vp, i64, i64, f32, u64, u64, i64, _vp, i64, _vp, _vp, _vp],
         "drl_qnet_act_synth": [D, _vp, _vp, i64, i64, f32, u64, u64, i64, _vp, i32, u64, u64, _vp, _vp, _vp],
+        "drl_qnet_act_code": [D, _vp, _vp, i64, f32, u64, u64, i64, _vp, i64, i32, u64, u64, _vp, _vp, _vp],
         "drl_replay_add": [ctypes.POINTER(DrlReplay), i64, i64, _vp, i64, _vp, i64, _vp, i64, _vp, i64, _vp, i64, _vp],
     }
     for name, args in sig.items():
@@ -83,13 +87,29 @@ class QNetwork:
     precision "bf16": bf16 MFMA operands, f32 accumulation (Q to ~1e-2
     relative).  "f32": the reference's f32 nets (jax dqn.py:47-63, torch
     dqn.py:44-82): split fp16 hi/lo operands, three MFMAs per product tile,
-    Q to f32 rounding (include/dronerl.h DRL_QNET_F32)."""
+    Q to f32 rounding (include/dronerl.h DRL_QNET_F32).
+
+    input "obs": `act` reads the f32 observation rows.  "code" (f32 only, a
+    5x5, 7x7 or 9x9 window): `act` reads drone 0's policy code, which
+    ``BatchedDeliveryDrones.step(..., code=...)`` writes next to the
+    observation (128 B per env at radius 3 instead of 1,176 B of f32); the
+    parameters and Q values are the same (drl_qnet_act_code)."""
 
     def __init__(self, in_features: int, hidden: Sequence[int] = (32, 32), n_actions: int = NUM_ACTIONS,
-                 device=None, generator: Optional[torch.Generator] = None, precision: str = "bf16"):
+                 device=None, generator: Optional[torch.Generator] = None, precision: str = "bf16",
+                 input: str = "obs"):
         if precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
+        if input not in INPUTS:
+            raise ValueError(f"input must be one of {sorted(INPUTS)}")
         self.precision = precision
+        self.input = input
+        self.code_bytes = 0
+        if input == "code":
+            w = round((in_features / 6) ** 0.5)
+            if precision != "f32" or w not in (5, 7, 9) or w * w * 6 != in_features:
+                raise ValueError("input='code' needs precision='f32' and in_features = W*W*6 with W in 5, 7, 9")
+            self.code_bytes = int(lib().drl_policy_code_bytes((w - 1) // 2))
         self.L = _bind(lib())
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type == "cuda" and self.device.index is None:
@@ -105,7 +125,7 @@ class QNetwork:
             self.weights.append(w.to(self.device))
             self.biases.append(torch.zeros(sizes[i + 1], device=self.device))
         self.desc = DrlQnetDesc(in_features, len(self.hidden), (ctypes.c_int32 * 3)(*self.hidden, *[0] * (3 - len(self.hidden))),
-                                n_actions, PRECISIONS[precision])
+                                n_actions, PRECISIONS[precision], INPUTS[input])
         nb = ctypes.c_int64()
         _check(self.L, self.L.drl_qnet_packed_bytes(ctypes.byref(self.desc), ctypes.byref(nb)))
         self.packed = torch.empty(nb.value // 4, dtype=torch.int32, device=self.device)  # 16-B aligned
@@ -148,15 +168,21 @@ class QNetwork:
     def act(self, obs: torch.Tensor, epsilon: float, seed: int = 0, step: int = 0, env_offset: int = 0,
             actions: Optional[torch.Tensor] = None, q_out: Optional[torch.Tensor] = None,
             synth: Optional[Tuple[int, int]] = None) -> torch.Tensor:
-        """Epsilon-greedy action for each row of obs [E, ..., in_features].
+        """Epsilon-greedy action for each row of obs [E, ..., in_features]
+        (input "code": the policy code, uint8 [E, code_bytes]).
         `actions` may be an [E, n_drones] int32 tensor: column 0 is written (the
         other drones keep their actions, train_jax.py:47-49).  synth=(seed,
         step): the other columns get BatchedDeliveryDrones.synth_actions(seed,
         step)'s values in the same launch (drl_qnet_act_synth)."""
         E = obs.shape[0]
-        _on(obs, self.device, torch.float32, "obs")
+        if self.input == "code":
+            _on(obs, self.device, torch.uint8, "code")
+            if tuple(obs.shape) != (E, self.code_bytes) or not obs.is_contiguous():
+                raise ValueError(f"code must be a contiguous uint8 [E, {self.code_bytes}] tensor")
+        else:
+            _on(obs, self.device, torch.float32, "obs")
         flat = obs.reshape(E, -1)
-        if flat.shape[1] < self.in_features or flat.stride(1) != 1:
+        if self.input == "obs" and (flat.shape[1] < self.in_features or flat.stride(1) != 1):
             raise ValueError("obs must hold at least in_features contiguous float32 values per env")
         if actions is None:
             actions = torch.empty((E, 1), dtype=torch.int32, device=self.device)
@@ -168,6 +194,13 @@ class QNetwork:
             if tuple(q_out.shape) != (E, self.n_actions) or not q_out.is_contiguous():
                 raise ValueError(f"q_out must be a contiguous float32 [{E}, {self.n_actions}] tensor")
         stride_a = actions.shape[1] if actions.dim() == 2 else 1
+        if self.input == "code":
+            sn, ss, st = (stride_a, synth[0] & (2**64 - 1), synth[1]) if synth is not None else (0, 0, 0)
+            _check(self.L, self.L.drl_qnet_act_code(
+                ctypes.byref(self.desc), _vp(self.packed.data_ptr()), _vp(obs.data_ptr()), E, float(epsilon),
+                seed & (2**64 - 1), step, env_offset, _vp(actions.data_ptr()), stride_a, sn, ss, st,
+                None if q_out is None else _vp(q_out.data_ptr()), _vp(self.err.data_ptr()), _stream(self.device)))
+            return actions
         if synth is not None:
             _check(self.L, self.L.drl_qnet_act_synth(
                 ctypes.byref(self.desc), _vp(self.packed.data_ptr()), _vp(flat.data_ptr()), E, flat.stride(0),
@@ -195,33 +228,72 @@ class QNetwork:
             raise DroneRLError(f"qnet error bits {e:#x}")
 
 
+def decode_policy_code(code: torch.Tensor, window_radius: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Policy-code rows uint8 [n, code_bytes] -> drone 0's observation f32
+    [n, W*W*6], bit for bit what drl_obs writes (drl_code_decode)."""
+    L = lib()
+    W = 2 * window_radius + 1
+    n = code.shape[0]
+    _on(code, code.device, torch.uint8, "code")
+    if code.dim() != 2 or code.shape[1] != L.drl_policy_code_bytes(window_radius) or not code.is_contiguous():
+        raise ValueError("code must be a contiguous uint8 [n, policy_code_bytes] tensor")
+    if out is None:
+        out = torch.empty((n, W * W * 6), dtype=torch.float32, device=code.device)
+    _on(out, code.device, torch.float32, "out")
+    if out.numel() != n * W * W * 6 or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous float32 tensor of {n * W * W * 6} values")
+    _check(L, L.drl_code_decode(window_radius, _vp(code.data_ptr()), n, _vp(out.data_ptr()), _stream(code.device)))
+    return out
+
+
 @dataclass
 class ReplayBuffer:
-    """jax_impl/buffers.py ReplayBuffer on device tensors (drone-0 transitions)."""
+    """jax_impl/buffers.py ReplayBuffer on device tensors (drone-0 transitions).
+
+    code_radius > 0: the rows hold drone 0's policy code (uint8 [capacity,
+    code_bytes], 128 B at radius 3 instead of 1,176 B of f32) -- add_many
+    takes code rows (BatchedDeliveryDrones.step(..., code=...)) -- and sample
+    decodes the drawn rows to the f32 observation (decode_policy_code), so the
+    learner sees exactly the observations the reference buffer would hold."""
     capacity: int
     obs_floats: int
     device: torch.device
+    code_radius: int = 0
 
     def __post_init__(self):
         self.L = _bind(lib())
         d = torch.device(self.device)
-        self.obs = torch.zeros((self.capacity, self.obs_floats), device=d)
-        self.next_obs = torch.zeros((self.capacity, self.obs_floats), device=d)
+        if self.code_radius:
+            W = 2 * self.code_radius + 1
+            if self.obs_floats != W * W * 6:
+                raise ValueError(f"obs_floats must be {W * W * 6} for a code_radius {self.code_radius} buffer")
+            self.code_bytes = int(self.L.drl_policy_code_bytes(self.code_radius))
+            if self.code_bytes <= 0:
+                raise ValueError("bad code_radius")
+            self.obs = torch.zeros((self.capacity, self.code_bytes), dtype=torch.uint8, device=d)
+            self.next_obs = torch.zeros((self.capacity, self.code_bytes), dtype=torch.uint8, device=d)
+            row_words = self.code_bytes // 4
+        else:
+            self.obs = torch.zeros((self.capacity, self.obs_floats), device=d)
+            self.next_obs = torch.zeros((self.capacity, self.obs_floats), device=d)
+            row_words = self.obs_floats
         self.actions = torch.zeros(self.capacity, dtype=torch.int32, device=d)
         self.rewards = torch.zeros(self.capacity, device=d)
         self.dones = torch.zeros(self.capacity, dtype=torch.uint8, device=d)
         self.cursor = 0          # current_idx
         self.size = 0            # current_size
-        self._c = DrlReplay(self.capacity, self.obs_floats, self.obs.data_ptr(), self.next_obs.data_ptr(),
+        self._c = DrlReplay(self.capacity, row_words, self.obs.data_ptr(), self.next_obs.data_ptr(),
                             self.actions.data_ptr(), self.rewards.data_ptr(), self.dones.data_ptr())
 
     def add_many(self, obs: torch.Tensor, actions: torch.Tensor, rewards: torch.Tensor, next_obs: torch.Tensor,
                  dones: torch.Tensor):
-        """buffers.py:57-80.  obs/next_obs [E, >= obs_floats] f32 rows; actions
-        i32, rewards f32, dones u8 as [E] or [E, n_drones] (column 0 taken)."""
+        """buffers.py:57-80.  obs/next_obs [E, >= obs_floats] f32 rows (a code
+        buffer: uint8 [E, code_bytes] policy-code rows); actions i32, rewards
+        f32, dones u8 as [E] or [E, n_drones] (column 0 taken)."""
         E = obs.shape[0]
         dev = self.obs.device
-        for t, dt, name in ((obs, torch.float32, "obs"), (next_obs, torch.float32, "next_obs"),
+        odt = torch.uint8 if self.code_radius else torch.float32
+        for t, dt, name in ((obs, odt, "obs"), (next_obs, odt, "next_obs"),
                             (actions, torch.int32, "actions"), (rewards, torch.float32, "rewards"),
                             (dones, torch.uint8, "dones")):
             _on(t, dev, dt, name)
@@ -230,7 +302,11 @@ class ReplayBuffer:
             if name in ("actions", "rewards", "dones") and t.dim() > 2:
                 raise ValueError(f"{name} must be [E] or [E, n_drones]")
         o, no = obs.reshape(E, -1), next_obs.reshape(E, -1)
-        if o.shape[1] < self.obs_floats or no.shape[1] < self.obs_floats:
+        if self.code_radius:
+            if o.shape[1] != self.code_bytes or no.shape[1] != self.code_bytes:
+                raise ValueError(f"code rows must hold code_bytes={self.code_bytes} bytes")
+            o, no = o.view(torch.float32), no.view(torch.float32)  # copied bit for bit
+        elif o.shape[1] < self.obs_floats or no.shape[1] < self.obs_floats:
             raise ValueError(f"obs rows must hold at least obs_floats={self.obs_floats} values")
         col = lambda t: t.shape[1] if t.dim() == 2 else 1  # noqa: E731
         _check(self.L, self.L.drl_replay_add(ctypes.byref(self._c), self.cursor, E, _vp(o.data_ptr()), o.stride(0),
@@ -246,5 +322,9 @@ class ReplayBuffer:
     def sample(self, batch: int = 64, generator: Optional[torch.Generator] = None) -> dict:
         """buffers.py:82-93: uniform indices in [0, size)."""
         idx = torch.randint(0, self.size, (batch,), device=self.obs.device, generator=generator)
-        return dict(obs=self.obs[idx], actions=self.actions[idx], rewards=self.rewards[idx],
-                    next_obs=self.next_obs[idx], dones=self.dones[idx])
+        obs, next_obs = self.obs[idx], self.next_obs[idx]
+        if self.code_radius:
+            obs = decode_policy_code(obs, self.code_radius)
+            next_obs = decode_policy_code(next_obs, self.code_radius)
+        return dict(obs=obs, actions=self.actions[idx], rewards=self.rewards[idx],
+                    next_obs=next_obs, dones=self.dones[idx])

@@ -138,7 +138,7 @@ class BatchedDeliveryDrones:
 
     def step(self, actions: torch.Tensor, obs_k: int = 0, rewards: Optional[torch.Tensor] = None,
              dones: Optional[torch.Tensor] = None, obs: Optional[torch.Tensor] = None,
-             obs_stream: Optional[bool] = None):
+             obs_stream: Optional[bool] = None, code: Optional[torch.Tensor] = None):
         """env.py:112-215 for every env.  actions int32 [E, N] by drone index.
 
         Returns (rewards f32 [E,N], dones bool-as-uint8 [E,N]) and, when
@@ -148,9 +148,15 @@ class BatchedDeliveryDrones:
         (DRL_STEP_OBS_STREAM) or cached ones; None (default) picks
         ``default_obs_stream`` (streaming at step_group_lanes >= 16).  Results
         are identical either way.
+        code: uint8 [E, policy_code_bytes] (``new_code()``): also write drone
+        0's policy code after the step (drl_step_code), the input of a
+        QNetwork(input="code"); with obs_k = 0 the code alone (no f32
+        observation rows are written).
         """
         E, N = self.num_envs, self.n_drones
         actions = self._check(actions, torch.int32, (E, N), "actions")
+        if code is not None:
+            self._check_out(code, torch.uint8, (E, self.policy_code_bytes), "code")
         if rewards is None:
             rewards = torch.empty((E, N), dtype=torch.float32, device=self.device)
         if dones is None:
@@ -171,9 +177,9 @@ class BatchedDeliveryDrones:
             if self._since_refill >= self.refill_every:
                 self._since_refill = 0
                 flags |= DRL_STEP_REFILL
-        check(lib().drl_step_ex(ctypes.byref(self._cp), ctypes.byref(s), _ptr(actions), _ptr(rewards), _ptr(dones),
-                                _ptr(obs) if obs_k else None, int(obs_k), _ptr(self.err), flags,
-                                _stream(self.device)), "drl_step")
+        check(lib().drl_step_code(ctypes.byref(self._cp), ctypes.byref(s), _ptr(actions), _ptr(rewards), _ptr(dones),
+                                  _ptr(obs) if obs_k else None, int(obs_k), None if code is None else _ptr(code),
+                                  _ptr(self.err), flags, _stream(self.device)), "drl_step")
         if obs_k:
             return rewards, dones, obs
         return rewards, dones
@@ -214,15 +220,39 @@ class BatchedDeliveryDrones:
             return rewards, dones, obs
         return rewards, dones
 
-    def get_obs(self, k: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """WindowedGridView observation of drone indices 0..k-1: f32 [E, k, W, W, 6]."""
+    def get_obs(self, k: Optional[int] = None, out: Optional[torch.Tensor] = None,
+                code: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """WindowedGridView observation of drone indices 0..k-1: f32 [E, k, W, W, 6].
+        code: uint8 [E, policy_code_bytes], also filled with drone 0's policy code."""
         k = self.n_drones if k is None else int(k)
         W = self.layout.obs_window
         if out is None:
             out = torch.empty((self.num_envs, k, W, W, 6), dtype=torch.float32, device=self.device)
+        if code is not None:
+            self._check_out(code, torch.uint8, (self.num_envs, self.policy_code_bytes), "code")
         s = self.state.c()
-        check(lib().drl_obs(ctypes.byref(self._cp), ctypes.byref(s), k, _ptr(out), _stream(self.device)), "drl_obs")
+        check(lib().drl_obs_code(ctypes.byref(self._cp), ctypes.byref(s), k, _ptr(out),
+                                 None if code is None else _ptr(code), _stream(self.device)), "drl_obs")
         return out
+
+    def get_code(self, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Drone index 0's policy code alone, uint8 [E, policy_code_bytes] (drl_obs_code, no f32 rows)."""
+        if out is None:
+            out = self.new_code()
+        self._check_out(out, torch.uint8, (self.num_envs, self.policy_code_bytes), "code")
+        s = self.state.c()
+        check(lib().drl_obs_code(ctypes.byref(self._cp), ctypes.byref(s), 1, None, _ptr(out), _stream(self.device)),
+              "drl_obs")
+        return out
+
+    @property
+    def policy_code_bytes(self) -> int:
+        """Bytes per env of the policy code (drl_policy_code_bytes)."""
+        return int(lib().drl_policy_code_bytes(self.params.window_radius))
+
+    def new_code(self) -> torch.Tensor:
+        """A policy-code buffer, uint8 [E, policy_code_bytes] (16-B aligned rows)."""
+        return torch.empty((self.num_envs, self.policy_code_bytes), dtype=torch.uint8, device=self.device)
 
     def get_grid(self, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """GridView observation (wrappers.py:34-43): the base grid f32 [E, side, side, 6]

@@ -46,7 +46,7 @@ extern "C" {
 
 typedef struct ihipStream_t* hipStream_t;
 
-#define DRL_ABI_VERSION 6
+#define DRL_ABI_VERSION 7
 /* Per-env RNG row of `mt` (u32 words, 7104 B):
  *   [0, 624)     MT19937 block 0     the env's CPython stream lives in block
  *   [624, 1248)  MT19937 block 1     mt_index.par; the other block holds the
@@ -216,6 +216,27 @@ int drl_mt_set(const drl_params* p, const drl_state* s, const uint32_t* d_words,
  * 0..k-1: f32 [E][k][W][W][6]. */
 int drl_obs(const drl_params* p, const drl_state* s, int32_t k, float* d_obs, hipStream_t stream);
 
+/* Policy code (ABI 7): drone index 0's window as one u16 per cell -- object
+ * code (bits 0-2, walls as DRL_SKYSCRAPER) | ((charge+1) | carry << 7) << 3
+ * (0 above: no drone) -- in four groups of ceil(W*W/4) cells, each padded
+ * with zero codes to a multiple of 8.  Bytes per env (16-B multiple): */
+int32_t drl_policy_code_bytes(int32_t window_radius);
+/* drl_step_ex that also writes the policy code of the state after the step
+ * (d_code, 16-B aligned, [E][drl_policy_code_bytes]): what drl_qnet_act_code
+ * reads instead of the observation.  With d_obs non-NULL the observation
+ * (obs_k >= 1) is written as well; with d_obs NULL the code alone (obs_k
+ * ignored): a consumer that only needs drone 0's window skips the f32 rows
+ * (6 floats per cell) entirely.  d_code NULL: exactly drl_step_ex. */
+int drl_step_code(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
+                  uint8_t* d_dones, float* d_obs, int32_t obs_k, void* d_code, int32_t* d_err, uint32_t flags,
+                  hipStream_t stream);
+/* Policy code rows -> drone index 0's observation, f32 [n][W][W][6] exactly
+ * as drl_obs writes it (a replay buffer of codes decodes its samples). */
+int drl_code_decode(int32_t window_radius, const void* d_code, int64_t n, float* d_obs, hipStream_t stream);
+/* drl_obs that also writes the policy code (d_code nullable); d_obs NULL:
+ * the code alone (k ignored). */
+int drl_obs_code(const drl_params* p, const drl_state* s, int32_t k, float* d_obs, void* d_code, hipStream_t stream);
+
 /* GridView observation (wrappers.py:10-31,34-43): the [side][side][6] f32
  * base grid of every env (each drone of an env sees the same grid):
  * d_grid f32 [E][side][side][6], channels as drl_obs, no wall padding. */
@@ -320,12 +341,19 @@ int drl_env_errors(drl_env* env, int32_t* flags, int32_t clear, hipStream_t stre
  * ------------------------------------------------------------------------ */
 #define DRL_QNET_BF16 0
 #define DRL_QNET_F32 1
+/* input: DRL_QNET_INPUT_OBS, the f32 observation rows (drl_qnet_act); or
+ * DRL_QNET_INPUT_CODE, drone index 0's policy code written by drl_step_code /
+ * drl_obs_code (drl_qnet_act_code; DRL_QNET_F32, window radius 2..4).  The
+ * weights are the same; the packed layout differs. */
+#define DRL_QNET_INPUT_OBS 0
+#define DRL_QNET_INPUT_CODE 1
 typedef struct drl_qnet_desc {
     int32_t in_features;  /* observation floats, W*W*6 (even, <= 512) */
     int32_t n_hidden;     /* 1..3 hidden layers */
     int32_t hidden[3];    /* widths: multiples of 32 in [32, 128] */
     int32_t n_actions;    /* 1..8 (Action.num_actions() = 5) */
     int32_t precision;    /* DRL_QNET_BF16 or DRL_QNET_F32 */
+    int32_t input;        /* DRL_QNET_INPUT_OBS or DRL_QNET_INPUT_CODE (ABI 7) */
 } drl_qnet_desc;
 
 /* Bytes of the packed network (weight fragments + f32 biases; DRL_QNET_F32
@@ -357,8 +385,22 @@ int drl_qnet_act_synth(const drl_qnet_desc* d, const void* d_packed, const float
                        int32_t* d_actions, int32_t n_drones, uint64_t synth_seed, uint64_t synth_step, float* d_q,
                        int32_t* d_err, hipStream_t stream);
 
+/* drl_qnet_act for a DRL_QNET_INPUT_CODE net, reading drone index 0's policy
+ * code (d_code, drl_policy_code_bytes(radius) per env, as drl_step_code /
+ * drl_obs_code write it) instead of the f32 observation: the 0/1 and
+ * charge/100 inputs are computed from the code exactly as the observation
+ * holds them, so Q is the f32 net's on the same window (to f32 rounding).
+ * synth_n > 1: as drl_qnet_act_synth (columns 1..synth_n-1 of d_actions from
+ * drl_synth_actions(synth_seed, synth_step), action_stride = synth_n). */
+int drl_qnet_act_code(const drl_qnet_desc* d, const void* d_packed, const void* d_code, int64_t num_envs,
+                      float epsilon, uint64_t seed, uint64_t step, int64_t env_offset, int32_t* d_actions,
+                      int64_t action_stride, int32_t synth_n, uint64_t synth_seed, uint64_t synth_step, float* d_q,
+                      int32_t* d_err, hipStream_t stream);
+
 /* Replay ring buffer storage (device, caller-owned): obs/next_obs f32
- * [capacity][obs_floats], actions i32, rewards f32, dones u8 [capacity]. */
+ * [capacity][obs_floats], actions i32, rewards f32, dones u8 [capacity].
+ * Rows are copied bit for bit: policy-code rows (drl_policy_code_bytes / 4
+ * words each) store the same way. */
 typedef struct drl_replay {
     int64_t capacity;
     int32_t obs_floats;

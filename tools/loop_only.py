@@ -1,5 +1,8 @@
 #!/usr/bin/env python3
-"""Run only bench.train_loop_bench (for kernel traces of the train loop)."""
+"""Run bench.train_loop_bench alone (diagnostic, e.g. under rocprofv3 --kernel-trace).
+
+python tools/loop_only.py [--config c3] [--segments 3] [--input code|obs] [--precision f32]
+"""
 import argparse
 import json
 import os
@@ -8,21 +11,23 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-import torch  # noqa: E402
-
 import bench  # noqa: E402
-import dronerl_amd._native as nat  # noqa: E402
 from dronerl_amd import BatchedDeliveryDrones, EnvParams  # noqa: E402
 
-ap = argparse.ArgumentParser()
-ap.add_argument("--config", default="c3")
-ap.add_argument("--segments", type=int, default=2)
-ap.add_argument("--lib", default="", help="alternative library (tools/variants.py)")
-args = ap.parse_args()
-if args.lib:
-    nat.LIB_PATH = os.path.abspath(args.lib)
-G, N, E, K = bench.CONFIGS[args.config]
-env = BatchedDeliveryDrones(EnvParams(n_drones=N, grid_size=G), E)
-env.reset(seed=0)
-r = bench.train_loop_bench(env, args.segments)
-print(os.path.basename(nat.LIB_PATH), args.config, f"train loop {r['us_per_step']:.2f} us/step")
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--segments", type=int, default=3)
+    ap.add_argument("--input", default="code", choices=("code", "obs"))
+    ap.add_argument("--precision", default="f32", choices=("f32", "bf16"))
+    args = ap.parse_args()
+    G, N, E = bench.CONFIGS[args.config][:3]
+    env = BatchedDeliveryDrones(EnvParams(n_drones=N, grid_size=G), E)
+    env.reset(seed=0)
+    r = bench.train_loop_bench(env, args.segments, precision=args.precision, input=args.input)
+    print(json.dumps({k: r[k] for k in ("us_per_step", "precision", "input")}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--stride", type=int, default=294, help="obs row stride in floats (296: 16-B aligned rows)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--input", default="obs", choices=["obs", "code"], help="code: drl_qnet_act_code (f32)")
     args = ap.parse_args()
     if args.lib:
         import dronerl_amd._native as nat
@@ -25,13 +26,20 @@ def main():
     E = args.envs
     obs = torch.rand((E, 1, 7, 7, 6), device="cuda")
     net = QNetwork(294, tuple(int(x) for x in args.hidden.split(",")), generator=torch.Generator().manual_seed(0),
-                   precision=args.precision)
+                   precision=args.precision, input=args.input)
     a = torch.zeros((E, 8), dtype=torch.int32, device="cuda")
     flat = obs.reshape(E, -1)
     if args.stride != 294:
         big = torch.zeros((E, args.stride), device="cuda")
         big[:, :294] = flat
         flat = big[:, :294]
+    if args.input == "code":  # real codes from a C3 env (drone 0's window)
+        from dronerl_amd import BatchedDeliveryDrones, EnvParams
+        env = BatchedDeliveryDrones(EnvParams(n_drones=8, grid_size=16), E)
+        env.reset(seed=0)
+        flat = env.new_code()
+        for t in range(4):
+            env.step(env.synth_actions(seed=1, step=t), obs_k=1, code=flat)
     for _ in range(20):
         net.act(flat, 0.1, actions=a)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -42,8 +50,9 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / args.iters
-    print(f"{os.path.basename(args.lib) or 'libdronerl.so'} E={E} hidden={args.hidden} {args.precision}: {us:.2f} us/launch, "
-          f"{E * 1176 / us / 1e3:.0f} GB/s obs read (row stride {flat.stride(0)} floats)")
+    nb = flat.shape[1] * flat.element_size()
+    print(f"{os.path.basename(args.lib) or 'libdronerl.so'} E={E} hidden={args.hidden} {args.precision} "
+          f"input={args.input}: {us:.2f} us/launch, {E * nb / us / 1e3:.0f} GB/s input read ({nb} B/env)")
 
 
 if __name__ == "__main__":
