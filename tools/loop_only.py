@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run bench.train_loop_bench alone (diagnostic, e.g. under rocprofv3 --kernel-trace).
 
-python tools/loop_only.py [--config c3] [--segments 3] [--input code|obs] [--precision f32]
+python tools/loop_only.py [--config c3] [--segments 3] [--input code|obs] [--precision f32] [--lib var.so]
 """
 import argparse
 import json
@@ -21,7 +21,11 @@ def main():
     ap.add_argument("--segments", type=int, default=3)
     ap.add_argument("--input", default="code", choices=("code", "obs"))
     ap.add_argument("--precision", default="f32", choices=("f32", "bf16"))
+    ap.add_argument("--lib", default="", help="alternative library (tools/variants.py)")
     args = ap.parse_args()
+    if args.lib:
+        import dronerl_amd._native as nat
+        nat.LIB_PATH = os.environ["DRL_LIB"] = os.path.abspath(args.lib)
     G, N, E = bench.CONFIGS[args.config][:3]
     env = BatchedDeliveryDrones(EnvParams(n_drones=N, grid_size=G), E)
     env.reset(seed=0)
