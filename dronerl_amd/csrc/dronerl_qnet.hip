@@ -65,11 +65,14 @@ __global__ void drl_qnet_pack_kernel(QnetPack p) {
             const int ch = sl < 5 * cpg ? (sl % 5 < 4 ? sl % 5 : 5) : 4;
             const bool ok = sl < 6 * cpg && lc < cpg && g * cpg + lc < cells;
             k = ok ? (g * cpg + lc) * 6 + ch : p.in[l];  // (in[l]: a zero weight)
+            // the first padding slot of lane group 0 carries the bias (input 1)
+            if (g == 0 && sl == 6 * cpg) k = -1;
         }
-        float w = (row < p.out[l] && k < p.in[l]) ? p.w[l][(int64_t)row * p.in[l] + k] : 0.0f;
+        float w = (row < p.out[l] && k >= 0 && k < p.in[l]) ? p.w[l][(int64_t)row * p.in[l] + k] : 0.0f;
+        if (k < 0) w = row < p.out[l] ? p.b[l][row] : 0.0f;
         // the charge channel's 1/100 moves into its weights: the kernel feeds
         // the integer charge (exact in fp16), so no input needs an x_lo product
-        if (l == 0 && p.code_w > 0 && k < p.in[l] && k % 6 == 4) w /= 100.0f;
+        if (l == 0 && p.code_w > 0 && k >= 0 && k < p.in[l] && k % 6 == 4) w /= 100.0f;
         if (p.precision == DRL_QNET_F32) {  // hi = fp16(w), lo = fp16((w - hi) * 2^11), lo after the LDS image
             const _Float16 hi = (_Float16)w;
             reinterpret_cast<_Float16*>(p.packed_w)[(int64_t)p.frag_off[l] * 8 + e] = hi;
@@ -569,7 +572,14 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_f32_kernel(QnetArg
 // One workgroup per CU (the net fills the LDS); the kernel's ~140 VGPRs leave
 // room for 3 waves per SIMD, so a workgroup runs up to 12 waves (the obs act's
 // 4 hide its observation reads behind a register ring instead).
-constexpr int QN_CODE_MAXW = 12;
+#ifndef DRL_QN_CODE2_WAVES
+#define DRL_QN_CODE2_WAVES 8  // drl_qnet_act_code2_kernel: 2 waves per SIMD (its ~230 VGPRs)
+#endif
+constexpr int QN_CODE2_WAVES = DRL_QN_CODE2_WAVES;
+#ifndef DRL_QN_CODE_MAXW
+#define DRL_QN_CODE_MAXW 8
+#endif
+constexpr int QN_CODE_MAXW = DRL_QN_CODE_MAXW;
 #ifndef DRL_QN_CODE_WAVES
 #define DRL_QN_CODE_WAVES 8
 #endif
@@ -588,13 +598,17 @@ __device__ __forceinline__ float code_channel(uint32_t code, int ch) {
     }
 }
 
-template <int NT0, bool LO0, int WN>
+// NT1 > 0: the net has exactly two hidden layers, the second 16 * NT1 wide
+// (the benchmark's 294->128->64->5): the later layers' loops are compile-time,
+// so only the live accumulators hold registers (16 waves per CU fit).
+template <int NT0, bool LO0, int WN, int NT1>
 __global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(QnetArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint4 wl[];
     constexpr int CPG = lay::code_cpg(WN), CPG8 = lay::code_cpg8(WN), CELLS = WN * WN;
     constexpr int NV = CPG8 / 8;                 // 16-B code vectors per lane group
     constexpr int NB = 5 * CPG;                  // slots of the 0/1 channels
     constexpr int KP = lay::code_kt(WN);         // layer 0's K-slices (host: QnetLayout::kt[0])
+    static_assert(8 * KP > 6 * CPG, "no padding slot for layer 0's bias");
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int c = lane & 15, g = lane >> 4;
     constexpr int nt0 = NT0;
@@ -615,14 +629,17 @@ __global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(Qn
             dst[4 * v + 3] = q.w;
         }
     };
+#ifdef DRL_QC_STAMPS
+    const uint64_t t_entry = __builtin_amdgcn_s_memtime();
+#endif
     const int64_t grp0 = (int64_t)blockIdx.x * nw + wave;
     int64_t grp = grp0;
-    uint32_t cw[4 * NV];
-    load_codes(grp < ntiles ? grp : 0, cw);
+#ifndef DRL_DIAG_NO_WLOAD  // timing diagnostic (wrong results): no weight staging
     for (int v0 = wave * 64; v0 < a.lds_vec; v0 += 64 * nw)
         if (v0 + lane < a.lds_vec)
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(a.packed + v0 + lane),
                                              (__attribute__((address_space(3))) void*)(wl + v0), 16, 0, 0);
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     bool bad = false;
@@ -636,6 +653,9 @@ __global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(Qn
     const auto pbuf = __builtin_amdgcn_make_buffer_rsrc((void*)a.packed, 0, a.total_bytes, 0x00020000);
     const int lane16 = lane * 16;
     auto frag_ld = [&](int frag_u4) __attribute__((always_inline)) {  // 64 lanes x 16 B at uint4 offset frag_u4
+#ifdef DRL_DIAG_QC_LDS_HIDDEN  // timing diagnostic (wrong results): hidden fragments from the LDS image
+        return wl[(frag_u4 & 0x3fff) + lane];
+#endif
         if constexpr (LO0) {
             const auto v = __builtin_amdgcn_raw_buffer_load_b128(pbuf, lane16, frag_u4 * 16, 0);
             uint4 r;
@@ -647,6 +667,9 @@ __global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(Qn
     };
     auto bias4 = [&](int off) __attribute__((always_inline)) {  // biases off + 4g .. off + 4g + 3
         f32x4 r;
+#ifdef DRL_DIAG_QC_NO_BIAS  // timing diagnostic (wrong results): no bias loads
+        return f32x4{0.01f * off, 0.0f, 0.0f, 0.0f};
+#endif
         if constexpr (LO0) {
             const auto v = __builtin_amdgcn_raw_buffer_load_b128(pbuf, 16 * g, a.bias_vec * 16 + off * 4, 0);
             __builtin_memcpy(&r, &v, 16);
@@ -657,6 +680,8 @@ __global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(Qn
         return r;
     };
 
+    uint32_t cw[4 * NV];
+    load_codes(grp < ntiles ? grp : 0, cw);
     for (; grp < ntiles; grp += gstride) {
         const int64_t ngrp = grp + gstride;
         uint32_t ncw[4 * NV];  // the next tile's codes, in flight while this tile runs
@@ -665,6 +690,9 @@ __global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(Qn
         // inline zero (no zeroing moves)
         f32x4 acc[QN_MAXT], acl[QN_MAXT];
         const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+#ifdef DRL_QC_STAMPS  // diagnostic: s_memtime per phase of each wave's tiles into q (raw u32)
+        const uint64_t ts0 = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll
         for (int t = 0; t < KP; ++t) {
             const uint32_t* cs = cw;
@@ -674,10 +702,14 @@ __global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(Qn
                 const int sl = 8 * t + j;  // compile-time slot
                 const int l = sl < NB ? sl / 5 : sl - NB;
                 const int ch = sl < NB ? (sl % 5 < 4 ? sl % 5 : 5) : 4;
-                float x = 0.0f;
+                float x = (sl == 6 * CPG && g == 0) ? 1.0f : 0.0f;  // the bias slot (drl_qnet_pack)
                 if (sl < 6 * CPG) {
                     const uint32_t cd = (cs[l >> 1] >> (16 * (l & 1))) & 0xffffu;
+#ifdef DRL_DIAG_QC_NO_DECODE  // timing diagnostics of the code act (wrong results)
+                    x = (float)(cd & 1u);
+#else
                     x = l < ncell_g ? code_channel(cd, ch) : 0.0f;
+#endif
                 }
                 bh[j] = (_Float16)x;
             }
@@ -690,23 +722,35 @@ __global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(Qn
             for (int m = 0; m < nt0; ++m) {
                 const f16x8 wh = as_f16x8(W0[(m * KP + ts) * 64 + lane]);
                 const f16x8 wo = as_f16x8(W0lo[(m * KP + ts) * 64 + lane]);
+#ifdef DRL_DIAG_QC_NO_L0MFMA
+                acc[m] = (t == 0 ? z4 : acc[m]) + (float)bh[m] + (float)wh[0] + (float)wo[1];
+                acl[m] = t == 0 ? z4 : acl[m];
+#else
                 acc[m] = MFMA_F16(wh, bh, t == 0 ? z4 : acc[m], 0, 0, 0);
                 acl[m] = MFMA_F16(wo, bh, t == 0 ? z4 : acl[m], 0, 0, 0);
+#endif
+                if (m % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // <= 8 fragments in flight (registers)
             }
             __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
         for (int i = 0; i < 4 * NV; ++i) cw[i] = ncw[i];
-        // ---- hidden layers and the output layer: as drl_qnet_act_f32_kernel
-        int nt_prev = nt0;
-        int bprev = a.bias_off[0];
-        for (int l = 1; l <= a.n_hidden; ++l) {
-            f16x8 ah[QN_MAXT / 2], al[QN_MAXT / 2];
+#ifdef DRL_QC_STAMPS
+        const uint64_t ts1 = __builtin_amdgcn_s_memtime();
+#endif
+        // ---- hidden layers and the output layer: as drl_qnet_act_f32_kernel.
+        // layer(NTP, NTL, l): inputs from NTP accumulator tiles, NTL outputs
+        // (compile-time bounds; the generic path passes QN_MAXT and masks)
+        auto layer = [&](auto ntp_c, auto ntl_c, int l, int nt_prev, int nt_l) __attribute__((always_inline)) {
+            constexpr int NTP = decltype(ntp_c)::value, NTL = decltype(ntl_c)::value;
+            const int bprev = a.bias_off[l - 1];
+            f16x8 ah[NTP / 2], al[NTP / 2];
 #pragma unroll
-            for (int s2 = 0; s2 < QN_MAXT / 2; ++s2) {
+            for (int s2 = 0; s2 < NTP / 2; ++s2) {
                 ah[s2] = al[s2] = f16x8{};  // (not carried across layers and tiles as undefined values)
                 if (2 * s2 < nt_prev) {
-                    const f32x4 b0 = bias4(bprev + 32 * s2), b1 = bias4(bprev + 32 * s2 + 16);
+                    // (layer 0's bias is folded into its K padding: drl_qnet_pack)
+                    const f32x4 b0 = l == 1 ? z4 : bias4(bprev + 32 * s2), b1 = l == 1 ? z4 : bias4(bprev + 32 * s2 + 16);
                     float v[8];
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
@@ -716,14 +760,13 @@ __global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(Qn
                     split_f16(v, ah[s2], al[s2], bad);
                 }
             }
-            const int nt_l = (l < a.n_hidden) ? a.nt[l] : 1;
             const int kt = nt_prev / 2, ms = kt * 64;  // (ms: the fragment stride of an output tile)
             const int fl = a.frag_off[l], flo = a.frag_lo_off[l];
 #pragma unroll
-            for (int t = 0; t < QN_MAXT / 2; ++t) {
+            for (int t = 0; t < NTP / 2; ++t) {
                 if (t < kt) {
 #pragma unroll
-                    for (int m = 0; m < QN_MAXT; ++m) {
+                    for (int m = 0; m < NTL; ++m) {
                         if (m < nt_l) {
                             const f16x8 wh = as_f16x8(frag_ld(fl + m * ms + t * 64));
                             const f16x8 wo = as_f16x8(frag_ld(flo + m * ms + t * 64));
@@ -733,11 +776,94 @@ __global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(Qn
                         }
                     }
                 }
-                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_sched_barrier(0);  // fragment reads next to their MFMAs (register pressure)
             }
-            nt_prev = nt_l;
-            bprev = a.bias_off[l];
+        };
+        int bprev;
+        if constexpr (NT1 > 0) {
+#ifndef DRL_DIAG_QC_NO_HIDDEN
+            // every fragment of a layer requested at once, one L2 round trip
+            // per layer (fragment by fragment the loads serialise on vmcnt)
+            constexpr int KT1 = NT0 / 2, KT2 = NT1 / 2;
+            uint4 f1h[KT1][NT1], f1l[KT1][NT1];
+            {
+                const int fl = a.frag_off[1], flo = a.frag_lo_off[1];
+#pragma unroll
+                for (int t = 0; t < KT1; ++t)
+#pragma unroll
+                    for (int m = 0; m < NT1; ++m) {
+                        f1h[t][m] = frag_ld(fl + (m * KT1 + t) * 64);
+                        f1l[t][m] = frag_ld(flo + (m * KT1 + t) * 64);
+                    }
+            }
+            f16x8 ah[KT1], al[KT1];
+#pragma unroll
+            for (int s2 = 0; s2 < KT1; ++s2) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int m = 2 * s2 + (j >> 2), i = j & 3;
+                    v[j] = fmaxf(acc[m][i] + acl[m][i] * kLo, 0.0f);  // (bias folded into layer 0)
+                }
+                split_f16(v, ah[s2], al[s2], bad);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int t = 0; t < KT1; ++t)
+#pragma unroll
+                for (int m = 0; m < NT1; ++m) {
+                    const f16x8 wh = as_f16x8(f1h[t][m]), wo = as_f16x8(f1l[t][m]);
+                    acc[m] = MFMA_F16(wh, ah[t], t == 0 ? z4 : acc[m], 0, 0, 0);
+                    acl[m] = MFMA_F16(wh, al[t], t == 0 ? z4 : acl[m], 0, 0, 0);
+                    acl[m] = MFMA_F16(wo, ah[t], acl[m], 0, 0, 0);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+            // the output layer: fragments and layer 1's biases at once
+            uint4 f2h[KT2], f2l[KT2];
+            f32x4 b1[KT2][2];
+            {
+                const int fl = a.frag_off[2], flo = a.frag_lo_off[2], bo = a.bias_off[1];
+#pragma unroll
+                for (int t = 0; t < KT2; ++t) {
+                    f2h[t] = frag_ld(fl + t * 64);
+                    f2l[t] = frag_ld(flo + t * 64);
+                    b1[t][0] = bias4(bo + 32 * t);
+                    b1[t][1] = bias4(bo + 32 * t + 16);
+                }
+            }
+            f16x8 ah2[KT2], al2[KT2];
+#pragma unroll
+            for (int s2 = 0; s2 < KT2; ++s2) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int m = 2 * s2 + (j >> 2), i = j & 3;
+                    v[j] = fmaxf((acc[m][i] + acl[m][i] * kLo) + b1[s2][j >> 2][i], 0.0f);
+                }
+                split_f16(v, ah2[s2], al2[s2], bad);
+            }
+#pragma unroll
+            for (int t = 0; t < KT2; ++t) {
+                const f16x8 wh = as_f16x8(f2h[t]), wo = as_f16x8(f2l[t]);
+                acc[0] = MFMA_F16(wh, ah2[t], t == 0 ? z4 : acc[0], 0, 0, 0);
+                acl[0] = MFMA_F16(wh, al2[t], t == 0 ? z4 : acl[0], 0, 0, 0);
+                acl[0] = MFMA_F16(wo, ah2[t], acl[0], 0, 0, 0);
+            }
+#endif
+            bprev = a.bias_off[2];
+        } else {
+            int nt_prev = nt0;
+            for (int l = 1; l <= a.n_hidden; ++l) {
+                const int nt_l = (l < a.n_hidden) ? a.nt[l] : 1;
+                layer(std::integral_constant<int, QN_MAXT>{}, std::integral_constant<int, QN_MAXT>{}, l, nt_prev, nt_l);
+                nt_prev = nt_l;
+            }
+            bprev = a.bias_off[a.n_hidden];
         }
+#ifdef DRL_QC_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t ts2 = __builtin_amdgcn_s_memtime();
+#endif
         const f32x4 bq = bias4(bprev);
         float q[8];
 #pragma unroll
@@ -756,9 +882,22 @@ __global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(Qn
             const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
             const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
             a.actions[env * a.action_stride] = (u < a.epsilon) ? rnd : best;
+#ifndef DRL_QC_STAMPS
             if (a.q)
                 for (int i = 0; i < a.n_actions; ++i) a.q[env * a.n_actions + i] = q[i];
+#endif
         }
+#ifdef DRL_QC_STAMPS
+        const uint64_t ts3 = __builtin_amdgcn_s_memtime();
+        if (lane == 0 && a.q) {
+            uint32_t* st = reinterpret_cast<uint32_t*>(a.q) + grp * 5;
+            st[0] = (uint32_t)(ts1 - ts0);
+            st[1] = (uint32_t)(ts2 - ts1);
+            st[2] = (uint32_t)(ts3 - ts2);
+            st[3] = (uint32_t)(ts0 - t_entry);
+            st[4] = (uint32_t)(ts3 - t_entry);
+        }
+#endif
     }
     if (__ballot(bad) && lane == 0 && a.err) atomicOr(a.err, DRL_ERR_QNET_RANGE);
     if (a.synth_n > 1) {  // as in drl_qnet_act_kernel (one 16-env tile per group)
@@ -773,6 +912,247 @@ __global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(Qn
                     const uint64_t ctr = (a.synth_step << 40) ^ ((uint64_t)(a.env_offset + env) << 8) ^ drone;
                     const uint64_t h = qn_splitmix64(a.synth_seed ^ qn_splitmix64(ctr));
                     a.actions[env * a.action_stride + (int64_t)drone] = (int32_t)(((h >> 32) * 5ull) >> 32);
+                }
+            }
+        }
+    }
+}
+
+// drl_qnet_act_code for the two-hidden-layer nets of the benchmark shape
+// (NT0 = 8, NT1 = hidden[1] / 16), two 16-env tiles per wave: layer 0 is
+// bound by the LDS bandwidth of its weight fragments (every tile reads the
+// whole 160 KB image), so each fragment read feeds both tiles' MFMAs -- half
+// the LDS bytes per env -- and each L2 fragment of the later layers serves
+// both tiles.  Same arithmetic, order and results as drl_qnet_act_code_kernel.
+template <int NT0, bool LO0, int WN, int NT1>
+__global__ void __launch_bounds__(64 * QN_CODE2_WAVES) drl_qnet_act_code2_kernel(QnetArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint4 wl[];
+    constexpr int TP = 2;
+    constexpr int CPG = lay::code_cpg(WN), CPG8 = lay::code_cpg8(WN), CELLS = WN * WN;
+    constexpr int NV = CPG8 / 8;                 // 16-B code vectors per lane group
+    constexpr int NB = 5 * CPG;                  // slots of the 0/1 channels
+    constexpr int KP = lay::code_kt(WN);         // layer 0's K-slices
+    constexpr int KT1 = NT0 / 2, KT2 = NT1 / 2;  // K-slices of layer 1 and of the output layer
+    static_assert(8 * KP > 6 * CPG, "no padding slot for layer 0's bias");
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int c = lane & 15, g = lane >> 4;
+    const int64_t ntiles = (a.E + 15) / 16;
+    const int64_t ngroups = (ntiles + TP - 1) / TP;
+    const int64_t gstride = (int64_t)gridDim.x * nw;
+    constexpr float kLo = 1.0f / 2048.0f;
+    const int ncell_g = min(CPG, CELLS - g * CPG);
+    const uint4* const code = reinterpret_cast<const uint4*>(a.obs);
+    auto load_codes = [&](int64_t tile, uint32_t (&dst)[4 * NV]) __attribute__((always_inline)) {
+        const int64_t env = min(tile * 16 + c, a.E - 1);
+        const uint4* src = code + env * (4 * NV) + g * NV;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const uint4 q = src[v];
+            dst[4 * v + 0] = q.x;
+            dst[4 * v + 1] = q.y;
+            dst[4 * v + 2] = q.z;
+            dst[4 * v + 3] = q.w;
+        }
+    };
+    const int64_t grp0 = (int64_t)blockIdx.x * nw + wave;
+    int64_t grp = grp0;
+    uint32_t cw[TP][4 * NV];
+#pragma unroll
+    for (int h = 0; h < TP; ++h) load_codes(TP * (grp < ngroups ? grp : 0) + h, cw[h]);
+    for (int v0 = wave * 64; v0 < a.lds_vec; v0 += 64 * nw)
+        if (v0 + lane < a.lds_vec)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(a.packed + v0 + lane),
+                                             (__attribute__((address_space(3))) void*)(wl + v0), 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    bool bad = false;
+    const uint4* W0 = wl + a.frag_off[0];
+    const uint4* W0lo = LO0 ? wl + a.frag_lo_off[0] : a.packed + a.frag_lo_off[0];
+    const float* bias = LO0 ? reinterpret_cast<const float*>(a.packed + a.bias_vec)
+                            : reinterpret_cast<const float*>(wl + a.frag_total);
+    const auto pbuf = __builtin_amdgcn_make_buffer_rsrc((void*)a.packed, 0, a.total_bytes, 0x00020000);
+    const int lane16 = lane * 16;
+    auto frag_ld = [&](int frag_u4) __attribute__((always_inline)) {
+        if constexpr (LO0) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(pbuf, lane16, frag_u4 * 16, 0);
+            uint4 r;
+            __builtin_memcpy(&r, &v, 16);
+            return r;
+        } else {
+            return wl[frag_u4 + lane];
+        }
+    };
+    auto bias4 = [&](int off) __attribute__((always_inline)) {
+        f32x4 r;
+        if constexpr (LO0) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(pbuf, 16 * g, a.bias_vec * 16 + off * 4, 0);
+            __builtin_memcpy(&r, &v, 16);
+        } else {
+            const float* bp = bias + off + 4 * g;
+            r = f32x4{bp[0], bp[1], bp[2], bp[3]};
+        }
+        return r;
+    };
+    const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+
+    for (; grp < ngroups; grp += gstride) {
+        const int64_t ngrp = grp + gstride;
+        uint32_t ncw[TP][4 * NV];  // the next group's codes, in flight while this one runs
+#pragma unroll
+        for (int h = 0; h < TP; ++h) load_codes(TP * (ngrp < ngroups ? ngrp : grp) + h, ncw[h]);
+        // ---- layer 0: each fragment read feeds both tiles
+        f32x4 acc[TP][NT0], acl[TP][NT0];
+#pragma unroll
+        for (int t = 0; t < KP; ++t) {
+            f16x8 bh[TP];  // inputs 0, 1 or an integer charge <= 100: exact in fp16
+#pragma unroll
+            for (int h = 0; h < TP; ++h) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int sl = 8 * t + j;  // compile-time slot
+                    const int l = sl < NB ? sl / 5 : sl - NB;
+                    const int ch = sl < NB ? (sl % 5 < 4 ? sl % 5 : 5) : 4;
+                    float x = (sl == 6 * CPG && g == 0) ? 1.0f : 0.0f;  // the bias slot (drl_qnet_pack)
+                    if (sl < 6 * CPG) {
+                        const uint32_t cd = (cw[h][l >> 1] >> (16 * (l & 1))) & 0xffffu;
+                        x = l < ncell_g ? code_channel(cd, ch) : 0.0f;
+                    }
+                    bh[h][j] = (_Float16)x;
+                }
+            }
+            int ts = t;  // opaque slice index (see drl_qnet_act_code_kernel)
+            asm volatile("" : "+s"(ts));
+#pragma unroll
+            for (int m = 0; m < NT0; ++m) {
+                const f16x8 wh = as_f16x8(W0[(m * KP + ts) * 64 + lane]);
+                const f16x8 wo = as_f16x8(W0lo[(m * KP + ts) * 64 + lane]);
+#pragma unroll
+                for (int h = 0; h < TP; ++h) {
+                    acc[h][m] = MFMA_F16(wh, bh[h], t == 0 ? z4 : acc[h][m], 0, 0, 0);
+                    acl[h][m] = MFMA_F16(wo, bh[h], t == 0 ? z4 : acl[h][m], 0, 0, 0);
+                }
+                if (m % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // <= 8 fragments in flight
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int h = 0; h < TP; ++h)
+#pragma unroll
+            for (int i = 0; i < 4 * NV; ++i) cw[h][i] = ncw[h][i];
+        // ---- layer 1 (bias folded into layer 0): inputs as fp16 hi/lo
+        f16x8 ah[TP][KT1], al[TP][KT1];
+#pragma unroll
+        for (int h = 0; h < TP; ++h)
+#pragma unroll
+            for (int s2 = 0; s2 < KT1; ++s2) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int m = 2 * s2 + (j >> 2), i = j & 3;
+                    v[j] = fmaxf(acc[h][m][i] + acl[h][m][i] * kLo, 0.0f);
+                }
+                split_f16(v, ah[h][s2], al[h][s2], bad);
+            }
+        f32x4 bcc[TP][NT1], bcl[TP][NT1];
+        {
+            const int fl = a.frag_off[1], flo = a.frag_lo_off[1];
+#pragma unroll
+            for (int t0 = 0; t0 < KT1; ++t0) {  // a K-slice's fragments at once (two: spills)
+                uint4 fh[1][NT1], fo[1][NT1];
+#pragma unroll
+                for (int u = 0; u < 1; ++u)
+#pragma unroll
+                    for (int m = 0; m < NT1; ++m) {
+                        fh[u][m] = frag_ld(fl + (m * KT1 + t0 + u) * 64);
+                        fo[u][m] = frag_ld(flo + (m * KT1 + t0 + u) * 64);
+                    }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < 1; ++u)
+#pragma unroll
+                    for (int m = 0; m < NT1; ++m) {
+                        const int t = t0 + u;
+                        const f16x8 wh = as_f16x8(fh[u][m]), wo = as_f16x8(fo[u][m]);
+#pragma unroll
+                        for (int h = 0; h < TP; ++h) {
+                            bcc[h][m] = MFMA_F16(wh, ah[h][t], t == 0 ? z4 : bcc[h][m], 0, 0, 0);
+                            bcl[h][m] = MFMA_F16(wh, al[h][t], t == 0 ? z4 : bcl[h][m], 0, 0, 0);
+                            bcl[h][m] = MFMA_F16(wo, ah[h][t], bcl[h][m], 0, 0, 0);
+                        }
+                    }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        // ---- the output layer: fragments and layer 1's biases at once
+        uint4 f2h[KT2], f2l[KT2];
+        f32x4 b1[KT2][2];
+        {
+            const int fl = a.frag_off[2], flo = a.frag_lo_off[2], bo = a.bias_off[1];
+#pragma unroll
+            for (int t = 0; t < KT2; ++t) {
+                f2h[t] = frag_ld(fl + t * 64);
+                f2l[t] = frag_ld(flo + t * 64);
+                b1[t][0] = bias4(bo + 32 * t);
+                b1[t][1] = bias4(bo + 32 * t + 16);
+            }
+        }
+        const f32x4 bq = bias4(a.bias_off[2]);
+#pragma unroll
+        for (int h = 0; h < TP; ++h) {
+            f16x8 ah2[KT2], al2[KT2];
+#pragma unroll
+            for (int s2 = 0; s2 < KT2; ++s2) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int m = 2 * s2 + (j >> 2), i = j & 3;
+                    v[j] = fmaxf((bcc[h][m][i] + bcl[h][m][i] * kLo) + b1[s2][j >> 2][i], 0.0f);
+                }
+                split_f16(v, ah2[s2], al2[s2], bad);
+            }
+            f32x4 qc, ql;
+#pragma unroll
+            for (int t = 0; t < KT2; ++t) {
+                const f16x8 wh = as_f16x8(f2h[t]), wo = as_f16x8(f2l[t]);
+                qc = MFMA_F16(wh, ah2[t], t == 0 ? z4 : qc, 0, 0, 0);
+                ql = MFMA_F16(wh, al2[t], t == 0 ? z4 : ql, 0, 0, 0);
+                ql = MFMA_F16(wo, ah2[t], ql, 0, 0, 0);
+            }
+            float q[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float own = (qc[i] + ql[i] * kLo) + bq[i];
+                const float hi = __shfl(own, c + 16);
+                q[i] = own;
+                q[i + 4] = hi;
+            }
+            const int64_t env = (TP * grp + h) * 16 + c;
+            if (g == 0 && env < a.E) {
+                int best = 0;
+                for (int i = 1; i < a.n_actions; ++i) best = q[i] > q[best] ? i : best;
+                const uint64_t ge = (uint64_t)(a.env_offset + env);
+                const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (ge << 8) ^ 0xa5ull));
+                const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
+                const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
+                a.actions[env * a.action_stride] = (u < a.epsilon) ? rnd : best;
+                if (a.q)
+                    for (int i = 0; i < a.n_actions; ++i) a.q[env * a.n_actions + i] = q[i];
+            }
+        }
+    }
+    if (__ballot(bad) && lane == 0 && a.err) atomicOr(a.err, DRL_ERR_QNET_RANGE);
+    if (a.synth_n > 1) {  // as in drl_qnet_act_kernel (TP 16-env tiles per group)
+        const uint32_t nd = (uint32_t)a.synth_n - 1u;
+        const uint32_t per = (uint32_t)(TP * 16) * nd;
+        for (int64_t gg = grp0; gg < ngroups; gg += gstride) {
+            for (uint32_t k = (uint32_t)lane; k < per; k += 64u) {
+                const uint32_t el = k / nd;
+                const int64_t env = TP * 16 * gg + el;
+                const uint64_t drone = 1u + (k - el * nd);
+                if (env < a.E) {
+                    const uint64_t ctr = (a.synth_step << 40) ^ ((uint64_t)(a.env_offset + env) << 8) ^ drone;
+                    const uint64_t hh = qn_splitmix64(a.synth_seed ^ qn_splitmix64(ctr));
+                    a.actions[env * a.action_stride + (int64_t)drone] = (int32_t)(((hh >> 32) * 5ull) >> 32);
                 }
             }
         }
@@ -878,10 +1258,18 @@ hipError_t launch_qnet_act_code(const QnetArgs& a, int window, int num_cus, hipS
     if (nb > num_cus) nb = num_cus;
     const dim3 grid((unsigned)nb), block(64 * waves);
     const size_t lds = (size_t)a.lds_vec * 16;
-#define QN_CODE_LAUNCH(NT, W)                                                                               \
-    if (a.lo0_lds) hipLaunchKernelGGL((drl_qnet_act_code_kernel<NT, true, W>), grid, block, lds, s, a);    \
-    else hipLaunchKernelGGL((drl_qnet_act_code_kernel<NT, false, W>), grid, block, lds, s, a)
+    int64_t nb2 = ((nt + 1) / 2 + QN_CODE2_WAVES - 1) / QN_CODE2_WAVES;  // (two tiles per wave)
+    if (nb2 > num_cus) nb2 = num_cus;
+    const dim3 grid2((unsigned)nb2), block2(64 * QN_CODE2_WAVES);
+#define QN_CODE_LAUNCH(NT, W)                                                                                   \
+    if (a.lo0_lds) hipLaunchKernelGGL((drl_qnet_act_code_kernel<NT, true, W, 0>), grid, block, lds, s, a);     \
+    else hipLaunchKernelGGL((drl_qnet_act_code_kernel<NT, false, W, 0>), grid, block, lds, s, a)
+#define QN_CODE_SPEC(W)                                                                                         \
+    if (a.lo0_lds) hipLaunchKernelGGL((drl_qnet_act_code2_kernel<8, true, W, 4>), grid2, block2, lds, s, a);   \
+    else hipLaunchKernelGGL((drl_qnet_act_code2_kernel<8, false, W, 4>), grid2, block2, lds, s, a)
+    const bool spec = a.n_hidden == 2 && a.nt[0] == 8 && a.nt[1] == 4;  // 128 -> 64 hidden
 #define QN_CODE_W(W)                             \
+    if (spec) { QN_CODE_SPEC(W); } else           \
     switch (a.nt[0]) {                            \
         case 2: QN_CODE_LAUNCH(2, W); break;      \
         case 4: QN_CODE_LAUNCH(4, W); break;      \
@@ -896,6 +1284,7 @@ hipError_t launch_qnet_act_code(const QnetArgs& a, int window, int num_cus, hipS
         default: return hipErrorInvalidValue;
     }
 #undef QN_CODE_W
+#undef QN_CODE_SPEC
 #undef QN_CODE_LAUNCH
     return hipGetLastError();
 }

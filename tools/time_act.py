@@ -18,6 +18,10 @@ def main():
     ap.add_argument("--stride", type=int, default=294, help="obs row stride in floats (296: 16-B aligned rows)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--input", default="obs", choices=["obs", "code"], help="code: drl_qnet_act_code (f32)")
+    ap.add_argument("--synth", action="store_true", help="also write drones 1..7's synthetic actions (act_synth)")
+    ap.add_argument("--stamps", action="store_true", help="library built with -DDRL_QC_STAMPS: phase cycles")
+    ap.add_argument("--flush", action="store_true",
+                    help="overwrite 256 MB between launches (cold L2/MALL, as after a step) and time each launch")
     args = ap.parse_args()
     if args.lib:
         import dronerl_amd._native as nat
@@ -42,17 +46,44 @@ def main():
             env.step(env.synth_actions(seed=1, step=t), obs_k=1, code=flat)
     for _ in range(20):
         net.act(flat, 0.1, actions=a)
+    syn = (lambda t: (5, t)) if args.synth else (lambda t: None)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
-    e0.record()
-    for t in range(args.iters):
-        net.act(flat, 0.1, step=t, actions=a)
-    e1.record()
-    torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) * 1e3 / args.iters
+    if args.flush:
+        junk = torch.empty(64 << 20, dtype=torch.float32, device="cuda")
+        tot = 0.0
+        for t in range(args.iters):
+            junk.fill_(float(t))
+            e0.record()
+            net.act(flat, 0.1, step=t, actions=a, synth=syn(t))
+            e1.record()
+            torch.cuda.synchronize()
+            tot += e0.elapsed_time(e1)
+        us = tot * 1e3 / args.iters
+    else:
+        e0.record()
+        for t in range(args.iters):
+            net.act(flat, 0.1, step=t, actions=a, synth=syn(t))
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / args.iters
+    if args.stamps:
+        q = torch.zeros((E, 5), device="cuda")
+        net.act(flat, 0.1, actions=a, q_out=q)
+        torch.cuda.synchronize()
+        st = q.view(torch.int32).cpu().numpy().astype("int64")[: (E + 15) // 16]
+        import numpy as np
+        for i, name in enumerate(("layer0", "hidden", "epilogue")):
+            v = st[:, i]
+            print(f"stamps {name}: median {np.median(v):.0f} p10 {np.percentile(v, 10):.0f} "
+                  f"p90 {np.percentile(v, 90):.0f} cycles (s_memtime)")
+        t0 = st[:, 3] & 0xffffffff
+        t3 = st[:, 4] & 0xffffffff
+        print(f"tile start since kernel entry: min {t0.min()} median {np.median(t0):.0f} max {t0.max()}; "
+              f"tile end: median {np.median(t3):.0f} max {t3.max()} cycles")
     nb = flat.shape[1] * flat.element_size()
     print(f"{os.path.basename(args.lib) or 'libdronerl.so'} E={E} hidden={args.hidden} {args.precision} "
-          f"input={args.input}: {us:.2f} us/launch, {E * nb / us / 1e3:.0f} GB/s input read ({nb} B/env)")
+          f"input={args.input}{' synth' if args.synth else ''}{' flushed' if args.flush else ''}: {us:.2f} us/launch, {E * nb / us / 1e3:.0f} GB/s input read ({nb} B/env)")
 
 
 if __name__ == "__main__":
