@@ -594,6 +594,13 @@ def loop_input(args, env) -> str:
     return "code" if args.loop_precision == "f32" and env.layout.obs_window in (5, 7, 9) else "obs"
 
 
+# refill cycles of untimed steps after the reset, before the warm-up: the
+# refills measured there (all but the first two) price the timed region's
+# pro-rated refill share at short step counts (tools/refill_time.py: the
+# steady state needs a few cycles after a reset)
+PRE_ROLL_CYCLES = 8
+
+
 def refill_plan(pre: int, warmup: int, steps: int, every: int):
     """env.step()'s refill cadence over one bench run: drl_refill follows
     global step s when (s + 1) % every == 0, counting from the first pre-roll
@@ -692,10 +699,13 @@ class StepRunner:
         plan, charge = refill_plan(0, self.s - steps, steps, self.every)
         assert len(plan) == len(inside), (plan, len(inside))
         ref_in_ms = sum(a.elapsed_time(b) for a, b, _ in inside)
-        # the refill's average launch: every one measured except the first
-        # after the reset (the pre-roll's, on a cold machine)
+        # the refill's average launch: every one measured except the first two
+        # after the reset (the first fills the empty rings; the rings of all
+        # envs then cross block ends in step, so the next few refills are
+        # lighter than the steady state a long run sees -- hence the pre-roll
+        # of PRE_ROLL_CYCLES refill cycles)
         all_ms = [a.elapsed_time(b) for a, b, _ in self.refill_ev]
-        use = all_ms[1:] if len(all_ms) > 1 else all_ms
+        use = all_ms[2:] if len(all_ms) > 2 else all_ms[-1:]
         refill_avg_s = max_over_ranks(sum(use) / len(use) / 1e3 if use else 0.0, world)
         region_s = max_over_ranks(ev0.elapsed_time(ev1) / 1e3, world)
         charged = region_s + charge * refill_avg_s
@@ -773,7 +783,7 @@ def pmc_child(args):
             K = args.obs_k
         stream = args.obs_stream or (env.default_obs_stream and not args.obs_cached)
         run = StepRunner(env, K, 8, stream)
-        run.run(args.steps, args.warmup, 1, pre=2 * env.refill_every)
+        run.run(args.steps, args.warmup, 1, pre=PRE_ROLL_CYCLES * env.refill_every)
         P = env.layout.step_group_lanes
         grids[name] = {"envs": E, "step_grid": -(-E // (64 // P)) * 64, "refill_grid": -(-E // 4) * 64}
         del run, env
@@ -850,7 +860,7 @@ def main():
     # ---- the headline: setup rolls one refill cycle (steady-state rings),
     # then W warm-up and K timed steps
     runner = StepRunner(env, K, args.warmup + args.steps + 2 * env.refill_every, args.obs_stream)
-    main_res = runner.run(args.steps, args.warmup, world, pre=2 * env.refill_every)
+    main_res = runner.run(args.steps, args.warmup, world, pre=PRE_ROLL_CYCLES * env.refill_every)
     actions, rewards, dones, obs, stream = runner.actions, runner.rewards, runner.dones, runner.obs, runner.stream
 
     def traffic_of(name):
@@ -924,7 +934,7 @@ def main():
         st5 = env5.default_obs_stream
         steps5 = max(args.c5_steps, 200)
         run5 = StepRunner(env5, K5, steps5 + 20 + 2 * env5.refill_every, st5)
-        r5 = run5.run(steps5, 20, world, pre=2 * env5.refill_every)
+        r5 = run5.run(steps5, 20, world, pre=PRE_ROLL_CYCLES * env5.refill_every)
         R5, W5 = algorithmic_bytes(G5, N5, K5, env5.layout.obs_window)
         c5 = {"value": r5["value"], "unit": "env-steps/s", "n_gpus": world, "steps": steps5, "warmup": 20,
               "ms_per_step": r5["ms_per_step"], "wall_ms_per_step": r5["wall_ms_per_step"],
@@ -963,8 +973,8 @@ def main():
                        "grid": G, "n_drones": N, "num_envs_per_gpu": E, "num_envs_total": E * world,
                        "obs_k": K, "obs_stores": "streaming" if args.obs_stream else "cached",
                        "parallelism": f"env-shard x{world}",
-                       "setup": f"reset(seed=0), then {2 * main_res['refill']['every']} pre-roll steps (two refill "
-                                "cycles: steady-state candidate rings) before the warm-up"},
+                       "setup": f"reset(seed=0), then {PRE_ROLL_CYCLES * main_res['refill']['every']} pre-roll steps "
+                                f"({PRE_ROLL_CYCLES} refill cycles: steady-state candidate rings) before the warm-up"},
             "wall_ms_per_step": main_res["wall_ms_per_step"],
             "roofline": roofline(E, R, Wb, main_res["launch_s"], main_res["refill"], traffic_of(args.config)),
             "refill": main_res["refill"],

@@ -94,8 +94,15 @@ def test_refill_share_charged_at_any_step_count(pre, warmup, steps, every):
 
 
 def test_driver_run_charges_a_refill():
-    inside, charge = bench.refill_plan(32, 5, 20, 32)
+    inside, charge = bench.refill_plan(bench.PRE_ROLL_CYCLES * 32, 5, 20, 32)
     assert inside == [] and charge == pytest.approx(20 / 32)
+
+
+def test_pre_roll_prices_the_refill_in_steady_state():
+    """The pro-rated refill of a short run is priced by the pre-roll's refills
+    minus the first two after the reset (lighter than the steady state):
+    enough cycles remain to average."""
+    assert bench.PRE_ROLL_CYCLES - 2 >= 4
 
 
 def test_roofline_fractions_stay_below_one():
