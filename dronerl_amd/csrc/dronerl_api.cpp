@@ -223,6 +223,8 @@ int launch_refill(const drl_params* p, const drl_state* s, hipStream_t stream) {
     a.E = s->num_envs;
     a.mt = s->mt;
     a.mt_index = s->mt_index;
+    const char* lv = getenv("DRL_REFILL_LIST");  // 0: the wave-per-env kernel (A/B)
+    a.list = lv ? atoi(lv) != 0 : 1;
     hipError_t e = drl::launch_refill(a, stream);
     return e == hipSuccess ? 0 : hip_fail(e, "drl_refill launch");
 }

@@ -181,6 +181,7 @@ struct StepArgs {
 
 struct RefillArgs {
     int side, kbits;
+    int list;  // 1: drl_refill_list_kernel (a per-workgroup worklist of the envs to convert); 0: one wave per env
     int64_t E;
     uint32_t* mt;
     uint32_t* mt_index;

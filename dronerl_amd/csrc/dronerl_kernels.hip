@@ -2159,6 +2159,62 @@ __global__ void __launch_bounds__(64 * kRefillWaves) drl_refill_kernel(RefillArg
         if (need[e]) refill_env(a, env0 + e, mw[e], rend[e], from[e], x[e], lane);
 }
 
+// Worklist form (the default; DRL_REFILL_LIST=0 selects the wave-per-env
+// kernel above): a workgroup owns kRefillListEnvs consecutive envs.  Its first
+// wave reads their mt_index and ring-end words (one lane per env: two vector
+// loads instead of a wave and two scalar round trips per env) and lists the
+// envs that need a conversion in LDS; then the workgroup's waves take the
+// listed envs in turn, so no wave is spent on an env with nothing to convert.
+// At the benchmark cadences 40-60 % of the envs convert per refill, and a
+// conversion moves ~5.6 KB (block s read, block s+1 written, ~156 entries):
+// both forms run those bytes at ~5.6 TB/s, so the worklist saves only the
+// per-env overhead: 2-6 % per refill, paired on identical states (C3 46.9 vs
+// 50.0 us, C4 52.1 vs 52.3, C5 103.8 vs 106.3; 64 envs with 8 or 16 waves per
+// workgroup measured no better; profiles/r03_refill/).
+constexpr int kRefillListEnvs = 32, kRefillListWaves = 8;
+template <int NENV, int NW>  // envs per workgroup (<= 64), waves per workgroup
+__global__ void __launch_bounds__(64 * NW) drl_refill_list_kernel(RefillArgs a) {
+    __shared__ uint32_t q_mw[64], q_rend[64];
+    __shared__ int q_env[64], q_from[64];
+    __shared__ int q_n;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t base = (int64_t)xcd_block(blockIdx.x, gridDim.x) * NENV;
+    if (wv == 0) {
+        const int64_t ev = base + lane;
+        const bool ok = lane < NENV && ev < a.E;
+        const int64_t evc = ok ? ev : a.E - 1;
+        const uint32_t mw = a.mt_index[evc];
+        const uint32_t rend = a.mt[evc * MT_WORDS + MT_RING_END];
+        const int cnt = mi_cnt(mw), spar = mi_par(mw);
+        const int from = cnt > 0 ? min((int)(rend & 0x3ffu), MT_N) + ((int)((rend >> 10) & 1u) != spar ? MT_N : 0)
+                                 : min(mi_idx(mw), MT_N);
+        const bool need = ok && from <= MT_N;
+        const uint64_t M = __ballot(need);
+        if (need) {
+            const int k = mbcnt64(M);
+            q_env[k] = lane;
+            q_mw[k] = mw;
+            q_rend[k] = rend;
+            q_from[k] = from;
+        }
+        if (lane == 0) q_n = __popcll(M);
+    }
+    __syncthreads();
+    const int n = __builtin_amdgcn_readfirstlane(q_n);
+    for (int q = wv; q < n; q += NW) {
+        const int64_t env = base + __builtin_amdgcn_readfirstlane(q_env[q]);
+        const uint32_t mw = __builtin_amdgcn_readfirstlane(q_mw[q]);
+        const uint32_t rend = __builtin_amdgcn_readfirstlane(q_rend[q]);
+        const int from = __builtin_amdgcn_readfirstlane(q_from[q]);
+        const uint32_t* src = a.mt + env * MT_WORDS + (uint32_t)mi_par(mw) * MT_ALT;
+        uint32_t x[10];
+#pragma unroll
+        for (int c = 0; c < 10; ++c) x[c] = (64 * c + lane < MT_N) ? src[64 * c + lane] : 0u;
+        refill_env(a, env, mw, rend, from, x, lane);
+    }
+}
+
 // ------------------------------------------------------- synthetic actions ---
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
     z += 0x9e3779b97f4a7c15ull;
@@ -2304,6 +2360,12 @@ hipError_t launch_encode(uint32_t* drones, int64_t E, int N, const int32_t* orde
 }
 
 hipError_t launch_refill(const RefillArgs& a, hipStream_t s) {
+    if (a.list) {
+        hipLaunchKernelGGL((drl_refill_list_kernel<kRefillListEnvs, kRefillListWaves>),
+                           dim3((unsigned)((a.E + kRefillListEnvs - 1) / kRefillListEnvs)), dim3(64 * kRefillListWaves),
+                           0, s, a);
+        return hipGetLastError();
+    }
     const int64_t blocks = (a.E + kRefillWaves * kRefillEnvs - 1) / (kRefillWaves * kRefillEnvs);
     hipLaunchKernelGGL(drl_refill_kernel, dim3((unsigned)blocks), dim3(64 * kRefillWaves), 0, s, a);
     return hipGetLastError();

@@ -221,6 +221,7 @@ def test_rollout_matches_oracle(name, E, steps, every, monkeypatch):
     env.check_errors()
 
 
+@pytest.mark.parametrize("refill_kernel", ["list", "wave"])
 @pytest.mark.parametrize("refill", [0, 1, 3])
 @pytest.mark.parametrize("name,E,steps", [
     ("c1_8x8_n4", 256, 120),
@@ -230,12 +231,16 @@ def test_rollout_matches_oracle(name, E, steps, every, monkeypatch):
     ("c5_64x64_n32", 96, 60),
     ("bigside_128_n4", 40, 60),
 ])
-def test_candidate_ring_cadence_matches_oracle(name, E, steps, refill):
+def test_candidate_ring_cadence_matches_oracle(name, E, steps, refill, refill_kernel, monkeypatch):
     """The respawn-candidate ring never changes results: topped up every step
     (refill 1), every 3rd, or never after the reset's fill (0: it runs dry and
     every later respawn is drawn from the stream in the step, from the end of
     the ring's last entry, which may lie in the next MT block).  Rewards, dones
-    and the full state, MT words included, equal the oracle at every step."""
+    and the full state, MT words included, equal the oracle at every step.
+    refill_kernel "list": drl_refill's worklist form (the default), "wave": one
+    wave per env (DRL_REFILL_LIST=0)."""
+    if refill_kernel == "wave":
+        monkeypatch.setenv("DRL_REFILL_LIST", "0")
     p = EnvParams(**CONFIGS[name])
     env = Env(p, E)
     env.refill_every = refill
@@ -741,7 +746,8 @@ def test_reset_states_fixture_on_gpu(name, kernel, monkeypatch):
 
 @pytest.mark.parametrize("name", ["c1_8x8_n4", "c2_16x16_n8", "c5_64x64_n32", "bigside_128_n4", "n6_11x11",
                                   "n1_5x5"])
-def test_candidate_ring_holds_the_streams_randint_pairs(name):
+@pytest.mark.parametrize("refill_kernel", ["list", "wave"])
+def test_candidate_ring_holds_the_streams_randint_pairs(name, refill_kernel, monkeypatch):
     """drl_refill's ring, entry by entry, against CPython's own generator:
     entry k is the k-th (randint(0, side-1), randint(0, side-1)) pair drawn
     from the env's stream (random.setstate of its getstate words), with the MT
@@ -752,6 +758,8 @@ def test_candidate_ring_holds_the_streams_randint_pairs(name):
     in the other block's words.  Checked after the reset's conversion and
     again mid-run (partly consumed, wrapped, converted again)."""
     import random
+    if refill_kernel == "wave":
+        monkeypatch.setenv("DRL_REFILL_LIST", "0")
     from dronerl_amd._native import DRL_CAND_SLOTS as CAP, DRL_MT_RING as RING, DRL_MT_RING_END as RING_END
     p = EnvParams(**CONFIGS[name])
     G, E = p.side, 48

@@ -33,7 +33,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c3,c5")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--variants", default="wave", help="list (drl_refill_list_kernel, the default), wave (DRL_REFILL_LIST=0: "
+                    "drl_refill_kernel); "
+                    "each timed on the same state per rep")
     args = ap.parse_args()
+    variants = args.variants.split(",")
     s = torch.cuda.current_stream()
     for name in args.configs.split(","):
         G, N, E = CFG[name]
@@ -44,19 +48,36 @@ def main():
         for t in range(2 * every):
             env.step(env.synth_actions(seed=1, step=t), obs_k=1, obs=obs)
         env.refill_every = 0
-        ts, dry = [], []
+        tsv, dry, convs = {v: [] for v in variants}, [], {}
         for r in range(args.reps):
             for t in range(every):
                 env.step(env.synth_actions(seed=5, step=1000 + r * every + t), obs_k=1, obs=obs)
             dry.append(float((((env.state.mt_index >> 20) & 1023) == 0).float().mean()))
-            ts.append(timed_refill(env, s))
+            # every variant refills the same state (paired: same conversions)
+            snap = env.state.clone()
+            for v in variants[r % len(variants):] + variants[:r % len(variants)]:
+                env.state = snap.clone()
+                os.environ["DRL_REFILL_LIST"] = "1" if v == "list" else "0"
+                cnt0 = (env.state.mt_index >> 20) & 1023
+                tsv[v].append(timed_refill(env, s))
+                conv = int((((env.state.mt_index >> 20) & 1023) > cnt0).sum())  # envs whose ring grew
+                convs.setdefault(v, []).append(conv)
+        os.environ.pop("DRL_REFILL_LIST", None)
         env.check_errors()
-        ts.sort()
-        med = ts[len(ts) // 2]
-        print(json.dumps({"config": name, "envs": E, "refill_every": every, "refill_us_median": round(med, 2),
-                          "refill_us_min": round(ts[0], 2), "per_step_us": round(med / every, 3),
-                          "dry_fraction_mean": sum(dry) / len(dry), "lib": os.environ.get("DRL_LIB", "in-tree")}),
-              flush=True)
+        for v, ts in tsv.items():
+            print(json.dumps({"config": name, "variant": v, "us_and_converted": [[round(t, 1), c] for t, c in
+                                                                                zip(ts, convs[v])]}), flush=True)
+            ts.sort()
+            med = ts[len(ts) // 2]
+            cv = convs[v]
+            print(json.dumps({"config": name, "variant": v, "envs": E, "refill_every": every,
+                              "refill_us_median": round(med, 2), "refill_us_min": round(ts[0], 2),
+                              "refill_us_mean": round(sum(ts) / len(ts), 2),
+                              "per_step_us_mean": round(sum(ts) / len(ts) / every, 3),
+                              "converted_envs_mean": sum(cv) / len(cv), "converted_envs_min": min(cv),
+                              "converted_envs_max": max(cv),
+                              "per_step_us": round(med / every, 3), "dry_fraction_mean": sum(dry) / len(dry),
+                              "lib": os.environ.get("DRL_LIB", "in-tree")}), flush=True)
         del env, obs
         torch.cuda.empty_cache()
 
