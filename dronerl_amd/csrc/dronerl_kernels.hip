@@ -1573,7 +1573,11 @@ __device__ __forceinline__ void fy_swaps(const FyLds& f, uint64_t S, int m, bool
     const int ii = si0 - t;    // >= 0 on every lane (t <= m <= si0)
     const int slot = si0 - j;  // j's rank if j lies in the i range; rejected lanes: si0 >= m, none
     const uint32_t bit = acc ? 1u << (j >> f.bshift) : 0u;
-    uint32_t* const pw = f.bmap + (j & f.bmask);
+    // (rejected lanes OR / AND a zero bit into a word of their own: with one
+    // shared word (j = 0) their ~18 atomics per chunk serialised on one bank,
+    // C5 17.6e6 -> 19.3e6 resets/s; zeroing the whole bitmap with plain
+    // stores instead of the AND measured slower, 18.1e6; profiles/r03_reset_occ/)
+    uint32_t* const pw = f.bmap + ((acc ? j : lane) & f.bmask);
     uint16_t* const pi = list + ii;
     uint16_t* const pj = list + j;
     uint16_t* const pd = list + f.dummy + lane;
