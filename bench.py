@@ -103,7 +103,8 @@ def under_profiler():
 TORCHRUN_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
                  "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
 
-PMC_KERNELS = ("drl_step_kernel", "drl_refill_kernel")
+# (drl_refill_list_kernel: the refill's default form since round 3; drl_refill_kernel under DRL_REFILL_LIST=0)
+PMC_KERNELS = ("drl_step_kernel", "drl_refill_list_kernel", "drl_refill_kernel")
 
 
 def child_env():
@@ -116,7 +117,7 @@ def child_env():
 
 
 def measure_traffic(args, names):
-    """HBM bytes per launch of drl_step_kernel and drl_refill_kernel for each
+    """HBM bytes per launch of drl_step_kernel and drl_refill(_list)_kernel for each
     config in `names`, from rocprofv3 PMC passes of this same bench
     (MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE in separate passes,
     FETCH_SIZE doubled for gfx950, KiB -> bytes).  One child process per
@@ -177,7 +178,8 @@ def measure_traffic(args, names):
     out = {}
     for name, g in grids.items():
         rec = {}
-        for kern, key in (("drl_step_kernel", "step_grid"), ("drl_refill_kernel", "refill_grid")):
+        for kern, key in (("drl_step_kernel", "step_grid"), ("drl_refill_list_kernel", "refill_list_grid"),
+                          ("drl_refill_kernel", "refill_grid")):
             f = rows.get(("FETCH_SIZE", kern, g[key]))
             w = rows.get(("WRITE_SIZE", kern, g[key]))
             if not f or not w:
@@ -749,7 +751,7 @@ def roofline(E, R, Wb, launch_s, refill, traffic):
         out["traffic"] = st["bytes_per_launch"]
         out["frac_measured"] = st["bytes_per_launch"] / launch_s / 1e9 / PEAK_HBM_GBS
         out["traffic_detail"] = dict(st, source=traffic.get("source"), envs=traffic.get("envs"))
-        rf = traffic.get("drl_refill_kernel")
+        rf = traffic.get("drl_refill_list_kernel") or traffic.get("drl_refill_kernel")
         if rf and refill["every"] > 0:
             per_step_b = st["bytes_per_launch"] + rf["bytes_per_launch"] / refill["every"]
             out["with_refill"].update({"traffic_per_step": per_step_b,
@@ -785,7 +787,8 @@ def pmc_child(args):
         run = StepRunner(env, K, 8, stream)
         run.run(args.steps, args.warmup, 1, pre=PRE_ROLL_CYCLES * env.refill_every)
         P = env.layout.step_group_lanes
-        grids[name] = {"envs": E, "step_grid": -(-E // (64 // P)) * 64, "refill_grid": -(-E // 4) * 64}
+        grids[name] = {"envs": E, "step_grid": -(-E // (64 // P)) * 64, "refill_grid": -(-E // 4) * 64,
+                       "refill_list_grid": -(-E // 32) * 512}
         del run, env
         torch.cuda.synchronize()
         torch.cuda.empty_cache()

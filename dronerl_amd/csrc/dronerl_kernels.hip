@@ -1576,7 +1576,9 @@ __device__ __forceinline__ void fy_swaps(const FyLds& f, uint64_t S, int m, bool
     // (rejected lanes OR / AND a zero bit into a word of their own: with one
     // shared word (j = 0) their ~18 atomics per chunk serialised on one bank,
     // C5 17.6e6 -> 19.3e6 resets/s; zeroing the whole bitmap with plain
-    // stores instead of the AND measured slower, 18.1e6; profiles/r03_reset_occ/)
+    // stores instead of the AND measured slower, 18.1e6, and so did skipping
+    // the rejected lanes' atomics under an exec mask, 18.9e6, while a dword
+    // per dummy slot changed nothing; profiles/r03_reset_occ/)
     uint32_t* const pw = f.bmap + ((acc ? j : lane) & f.bmask);
     uint16_t* const pi = list + ii;
     uint16_t* const pj = list + j;
