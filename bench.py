@@ -449,12 +449,15 @@ class TrainSegment:
     transition; after `seg` steps a reset of every env (reset_env_every,
     train_jax.py:101-113) and its first observation.
 
-    fused=True (one stream only): the synthetic actions of drones 1..N-1 are
-    written by the act launch itself (drl_qnet_act_synth), one kernel fewer
-    per step with the same action rows.
+    fused=True: the synthetic actions of drones 1..N-1 are written by the act
+    launch itself (drl_qnet_act_synth), one kernel fewer per step with the
+    same action rows.
 
-    parallel=True: the synthetic actions and the replay add run on two side
-    streams, joined to the act -> step chain by events.  Observations, actions,
+    parallel=True: the replay add (and, unfused, the synthetic actions) run on
+    side streams, joined to the act -> step chain by events; so does the
+    respawn-candidate refill (env.step()'s cadence, launched on its own branch
+    after the step it follows: it overlaps the next act, and the next step
+    waits for it).  Observations, actions,
     rewards and dones rotate through 3 buffers, so step t only waits for the
     replay add of step t-2 and the actions of step t are drawn while step t-1
     runs.  parallel=False issues the same calls in the same order on one
@@ -473,7 +476,7 @@ class TrainSegment:
         # (f32 nets; Q to 1e-5 of the f32 forward) and the replay buffer
         # stores code rows, decoding the rows it samples to the observation
         self.input = input
-        self.fused = fused and not parallel
+        self.fused = fused
         # parallel branches need 3 rotating buffers (see above); on one stream 2
         # suffice, and the third 77 MB observation buffer costs MALL hits (C3
         # loop 79.4 vs 74.4 us per step)
@@ -489,7 +492,7 @@ class TrainSegment:
         else:
             self.obs = [torch.empty((E, 1, W, W, 6), dtype=torch.float32, device=dev) for _ in range(self.NB)]
         self._first_obs()
-        self.s_syn, self.s_rep = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        self.s_syn, self.s_rep, self.s_ref = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
 
     def _first_obs(self):
         if self.input == "code":
@@ -500,11 +503,13 @@ class TrainSegment:
     def _synth(self, t):
         self.env.synth_actions(seed=2024, step=t, out=self.acts[t % self.NB])
 
-    def _act_step(self, t):
+    def _act_step(self, t, before_step=None):
         b, nb = t % self.NB, (t + 1) % self.NB
         x = self.code[b] if self.input == "code" else self.obs[b].reshape(self.E, -1)
         self.net.act(x, 0.1, seed=7, step=t, env_offset=self.env.env_offset,
                      actions=self.acts[b], synth=(2024, t) if self.fused else None)
+        if before_step is not None:  # (parallel: the refill branch joins here)
+            before_step()
         if self.input == "code":
             self.env.step(self.acts[b], rewards=self.rewards[b], dones=self.dones[b], code=self.code[nb])
         else:
@@ -527,25 +532,44 @@ class TrainSegment:
             ev_syn = [torch.cuda.Event() for _ in range(self.seg)]
             ev_step = [torch.cuda.Event() for _ in range(self.seg)]
             ev_rep = [torch.cuda.Event() for _ in range(self.seg)]
+            ev_ref = None
+            every = self.env.refill_every
+            self.env.refill_every = 0  # (the refills below, on their own branch)
+            since = self.env._since_refill
             self.s_syn.wait_stream(main)
             self.s_rep.wait_stream(main)
             for t in range(self.seg):
-                with torch.cuda.stream(self.s_syn):
-                    if t >= self.NB:  # acts[t % 3] was last read by the replay add of step t-3
-                        self.s_syn.wait_event(ev_rep[t - self.NB])
-                    self._synth(t)
-                    ev_syn[t].record(self.s_syn)
-                main.wait_event(ev_syn[t])
+                if not self.fused:
+                    with torch.cuda.stream(self.s_syn):
+                        if t >= self.NB:  # acts[t % 3] was last read by the replay add of step t-3
+                            self.s_syn.wait_event(ev_rep[t - self.NB])
+                        self._synth(t)
+                        ev_syn[t].record(self.s_syn)
+                    main.wait_event(ev_syn[t])
+                elif t >= self.NB:  # the act writes acts[t % 3], read by the replay add of step t-3
+                    main.wait_event(ev_rep[t - self.NB])
                 if t >= 2:  # step t overwrites obs[(t+1) % 3], read by the replay add of step t-2
                     main.wait_event(ev_rep[t - 2])
-                self._act_step(t)
+                self._act_step(t, before_step=(lambda e=ev_ref: main.wait_event(e)) if ev_ref is not None else None)
+                ev_ref = None
                 ev_step[t].record(main)
+                since += 1
+                if every > 0 and since >= every:
+                    since = 0
+                    with torch.cuda.stream(self.s_ref):
+                        self.s_ref.wait_event(ev_step[t])
+                        self.env.refill()
+                        ev_ref = torch.cuda.Event()
+                        ev_ref.record(self.s_ref)
                 with torch.cuda.stream(self.s_rep):
                     self.s_rep.wait_event(ev_step[t])
                     self._replay(t)
                     ev_rep[t].record(self.s_rep)
             main.wait_stream(self.s_syn)
             main.wait_stream(self.s_rep)
+            main.wait_stream(self.s_ref)
+            self.env.refill_every = every
+            self.env._since_refill = since
         self.env.reset(seed=None)
         self._first_obs()
 
@@ -578,8 +602,9 @@ def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fus
     env.check_errors()
     dt = e0.elapsed_time(e1) / 1e3
     E = env.num_envs
-    branches = ("synthetic actions and replay add_many on parallel graph branches, 3 rotating buffers"
-                if parallel else "one stream" + ("; synthetic actions inside the act launch" if fused else ""))
+    branches = (("replay add_many" if fused else "synthetic actions and replay add_many") +
+                " on parallel graph branches, 3 rotating buffers" if parallel else "one stream") + \
+        ("; synthetic actions inside the act launch" if fused else "")
     return {"env_steps_per_s": E * seg * reps / dt, "us_per_step": dt / (seg * reps) * 1e6,
             "segments": reps, "steps_per_segment": seg, "precision": precision, "input": input,
             "loop": f"hipGraph of {seg} x [synth actions -> qnet act (drone 0, {precision}, input {input}) -> "
@@ -822,8 +847,9 @@ def main():
     ap.add_argument("--unfused-act", action="store_true",
                     help="train loop: synthetic actions as their own launch instead of inside the act launch")
     ap.add_argument("--parallel-loop", action="store_true",
-                    help="train loop with synth / replay on parallel graph branches (measured slower: the step "
-                         "kernel fills every CU in one generation, and co-running kernels delay its waves)")
+                    help="train loop with the replay add (and unfused synth) on parallel graph branches (with the "
+                         "f32 observation: slower, the step kernel fills every CU in one generation and co-running "
+                         "kernels delay its waves)")
     ap.add_argument("--obs-stream", action="store_true",
                     help="write the per-step observation with streaming stores (DRL_STEP_OBS_STREAM); default: "
                          "env.step()'s mode (cached at 8 lanes per env, streaming at >= 16)")

@@ -701,7 +701,7 @@ def test_train_segment_parallel_matches_serial():
     p = EnvParams(n_drones=8, grid_size=16)
     E, seg = 3000, 13
     runs = []
-    for parallel, fused in ((False, False), (True, False), (False, True)):
+    for parallel, fused in ((False, False), (True, False), (False, True), (True, True)):
         env = Env(p, E)
         env.reset(seed=5)
         loop = TrainSegment(env, seg, parallel=parallel, fused=fused)
@@ -711,7 +711,7 @@ def test_train_segment_parallel_matches_serial():
         env.check_errors()
         runs.append((gpu_state(env), loop))
     g0, l0 = runs[0]
-    for name, (g1, l1) in zip(("parallel", "fused"), runs[1:]):
+    for name, (g1, l1) in zip(("parallel", "fused", "parallel fused"), runs[1:]):
         assert_state(g1, g0, f"{name} vs serial segments")
         for k in ("obs", "next_obs", "actions", "rewards", "dones"):
             assert torch.equal(getattr(l0.rb, k), getattr(l1.rb, k)), (name, k)
