@@ -126,3 +126,20 @@ def test_roofline_fractions_stay_below_one():
     found = dict(fracs(rl))
     assert "frac_read_plus_write" not in found and "frac_measured" in found
     assert all(0.0 < v <= 1.0 for v in found.values()), found
+
+
+@pytest.mark.parametrize("kern", ["drl_refill_list_kernel", "drl_refill_kernel"])
+def test_refill_traffic_from_either_refill_form(kern):
+    """The refill's PMC bytes enter `with_refill` whichever form ran: the
+    worklist kernel (the default since round 3) or the wave-per-env kernel
+    (DRL_REFILL_LIST=0); the child's grid sizes tell their rows apart."""
+    E, R, Wb = 65536, 296, 1504
+    refill = {"every": 32, "per_step_us": 1.45}
+    traffic = {"drl_step_kernel": {"bytes_per_launch": 118e6, "read_bytes_per_launch": 35e6,
+                                   "write_bytes_per_launch": 83e6},
+               kern: {"bytes_per_launch": 180e6, "read_bytes_per_env": 1267.0, "write_bytes_per_env": 1481.0},
+               "source": "test", "envs": E}
+    wr = bench.roofline(E, R, Wb, 20.0e-6, refill, traffic)["with_refill"]
+    assert wr["refill_traffic_per_launch"] == 180e6
+    assert wr["traffic_per_step"] == pytest.approx(118e6 + 180e6 / 32)
+    assert set(bench.PMC_KERNELS) >= {"drl_step_kernel", "drl_refill_list_kernel", "drl_refill_kernel"}
