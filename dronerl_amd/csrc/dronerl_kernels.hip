@@ -21,6 +21,9 @@
 //      batched Fisher-Yates shuffles (64 draws per step) over an LDS list.
 //  drl_reset_kernel    one lane per env (the A/B alternative): the shuffle
 //      list lives in LDS, MT twists are done cooperatively by the whole wave.
+//  drl_refill_list_kernel  the respawn-candidate rings: per 32 envs, the ones
+//      whose stream reached the ring's last block get a wave that converts
+//      the next MT block in registers (drl_refill_kernel: one wave per env).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
