@@ -11,8 +11,16 @@ window train_jax.py:55-56 feeds the DQN).  Actions are synthetic uniform
 {0..4}, generated before the timed region and resident in HBM.
 
 Launch:  python bench.py [--gpus 1] [--steps 500] [--warmup 50]
+         python bench.py --gpus N          (starts its own N ranks, below)
          python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 Prints one JSON line on rank 0.
+
+`--gpus N > 1` without a torch.distributed.run environment (no WORLD_SIZE):
+this process becomes a launcher.  Before touching the GPU it runs
+`torch.distributed.run --nproc-per-node N` as a child process (never an
+exec), one rank per GPU over RCCL (train_jax.py:196-212: envs sharded over
+the devices, num_envs % devices == 0, :399-402), relays rank 0's JSON line
+and exits with the job's return code.
 """
 from __future__ import annotations
 
@@ -69,6 +77,58 @@ def dist_init():
     else:
         torch.cuda.set_device(local)
     return rank, world, local
+
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launcher_command(argv, n: int, port: int):
+    """The child command of `bench.py --gpus N` (N > 1, no WORLD_SIZE): N ranks
+    of this script under torch.distributed.run on one node, rendezvous on
+    127.0.0.1, the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def needs_launch(args) -> bool:
+    return args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.pmc_child
+
+
+def launch_ranks(argv, n: int) -> int:
+    """Run the N-rank job as a child process (this process never initialises
+    the GPU: argument parsing only), forward its output, print rank 0's JSON
+    line (the only line starting with '{"metric"') last on stdout, and return
+    the job's exit code: torch.distributed.run fails when any rank fails; a
+    clean job without a JSON line is an error too."""
+    import subprocess
+    if DIST_BACKEND == "nccl" and torch.cuda.device_count() < n:  # (device_count does not initialise HIP)
+        print(f"bench.py --gpus {n}: only {torch.cuda.device_count()} GPU(s) visible; nccl needs one GPU per rank "
+              "(DRL_DIST_BACKEND=gloo shares devices)", file=sys.stderr)
+        return 2
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    cmd = launcher_command(argv, n, free_port())
+    print("bench.py launcher: " + " ".join(cmd[1:]), file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env, cwd=REPO)
+    lines = []
+    for ln in p.stdout:
+        if ln.startswith('{"metric"'):
+            lines.append(ln.strip())
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    rc = p.wait()
+    if rc == 0 and len(lines) != 1:
+        print(f"bench.py launcher: expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr)
+        rc = 1
+    for ln in lines:
+        print(ln, flush=True)
+    return rc
 
 
 def barrier(world):
@@ -333,8 +393,9 @@ def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream,
     ev[3].record(stream)
     torch.cuda.synchronize()
     env.check_errors()
+    lnet.check_errors()  # the f32 acts flag operands outside fp16's split range only through the net
     # the f32 act from the policy code of the same state
-    act_code = None
+    act_code = act_code_rl = None
     W = env.layout.obs_window
     if W in (5, 7, 9):
         cnet = lnet if input == "code" else QNetwork(D, (128, 64), device=env.device,
@@ -352,6 +413,7 @@ def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream,
         torch.cuda.synchronize()
         act_code = c0.elapsed_time(c1) / 1e3 / steps
         cnet.check_errors()
+        act_code_rl = act_code_roofline(E, W, act_code)
     # the act in the other precision
     other = "bf16" if precision == "f32" else "f32"
     net32 = QNetwork(D, (128, 64), device=env.device, generator=torch.Generator().manual_seed(0), precision=other)
@@ -378,6 +440,7 @@ def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream,
             "act_bf16_note": "precision='bf16': bf16 MFMA operands, f32 accumulate (a labelled extra; narrower than "
                              "the reference)",
             "act_code_f32_us": None if act_code is None else act_code * 1e6,
+            "act_code_roofline": act_code_rl,
             "act_code_note": "f32 act from drone 0's policy code (drl_qnet_act_code; the step writes it beside the "
                              "observation): inputs exact in fp16, 2 MFMAs per layer-0 product tile, Q to 1e-5 of "
                              "the f32 forward",
@@ -386,6 +449,46 @@ def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream,
                      "code_t+1, done) of code rows (sample() decodes), capacity 10000") if input == "code" else
                     (f"act(obs_t, {precision}) -> step + obs(K=1) -> replay add_many(obs_t, a, r, obs_t+1, done), "
                      "capacity 10000")}
+
+
+MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense f16/bf16 MFMA (MI355X_MICROARCH.md; the 16x16x32 f16 form: 16 cycles)
+
+
+def act_code_flops(E: int, W: int, hidden=(128, 64), n_actions: int = 5):
+    """FLOPs of one drl_qnet_act_code launch over E envs (W x W window, 6
+    channels per cell; jax dqn.py:47-63's dense net).  Returns (executed,
+    algorithmic): executed = the v_mfma_f32_16x16x32_f16 instructions the
+    kernel issues (2*16*16*32 FLOPs each) per 16-env tile -- layer 0: its
+    K-slices (6 slots per cell of each lane group's ceil(W*W/4) cells + the
+    bias slot, 8 per slice, even count) x (h0/16) unit tiles x 2 (hi and lo
+    weights; the inputs are exact in fp16); each later layer: (h_prev/32)
+    K-slices x (h/16) tiles x 3 (hi*hi, hi*lo, lo*hi of the f32 split);
+    algorithmic = the f32 net's 2 * E * sum(in*out)."""
+    cpg = (W * W + 3) // 4
+    kp0 = -(-(6 * cpg + 1) // 8)
+    kp0 += kp0 % 2
+    sizes = [W * W * 6, *hidden, n_actions]
+    per_tile = kp0 * (hidden[0] // 16) * 2
+    for i in range(1, len(sizes) - 1):
+        per_tile += (sizes[i] // 32) * (-(-sizes[i + 1] // 16)) * 3
+    tiles = -(-E // 16)
+    executed = tiles * per_tile * 2 * 16 * 16 * 32
+    algorithmic = 2 * E * sum(sizes[i] * sizes[i + 1] for i in range(len(sizes) - 1))
+    return executed, algorithmic, per_tile
+
+
+def act_code_roofline(E: int, W: int, launch_s: float):
+    """SURVEY.md §8 F1's separate roofline for the MFMA consumer: the code act
+    is matrix work (bound "mfma"): executed MFMA FLOPs per launch / its average
+    launch duration (HIP events) against the dense f16 MFMA peak."""
+    ex, alg, per_tile = act_code_flops(E, W)
+    achieved = ex / launch_s / 1e12
+    return {"bound": "mfma", "achieved": achieved, "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / MFMA_PEAK_TFLOPS, "mfma_flops_per_launch": ex, "mfma_per_16env_tile": per_tile,
+            "algorithmic_f32_flops_per_launch": alg, "avg_launch_us": launch_s * 1e6,
+            "note": "executed v_mfma_f32_16x16x32_f16 FLOPs (f32 numerics as fp16 hi/lo pieces: 2 MFMAs per layer-0 "
+                    "product tile, 3 per later-layer tile) / average launch (HIP events); "
+                    "algorithmic_f32_flops_per_launch is the plain f32 net's 2*E*sum(in*out)"}
 
 
 def rollout_bench(env, actions, K, warmup_steps, steps, chunk: int, R: int, Wb: int, world: int):
@@ -536,40 +639,43 @@ class TrainSegment:
             every = self.env.refill_every
             self.env.refill_every = 0  # (the refills below, on their own branch)
             since = self.env._since_refill
-            self.s_syn.wait_stream(main)
-            self.s_rep.wait_stream(main)
-            for t in range(self.seg):
-                if not self.fused:
-                    with torch.cuda.stream(self.s_syn):
-                        if t >= self.NB:  # acts[t % 3] was last read by the replay add of step t-3
-                            self.s_syn.wait_event(ev_rep[t - self.NB])
-                        self._synth(t)
-                        ev_syn[t].record(self.s_syn)
-                    main.wait_event(ev_syn[t])
-                elif t >= self.NB:  # the act writes acts[t % 3], read by the replay add of step t-3
-                    main.wait_event(ev_rep[t - self.NB])
-                if t >= 2:  # step t overwrites obs[(t+1) % 3], read by the replay add of step t-2
-                    main.wait_event(ev_rep[t - 2])
-                self._act_step(t, before_step=(lambda e=ev_ref: main.wait_event(e)) if ev_ref is not None else None)
-                ev_ref = None
-                ev_step[t].record(main)
-                since += 1
-                if every > 0 and since >= every:
-                    since = 0
-                    with torch.cuda.stream(self.s_ref):
-                        self.s_ref.wait_event(ev_step[t])
-                        self.env.refill()
-                        ev_ref = torch.cuda.Event()
-                        ev_ref.record(self.s_ref)
-                with torch.cuda.stream(self.s_rep):
-                    self.s_rep.wait_event(ev_step[t])
-                    self._replay(t)
-                    ev_rep[t].record(self.s_rep)
-            main.wait_stream(self.s_syn)
-            main.wait_stream(self.s_rep)
-            main.wait_stream(self.s_ref)
-            self.env.refill_every = every
-            self.env._since_refill = since
+            try:  # (a capture that raises must not leave the env with refills off: ADVICE r3)
+                self.s_syn.wait_stream(main)
+                self.s_rep.wait_stream(main)
+                for t in range(self.seg):
+                    if not self.fused:
+                        with torch.cuda.stream(self.s_syn):
+                            if t >= self.NB:  # acts[t % 3] was last read by the replay add of step t-3
+                                self.s_syn.wait_event(ev_rep[t - self.NB])
+                            self._synth(t)
+                            ev_syn[t].record(self.s_syn)
+                        main.wait_event(ev_syn[t])
+                    elif t >= self.NB:  # the act writes acts[t % 3], read by the replay add of step t-3
+                        main.wait_event(ev_rep[t - self.NB])
+                    if t >= 2:  # step t overwrites obs[(t+1) % 3], read by the replay add of step t-2
+                        main.wait_event(ev_rep[t - 2])
+                    join = (lambda e=ev_ref: main.wait_event(e)) if ev_ref is not None else None
+                    self._act_step(t, before_step=join)
+                    ev_ref = None
+                    ev_step[t].record(main)
+                    since += 1
+                    if every > 0 and since >= every:
+                        since = 0
+                        with torch.cuda.stream(self.s_ref):
+                            self.s_ref.wait_event(ev_step[t])
+                            self.env.refill()
+                            ev_ref = torch.cuda.Event()
+                            ev_ref.record(self.s_ref)
+                    with torch.cuda.stream(self.s_rep):
+                        self.s_rep.wait_event(ev_step[t])
+                        self._replay(t)
+                        ev_rep[t].record(self.s_rep)
+                main.wait_stream(self.s_syn)
+                main.wait_stream(self.s_rep)
+                main.wait_stream(self.s_ref)
+            finally:
+                self.env.refill_every = every
+                self.env._since_refill = since
         self.env.reset(seed=None)
         self._first_obs()
 
@@ -600,6 +706,7 @@ def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fus
     e1.record()
     torch.cuda.synchronize(dev)
     env.check_errors()
+    loop.net.check_errors()  # (an f32 act's range flag lives in the net)
     dt = e0.elapsed_time(e1) / 1e3
     E = env.num_envs
     branches = (("replay add_many" if fused else "synthetic actions and replay add_many") +
@@ -751,23 +858,58 @@ class StepRunner:
                                    "step count"}}
 
 
-def roofline(E, R, Wb, launch_s, refill, traffic):
+def measure_copy_peak(dev, nbytes: int = 2 << 30, reps: int = 6):
+    """the measured copy-kernel rate beside the 8 TB/s spec
+    (MI355X_MICROARCH.md: 6.29 TB/s for a float4 copy).  Two 2-GiB buffers
+    (past the 256-MiB Infinity Cache), `copy_` timed with HIP events; GB/s of
+    bytes read + written.  Also a read-only rate (`sum`)."""
+    n = nbytes // 4
+    a = torch.ones(n, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    out = {}
+    for name, fn, mult in (("copy", lambda: b.copy_(a), 2), ("read", lambda: a.sum(), 1)):
+        fn()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        out[name] = mult * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return {"copy_GBs": out["copy"], "read_GBs": out["read"],
+            "note": f"in-run probe: torch copy_ of {nbytes >> 20} MiB (read + write bytes) and sum (read) on this GPU"}
+
+
+def roofline(E, R, Wb, launch_s, refill, traffic, G=None, peak_measured=None):
     """SURVEY.md §8 D3 roofline of the dominant kernel (drl_step_kernel):
     achieved = E * R (algorithmic read bytes per env-step) / its average
     launch duration (HIP events on the launch stream).  `traffic` = measured
     HBM bytes per launch (PMC); frac_measured = traffic / launch / peak, the
-    fraction of the HBM peak the kernel actually moves (<= 1 by construction,
-    unlike a read+write figure whose W counts a full ground write-back the
-    kernel never does).  with_refill adds the refill share per step."""
+    fraction of the HBM peak the kernel actually moves (<= 1 by construction).
+    frac_ceiling = R / (R + W - G^2): the frac of a kernel that reads R and
+    writes only the outputs every step must write (observation, rewards,
+    dones, records), no ground write-back (the survey's W counts all G^2
+    ground bytes; a step writes only the changed cells), at the spec peak --
+    a true upper bound of frac.  peak_measured: the in-run copy probe
+    (frac_vs_measured_peak = achieved / its rate).  with_refill adds the
+    refill share per step."""
     achieved = E * R / launch_s / 1e9
+    ceiling = R / (R + Wb - (G * G if G else 0))
     out = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
            "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": "drl_step_kernel",
            "avg_launch_us": launch_s * 1e6, "algorithmic_read_bytes_per_env_step": R,
-           "algorithmic_write_bytes_per_env_step": Wb, "frac_ceiling_read_only": R / (R + Wb),
-           "note": "frac counts SURVEY.md §8 D3's read bytes R only (achieved = E*R / avg drl_step launch); moving "
-                   "all R + W algorithmic bytes at the HBM peak would score frac_ceiling_read_only = R/(R+W). "
-                   "traffic = measured HBM bytes per drl_step launch (2*FETCH_SIZE + WRITE_SIZE), "
-                   "frac_measured = traffic / avg launch / peak"}
+           "algorithmic_write_bytes_per_env_step": Wb, "frac_ceiling": ceiling,
+           "note": "frac counts SURVEY.md §8 D3's read bytes R only (achieved = E*R / avg drl_step launch); "
+                   "frac_ceiling = R/(R + W - G^2) bounds it (the obligatory outputs moved at the spec peak, no "
+                   "ground write-back). traffic = measured HBM bytes per drl_step launch (2*FETCH_SIZE + "
+                   "WRITE_SIZE), frac_measured = traffic / avg launch / peak"}
+    if peak_measured:
+        out["peak_measured"] = peak_measured["copy_GBs"]
+        out["frac_vs_measured_peak"] = achieved / peak_measured["copy_GBs"]
+        out["peak_measured_detail"] = peak_measured
     per_step_s = launch_s + refill["per_step_us"] / 1e6
     out["with_refill"] = {"us_per_step": per_step_s * 1e6, "achieved": E * R / per_step_s / 1e9,
                           "frac": E * R / per_step_s / 1e9 / PEAK_HBM_GBS}
@@ -775,6 +917,8 @@ def roofline(E, R, Wb, launch_s, refill, traffic):
         st = traffic["drl_step_kernel"]
         out["traffic"] = st["bytes_per_launch"]
         out["frac_measured"] = st["bytes_per_launch"] / launch_s / 1e9 / PEAK_HBM_GBS
+        if peak_measured:
+            out["frac_measured_vs_measured_peak"] = st["bytes_per_launch"] / launch_s / 1e9 / peak_measured["copy_GBs"]
         out["traffic_detail"] = dict(st, source=traffic.get("source"), envs=traffic.get("envs"))
         rf = traffic.get("drl_refill_list_kernel") or traffic.get("drl_refill_kernel")
         if rf and refill["every"] > 0:
@@ -865,6 +1009,8 @@ def main():
     args = ap.parse_args()
     if args.pmc_child:
         return pmc_child(args)
+    if needs_launch(args):  # N ranks as a child job, before this process touches the GPU
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
 
     north = args.c5_envs > 0 and args.config != "c5"
     names = [args.config] + (["c5"] if north else [])
@@ -915,6 +1061,8 @@ def main():
                          "way; `value` uses env.step()'s default (cached stores at 8 lanes per env, streaming at "
                          ">= 16: the faster one in the train loop, profiles/r02_store_mode/)"}
 
+    copy_peak = measure_copy_peak(dev)
+
     # resets (train_jax.py:101-113 resets every 100 steps in C5): timed separately
     resets_per_s = None
     if not args.no_reset_bench:
@@ -949,7 +1097,9 @@ def main():
         loop = train_loop_bench(env, args.loop_segments, parallel=args.parallel_loop, fused=not args.unfused_act,
                                 precision=args.loop_precision, input=loop_input(args, env))
         loop["env_steps_per_s"] = min_over_ranks(loop["env_steps_per_s"], world) * world
+        loop["us_per_step"] = max_over_ranks(loop["us_per_step"], world)
         loop["n_gpus"] = world
+        loop["num_envs_total"] = E * world
     del runner, actions, rewards, dones, obs, env
 
     # ---- the north-star configuration (BASELINE.json north_star, SURVEY.md
@@ -971,11 +1121,24 @@ def main():
                                      f"step + fused obs(K={K5})", "num_envs_per_gpu": E5,
                          "num_envs_total": E5 * world, "obs_stores": "streaming" if st5 else "cached",
                          "parallelism": f"env-shard x{world}"},
-              "roofline": roofline(E5, R5, W5, r5["launch_s"], r5["refill"], traffic_of("c5")),
+              "roofline": roofline(E5, R5, W5, r5["launch_s"], r5["refill"], traffic_of("c5"), G5, copy_peak),
               "refill": r5["refill"],
+              "train_loop": None,
               "north_star": "BASELINE.json: >= 1e8 env-steps/s at num_envs=2^20 on 8 GPUs at >= 40% HBM-read "
                             "roofline (roofline.frac)"}
-        del run5, env5
+        del run5
+        # BASELINE.json configs[4]: "full scan-style train loop" at the C5 shape
+        # (train_jax.py:38-115, :215-236), the same graph-captured 100-step
+        # segments + reset as `train_loop`, c5_envs per rank
+        if args.loop_segments > 0 and not args.no_dqn and K5 >= 1:
+            l5 = train_loop_bench(env5, args.loop_segments, parallel=args.parallel_loop, fused=not args.unfused_act,
+                                  precision=args.loop_precision, input=loop_input(args, env5))
+            l5["env_steps_per_s"] = min_over_ranks(l5["env_steps_per_s"], world) * world
+            l5["us_per_step"] = max_over_ranks(l5["us_per_step"], world)
+            l5["n_gpus"] = world
+            l5["num_envs_total"] = E5 * world
+            c5["train_loop"] = l5
+        del env5
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -1005,7 +1168,8 @@ def main():
                        "setup": f"reset(seed=0), then {PRE_ROLL_CYCLES * main_res['refill']['every']} pre-roll steps "
                                 f"({PRE_ROLL_CYCLES} refill cycles: steady-state candidate rings) before the warm-up"},
             "wall_ms_per_step": main_res["wall_ms_per_step"],
-            "roofline": roofline(E, R, Wb, main_res["launch_s"], main_res["refill"], traffic_of(args.config)),
+            "roofline": roofline(E, R, Wb, main_res["launch_s"], main_res["refill"], traffic_of(args.config), G,
+                                 copy_peak),
             "refill": main_res["refill"],
             ("cached_obs" if args.obs_stream else "streaming_obs"): other,
             "c5": c5,

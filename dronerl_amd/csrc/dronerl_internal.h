@@ -227,6 +227,7 @@ struct QnetLayout {
     int bias_vec;                 // uint4 offset of the biases
     int lo0_lds;                  // F32: layer 0's hi and lo fragments are the LDS image (the rest is global)
     int code_w;                   // > 0: DRL_QNET_INPUT_CODE net of a code_w x code_w window
+    int status_vec;               // uint4 offset of the pack status vector (the last one)
 };
 
 struct QnetPack {
@@ -242,6 +243,7 @@ struct QnetPack {
     int frag_lo_off[QN_MAX_LAYERS];  // F32: lo fragments, uint4 offsets from packed_w
     int frag_src[QN_MAX_LAYERS];     // contiguous numbering of the hi elements (uint4 units) -> frag_off
     int code_w;                      // > 0: layer 0 in the policy code's K order for a code_w x code_w window
+    int32_t* status;                 // the packed net's status word (DRL_ERR_QNET_RANGE: a weight outside fp16's range)
 };
 
 struct QnetArgs {
@@ -264,6 +266,7 @@ struct QnetArgs {
     uint64_t synth_seed, synth_step;
     int32_t* err;                   // F32: DRL_ERR_QNET_RANGE when an operand leaves fp16's range (nullable)
     int total_bytes;                // bytes of the packed net (code act: buffer loads of the later layers)
+    int status_vec;                 // uint4 offset of the pack status vector (drl_qnet_pack's range flag)
 };
 
 struct ReplayArgs {

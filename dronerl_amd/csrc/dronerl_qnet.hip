@@ -74,6 +74,7 @@ __global__ void drl_qnet_pack_kernel(QnetPack p) {
         // the integer charge (exact in fp16), so no input needs an x_lo product
         if (l == 0 && p.code_w > 0 && k >= 0 && k < p.in[l] && k % 6 == 4) w /= 100.0f;
         if (p.precision == DRL_QNET_F32) {  // hi = fp16(w), lo = fp16((w - hi) * 2^11), lo after the LDS image
+            if (!(__builtin_fabsf(w) < 65504.0f)) atomicOr(p.status, DRL_ERR_QNET_RANGE);  // 
             const _Float16 hi = (_Float16)w;
             reinterpret_cast<_Float16*>(p.packed_w)[(int64_t)p.frag_off[l] * 8 + e] = hi;
             reinterpret_cast<_Float16*>(p.packed_w)[(int64_t)p.frag_lo_off[l] * 8 + e] =
@@ -328,6 +329,10 @@ __device__ __forceinline__ f16x8 as_f16x8(const uint4 v) {
 // `bad` collects operands outside fp16's range (|v| >= 65520 rounds hi to
 // inf; NaN stays NaN): the split would turn them into NaN Q values, so the
 // kernel flags DRL_ERR_QNET_RANGE instead of failing silently.
+// Weights (and a code net's layer-0 bias) are range-checked when packed (the
+// pack status word, read at the end of every f32 act).  With finite fp16
+// operands below 65520 and K <= 512, an f32 pre-activation is finite, so the
+// ReLU's fmaxf never sees a NaN that these two checks did not flag.
 __device__ __forceinline__ void split_f16(const float (&v)[8], f16x8& hi, f16x8& lo, bool& bad) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -531,6 +536,7 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_f32_kernel(QnetArg
             }
         }
     }
+    bad |= lane == 0 && reinterpret_cast<const int32_t*>(a.packed + a.status_vec)[0] != 0;  // pack range flag
     if (__ballot(bad) && lane == 0 && a.err) atomicOr(a.err, DRL_ERR_QNET_RANGE);
     if (a.synth_n > 1) {  // as in drl_qnet_act_kernel
         const uint32_t nd = (uint32_t)a.synth_n - 1u;
@@ -899,6 +905,7 @@ __global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(Qn
         }
 #endif
     }
+    bad |= lane == 0 && reinterpret_cast<const int32_t*>(a.packed + a.status_vec)[0] != 0;  // pack range flag
     if (__ballot(bad) && lane == 0 && a.err) atomicOr(a.err, DRL_ERR_QNET_RANGE);
     if (a.synth_n > 1) {  // as in drl_qnet_act_kernel (one 16-env tile per group)
         const uint32_t nd = (uint32_t)a.synth_n - 1u;
@@ -1140,6 +1147,7 @@ __global__ void __launch_bounds__(64 * QN_CODE2_WAVES) drl_qnet_act_code2_kernel
             }
         }
     }
+    bad |= lane == 0 && reinterpret_cast<const int32_t*>(a.packed + a.status_vec)[0] != 0;  // pack range flag
     if (__ballot(bad) && lane == 0 && a.err) atomicOr(a.err, DRL_ERR_QNET_RANGE);
     if (a.synth_n > 1) {  // as in drl_qnet_act_kernel (TP 16-env tiles per group)
         const uint32_t nd = (uint32_t)a.synth_n - 1u;

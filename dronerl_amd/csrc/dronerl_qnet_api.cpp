@@ -100,6 +100,12 @@ int qnet_layout(const drl_qnet_desc* d, drl::QnetLayout* L) {
     } else {
         L->total_vec = L->lds_vec;
     }
+    // a 16-B status vector ends the packed net: drl_qnet_pack ORs
+    // DRL_ERR_QNET_RANGE into its first word when a weight (or a code net's
+    // layer-0 bias, packed as a weight) is outside fp16's split range or not
+    // finite, and the f32 act kernels report it through their err word
+    L->status_vec = L->total_vec;
+    L->total_vec += 1;
     if (L->lds_vec * 16 > kQnetLdsMax) return fail("the packed network does not fit the 160 KB LDS of a CU");
     return 0;
 }
@@ -158,6 +164,9 @@ int drl_qnet_pack(const drl_qnet_desc* d, const float* const* d_weights, const f
     }
     p.precision = L.precision;
     p.code_w = L.code_w;
+    p.status = reinterpret_cast<int32_t*>(static_cast<uint8_t*>(d_packed) + (size_t)L.status_vec * 16);
+    if (hipError_t e0 = hipMemsetAsync(p.status, 0, 16, stream); e0 != hipSuccess)
+        return hip_fail(e0, "drl_qnet_pack status reset");
     for (int l = 0; l < L.n_layers; ++l) p.frag_lo_off[l] = L.frag_lo_off[l];
     p.n_wfrag_elems = (int64_t)L.frag_total * 8;
     p.n_bias = L.n_bias;
@@ -200,6 +209,7 @@ static int qnet_act_impl(const drl_qnet_desc* d, const void* d_packed, const flo
     a.lo0_lds = L.lo0_lds;
     a.lds_vec = L.lds_vec;
     a.n_bias = L.n_bias;
+    a.status_vec = L.status_vec;
     a.packed = static_cast<const uint4*>(d_packed);
     a.obs = d_obs;
     a.obs_stride = obs_stride;
@@ -248,6 +258,7 @@ int drl_qnet_act_code(const drl_qnet_desc* d, const void* d_packed, const void* 
     if ((uintptr_t)d_packed % 16 || (uintptr_t)d_code % 16) return fail("packed and code must be 16-byte aligned");
     if (action_stride < 1) return fail("action_stride must be >= 1");
     if (synth_n > 1 && action_stride < synth_n) return fail("action_stride must be >= synth_n");
+    if (synth_n > DRL_MAX_DRONES) return fail("synth_n must be <= DRL_MAX_DRONES (64)");
     drl::QnetArgs a;
     memset(&a, 0, sizeof a);
     a.in_features = d->in_features;
@@ -266,6 +277,7 @@ int drl_qnet_act_code(const drl_qnet_desc* d, const void* d_packed, const void* 
     a.lo0_lds = L.lo0_lds;
     a.lds_vec = L.lds_vec;
     a.n_bias = L.n_bias;
+    a.status_vec = L.status_vec;
     a.packed = static_cast<const uint4*>(d_packed);
     a.obs = static_cast<const float*>(d_code);
     a.E = num_envs;

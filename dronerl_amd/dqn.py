@@ -7,8 +7,8 @@ transition of drone 0 goes to the replay buffer), jax_impl/buffers.py:18-93.
 `QNetwork` holds fp32 parameters (torch nn.Linear layout [out][in]; a flax
 Dense kernel is the transpose) and packs them for the MFMA kernel
 (drl_qnet_pack) whenever they change; `act` runs the forward + epsilon-greedy
-choice for every env in one launch (drl_qnet_act, bf16 operands with f32
-accumulation).  `ReplayBuffer.add_many` is drl_replay_add; `sample` is plain
+choice for every env in one launch (drl_qnet_act; f32 numerics by default,
+bf16 operands as an opt-in).  `ReplayBuffer.add_many` is drl_replay_add; `sample` is plain
 torch indexing (64 rows).
 """
 from __future__ import annotations
@@ -84,10 +84,11 @@ def _stream(device):
 class QNetwork:
     """Dense Q-network: in_features -> hidden... (ReLU) -> n_actions.
 
-    precision "bf16": bf16 MFMA operands, f32 accumulation (Q to ~1e-2
-    relative).  "f32": the reference's f32 nets (jax dqn.py:47-63, torch
-    dqn.py:44-82): split fp16 hi/lo operands, three MFMAs per product tile,
-    Q to f32 rounding (include/dronerl.h DRL_QNET_F32).
+    precision "f32" (the default): the reference's f32 nets (jax
+    dqn.py:47-63, torch dqn.py:44-82): split fp16 hi/lo operands, three MFMAs
+    per product tile, Q to f32 rounding (include/dronerl.h DRL_QNET_F32).
+    "bf16" (opt-in, narrower than the reference): bf16 MFMA operands, f32
+    accumulation (Q to ~1e-2 relative; near-ties may pick another action).
 
     input "obs": `act` reads the f32 observation rows.  "code" (f32 only, a
     5x5, 7x7 or 9x9 window): `act` reads drone 0's policy code, which
@@ -96,7 +97,7 @@ class QNetwork:
     parameters and Q values are the same (drl_qnet_act_code)."""
 
     def __init__(self, in_features: int, hidden: Sequence[int] = (32, 32), n_actions: int = NUM_ACTIONS,
-                 device=None, generator: Optional[torch.Generator] = None, precision: str = "bf16",
+                 device=None, generator: Optional[torch.Generator] = None, precision: str = "f32",
                  input: str = "obs"):
         if precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
@@ -145,9 +146,10 @@ class QNetwork:
 
     def pack(self):
         if self.precision == "f32":  # fp16 hi/lo split range (include/dronerl.h DRL_QNET_F32)
-            for w, b in zip(self.weights, self.biases):
-                if not bool(torch.isfinite(w).all()) or float(w.abs().max()) >= 65504.0:
-                    raise ValueError("f32 precision needs finite weights with |w| < 65504")
+            for w, b in zip(self.weights, self.biases):  # (a code net splits layer 0's bias too: ADVICE r3)
+                for t in (w, b):
+                    if not bool(torch.isfinite(t).all()) or float(t.abs().max()) >= 65504.0:
+                        raise ValueError("f32 precision needs finite weights and biases with |w| < 65504")
         n = len(self.weights)
         wp = (_vp * n)(*[w.data_ptr() for w in self.weights])
         bp = (_vp * n)(*[b.data_ptr() for b in self.biases])

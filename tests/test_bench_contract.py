@@ -143,3 +143,66 @@ def test_refill_traffic_from_either_refill_form(kern):
     assert wr["refill_traffic_per_launch"] == 180e6
     assert wr["traffic_per_step"] == pytest.approx(118e6 + 180e6 / 32)
     assert set(bench.PMC_KERNELS) >= {"drl_step_kernel", "drl_refill_list_kernel", "drl_refill_kernel"}
+
+
+@pytest.mark.parametrize("cfg,launch_us", [("c3", 19.83), ("c3", 14.0), ("c4", 28.0), ("c5", 143.6), ("c5", 110.0)])
+def test_no_ceiling_below_its_frac(cfg, launch_us):
+    """every `*ceiling*` field bounds its frac (the r3
+    `frac_ceiling_read_only` was exceeded at C5: its W counted a G^2 ground
+    write-back no step does).  frac_ceiling = R / (R + W - G^2) holds for any
+    launch that moves at least the obligatory bytes at or below the spec peak."""
+    G, N, E, K = bench.CONFIGS[cfg]
+    R, Wb = bench.algorithmic_bytes(G, N, K)
+    refill = {"every": 32, "per_step_us": 2.0}
+    peak = {"copy_GBs": 6290.0, "read_GBs": 5900.0, "note": "test"}
+    rl = bench.roofline(E, R, Wb, launch_us * 1e-6, refill, None, G, peak)
+    assert rl["frac"] <= rl["frac_ceiling"] <= 1.0
+    # the bound itself: obligatory bytes E * (R + W - G^2) at the spec peak take at least this long
+    t_min = E * (R + Wb - G * G) / (bench.PEAK_HBM_GBS * 1e9)
+    if launch_us * 1e-6 >= t_min:
+        assert rl["frac"] <= rl["frac_ceiling"]
+    assert rl["frac_vs_measured_peak"] == pytest.approx(rl["achieved"] / 6290.0)
+    ceilings = {k: v for k, v in rl.items() if "ceiling" in k}
+    assert ceilings and all(v >= rl["frac"] for v in ceilings.values())
+
+
+def test_act_code_flops_count():
+    """the code act's MFMA count per 16-env tile (layer 0:
+    10 K-slices x 8 unit tiles x 2; layer 1: 4 x 4 x 3; output: 2 x 1 x 3)."""
+    ex, alg, per_tile = bench.act_code_flops(65536, 7)
+    assert per_tile == 10 * 8 * 2 + 4 * 4 * 3 + 2 * 1 * 3 == 214
+    assert ex == 4096 * 214 * 2 * 16 * 16 * 32
+    assert alg == 2 * 65536 * (294 * 128 + 128 * 64 + 64 * 5)
+    rl = bench.act_code_roofline(65536, 7, 21.75e-6)
+    assert rl["bound"] == "mfma" and rl["unit"] == "TFLOP/s"
+    assert rl["frac"] == pytest.approx(ex / 21.75e-6 / 1e12 / bench.MFMA_PEAK_TFLOPS)
+
+
+def test_launcher_plumbing(monkeypatch):
+    """`bench.py --gpus N` with no torch.distributed.run
+    environment starts its own N ranks as a child job (never an exec, before
+    any GPU call) with the same arguments; under torchrun (WORLD_SIZE set),
+    or for one GPU, or in a PMC child, it runs in-process."""
+    import argparse
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    ns = lambda gpus, pmc="": argparse.Namespace(gpus=gpus, pmc_child=pmc)  # noqa: E731
+    assert bench.needs_launch(ns(8)) and bench.needs_launch(ns(2))
+    assert not bench.needs_launch(ns(1)) and not bench.needs_launch(ns(8, "c3"))
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    assert not bench.needs_launch(ns(8))
+    argv = ["--gpus", "8", "--steps", "20", "--warmup", "5"]
+    cmd = bench.launcher_command(argv, 8, 29517)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd and "--master-port=29517" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-len(argv) - 1] == os.path.join(REPO, "bench.py") and cmd[-len(argv):] == argv
+    assert 1024 <= bench.free_port() < 65536
+
+
+def test_launcher_refuses_more_nccl_ranks_than_gpus(monkeypatch, capsys):
+    """No GPU here: nccl (RCCL) needs one device per rank, so the launcher
+    refuses before starting anything (exit 2); gloo may share devices."""
+    monkeypatch.setattr(bench, "DIST_BACKEND", "nccl")
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 0)
+    assert bench.launch_ranks(["--gpus", "2"], 2) == 2
+    assert "one GPU per rank" in capsys.readouterr().err

@@ -1,8 +1,8 @@
 """DQN consumer: Q-network act on MFMA + replay add_many.
 
 Reference: jax_impl/agents/dqn.py:47-63,132-146; jax_impl/buffers.py:57-93;
-train_jax.py:42-64.  Numerics: the kernel uses bf16 operands with f32
-accumulation, so Q is checked against a torch fp32 forward with the same
+train_jax.py:42-64.  Numerics (precision="bf16", the opt-in): the kernel uses
+bf16 operands with f32 accumulation, so Q is checked against a torch fp32 forward with the same
 bf16 rounding of weights/inputs/activations (tolerance below) and, looser,
 against the plain fp32 forward; greedy actions must match wherever the
 reference's top-two margin exceeds the tolerance.  The exploration draws come
@@ -49,17 +49,18 @@ def test_qnet_packed_size_formula():
     assert L.drl_qnet_packed_bytes(ctypes.byref(_desc(294, (128, 64))), ctypes.byref(nb)) == 0
     frags = 8 * 10 + 4 * 4 + 1 * 2          # (16-row tiles x 32-wide K-slices) per layer, 1 KB each
     biases = (128 + 64 + 16) * 4
-    assert nb.value == frags * 1024 + biases
+    status = 16  # drl_qnet_pack's range flag vector ends the packed net
+    assert nb.value == frags * 1024 + biases + status
     # DRL_QNET_F32: fp16 hi fragments, biases, the later layers' lo fragments (the LDS image), then layer 0's lo
     assert L.drl_qnet_packed_bytes(ctypes.byref(_desc(294, (128, 64), precision=1)), ctypes.byref(nb)) == 0
-    assert nb.value == 2 * frags * 1024 + biases
+    assert nb.value == 2 * frags * 1024 + biases + status
     assert L.drl_qnet_packed_bytes(ctypes.byref(_desc(294, (128, 64), precision=2)), ctypes.byref(nb)) != 0
     assert b"precision" in L.drl_last_error()
     # f32 with layer 0's hi + lo fragments alone in LDS (160 KB at 294 -> 128), the later layers in global
     # memory: three 128-wide hidden layers pack (same total bytes, another order)
     assert L.drl_qnet_packed_bytes(ctypes.byref(_desc(294, (128, 128, 128), precision=1)), ctypes.byref(nb)) == 0
     frags3 = 8 * 10 + 8 * 4 + 8 * 4 + 1 * 4
-    assert nb.value == 2 * frags3 * 1024 + (128 * 3 + 16) * 4
+    assert nb.value == 2 * frags3 * 1024 + (128 * 3 + 16) * 4 + status
     # 486 inputs (radius 4) at 128 units: neither layout fits the LDS
     assert L.drl_qnet_packed_bytes(ctypes.byref(_desc(486, (128, 128), precision=1)), ctypes.byref(nb)) != 0
 
@@ -97,7 +98,7 @@ def test_qnet_greedy_matches_torch_reference(hidden, E):
     from dronerl_amd.dqn import QNetwork
     obs, _ = _obs_batch(E)
     g = torch.Generator().manual_seed(len(hidden) * 1000 + E)
-    net = QNetwork(obs.shape[1], hidden, generator=g)
+    net = QNetwork(obs.shape[1], hidden, generator=g, precision="bf16")
     gb = torch.Generator(device="cuda").manual_seed(E + 3)
     for b in net.biases:
         b.normal_(0, 0.1, generator=gb)
@@ -177,10 +178,14 @@ def test_qnet_f32_weight_range_checked():
     w[0][0, 0] = 70000.0
     with pytest.raises(ValueError, match="65504"):
         net.load(w, net.biases)
+    b = [t.clone() for t in net.biases]
+    b[0][3] = float("inf")
+    with pytest.raises(ValueError, match="65504"):
+        net.load(net.weights, b)
 
 
 @gpu
-@pytest.mark.parametrize("where", ["input", "hidden", "nan", "ok"])
+@pytest.mark.parametrize("where", ["input", "hidden", "nan", "packed_weight", "ok"])
 def test_qnet_f32_activation_range_flagged(where):
     """an input or hidden activation beyond fp16's split range
     (|v| >= 65520) would become inf/NaN in the hi/lo split; the kernel flags
@@ -199,6 +204,16 @@ def test_qnet_f32_activation_range_flagged(where):
         w = [t.clone() for t in net.weights]
         w[0][:, :] = 3000.0
         net.load(w, net.biases)
+    elif where == "packed_weight":  # a weight outside the split range packed through the C ABI (no host check)
+        w = [t.clone() for t in net.weights]
+        w[2][1, 0] = 1.0e6
+        net.weights = w
+        from dronerl_amd.dqn import _check, _stream, _vp
+        n = len(w)
+        wp = (_vp * n)(*[t.data_ptr() for t in w])
+        bp = (_vp * n)(*[t.data_ptr() for t in net.biases])
+        _check(net.L, net.L.drl_qnet_pack(ctypes.byref(net.desc), wp, bp, _vp(net.packed.data_ptr()),
+                                          _stream(net.device)))
     net.act(x, epsilon=0.0)
     if where == "ok":
         net.check_errors()

@@ -7,6 +7,8 @@
    positions, charge, carry, all 625 MT words) is compared bit for bit, with
    every env's done count and reward sum.  Size-independent invariants are
    checked over every env as well.
+   The last step runs the headline kernel instance (fused obs(K=1)), and every
+   env's observation is compared with the oracle's.
 2. The C5 scan-style train-loop segment (train_jax.py:38-115, reset every
    100 steps :359): per step, synthetic actions for drones 1..N-1 plus the
    epsilon-greedy DQN action of drone 0 (one drl_qnet_act_synth launch),
@@ -15,6 +17,14 @@
    by the kernel's actions; env state, rewards, dones and the observation are
    compared every step, and the replay ring at the end against the ring the
    oracle's transitions give.
+3. The exact loop bench.py times (`train_loop`): C3 at
+   65,536 envs, f32 nets on drone 0's policy code, a code-row replay buffer,
+   bench.TrainSegment's own calls, 100 steps, then its reset.  The oracle is
+   driven by the kernel's actions; every step compares rewards, dones and the
+   code the step wrote (decoded on the host) with the oracle's observation,
+   the state every 10 steps; the act's Q on the step's code against an f32
+   forward of the oracle's observation; the code ring and sample()'s decoded
+   rows against the oracle's transitions; the reset's state and first code.
 """
 import os
 
@@ -43,13 +53,26 @@ def test_full_size_every_env_matches_oracle(cfg, E, steps):
     rsum = torch.zeros(E, dtype=torch.float64, device=env.device)
     dsum = torch.zeros(E, dtype=torch.int64, device=env.device)
     for t in range(steps):
-        r, dn = env.step(env.synth_actions(seed=77, step=t))
+        # the last step is the headline kernel instance: fused obs(K=1)
+        out = env.step(env.synth_actions(seed=77, step=t), obs_k=1 if t == steps - 1 else 0)
+        r, dn = out[0], out[1]
         rsum += r.double().sum(1)
         dsum += dn.sum(1)
+    obs = out[2]
     torch.cuda.synchronize()
     env.check_errors()
     o = rollout(oparams(p), E, steps, seed0=123, action_seed=77, nthreads=THREADS)
     assert_state(gpu_state(env), o, f"{G}x{G}/{N}, {E} envs x {steps} steps")
+    # every env's observation of drone 0 after the last step, against the oracle's WindowedGridView of its
+    # own final state (wrappers.py:10-31,55-73)
+    om = OracleMulti(oparams(p), E)
+    om.set_state(o["ground"], o["order"], o["y"], o["x"], o["charge"], o["packet"], o["mt"])
+    want = om.obs(3, 1)
+    got = obs.cpu().numpy()
+    if not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+        bad = np.argwhere((got != want).reshape(E, -1).any(1)).ravel()
+        raise AssertionError(f"obs differs in envs {bad[:10]} (of {len(bad)})")
+    del om, want, got
     np.testing.assert_array_equal(dsum.cpu().numpy(), o["done_sum"])
     assert np.abs(rsum.cpu().numpy() - o["reward_sum"]).max() <= steps * N * 1e-6
     # size-independent invariants over every env
@@ -131,3 +154,87 @@ def test_c5_train_loop_segment_matches_oracle(E, seg):
     o.reset(None)
     assert_state(gpu_state(env), o.state(), "C5 loop reset")
     np.testing.assert_array_equal(env.get_obs(1).cpu().numpy(), o.obs(3, 1), err_msg="C5 loop reset obs")
+
+
+def test_c3_code_train_loop_matches_oracle():
+    import bench
+    from tests.test_policy_code import decode_code
+    E, seg, N = 65536, 100, 8
+    p = EnvParams(n_drones=N, grid_size=16)
+    env = Env(p, E)
+    env.reset(seed=5)
+    o = OracleMulti(oparams(p), E)
+    o.reset(5 + np.arange(E))
+    loop = bench.TrainSegment(env, seg, precision="f32", input="code")  # the bench's own loop (one stream, fused)
+    assert loop.input == "code" and loop.net.precision == "f32" and loop.rb.code_radius == 3
+    W = env.layout.obs_window
+    want0 = o.obs(3, 1)[:, 0]
+    assert np.array_equal(decode_code(loop.code[0].cpu().numpy(), W), want0), "first code"
+    cap = loop.rb.capacity
+    t_keep = (seg * E - cap) // E
+    hist, prev = {}, want0
+    for t in range(seg):
+        b, nb = t % loop.NB, (t + 1) % loop.NB
+        loop._act_step(t)
+        loop._replay(t)
+        a = loop.acts[b].cpu().numpy()
+        np.testing.assert_array_equal(a[:, 1:], env.synth_actions(seed=2024, step=t).cpu().numpy()[:, 1:])
+        assert ((a[:, 0] >= 0) & (a[:, 0] < 5)).all()
+        ro, do = o.step(a, nthreads=THREADS)
+        ctx = f"C3 code loop step {t}"
+        assert_rewards(loop.rewards[b].cpu().numpy(), ro, ctx)
+        np.testing.assert_array_equal(loop.dones[b].cpu().numpy().astype(bool), do, err_msg=ctx)
+        nxt = o.obs(3, 1)[:, 0]
+        got = decode_code(loop.code[nb].cpu().numpy(), W)
+        if not np.array_equal(got.view(np.uint32), nxt.view(np.uint32)):
+            bad = np.argwhere((got != nxt).reshape(E, -1).any(1)).ravel()
+            raise AssertionError(f"{ctx}: code differs from the oracle's observation in envs {bad[:10]}")
+        if t % 10 == 9:
+            assert_state(gpu_state(env), o.state(), ctx)
+        if t in (0, 57, seg - 1):  # the act on the step's code == an f32 forward of the oracle's observation
+            q = torch.empty((E, 5), device=env.device)
+            tmp = torch.empty((E, 1), dtype=torch.int32, device=env.device)
+            loop.net.act(loop.code[nb], 0.0, actions=tmp, q_out=q)
+            x = torch.from_numpy(nxt.reshape(E, -1))
+            ref = x
+            for i, (w, bias) in enumerate(zip(loop.net.weights, loop.net.biases)):
+                ref = ref @ w.cpu().t() + bias.cpu()
+                if i < len(loop.net.weights) - 1:
+                    ref = torch.relu(ref)
+            scale = 1.0 + ref.abs().amax(dim=1, keepdim=True)
+            assert ((q.cpu() - ref).abs() / scale).max().item() <= 1e-5, ctx
+        if t >= t_keep:
+            hist[t] = (prev, a[:, 0].copy(), ro[:, 0].astype(np.float32), nxt, do[:, 0])
+        prev = nxt
+    torch.cuda.synchronize()
+    env.check_errors()
+    loop.net.check_errors()
+    # the code ring (buffers.py:57-80): transition i (step i // E, env i % E) in slot i % cap, decoded
+    rb = loop.rb
+    assert rb.cursor == (seg * E) % cap and rb.size == cap
+    slots = np.arange(seg * E - cap, seg * E)
+    tt, ee, order = slots // E, slots % E, slots % cap
+    want_obs = np.stack([hist[t][0][e] for t, e in zip(tt, ee)])
+    want_next = np.stack([hist[t][3][e] for t, e in zip(tt, ee)])
+    np.testing.assert_array_equal(decode_code(rb.obs.cpu().numpy(), W)[order], want_obs)
+    np.testing.assert_array_equal(decode_code(rb.next_obs.cpu().numpy(), W)[order], want_next)
+    np.testing.assert_array_equal(rb.actions.cpu().numpy()[order], [hist[t][1][e] for t, e in zip(tt, ee)])
+    np.testing.assert_array_equal(rb.rewards.cpu().numpy()[order], [hist[t][2][e] for t, e in zip(tt, ee)])
+    np.testing.assert_array_equal(rb.dones.cpu().numpy()[order].astype(bool), [hist[t][4][e] for t, e in zip(tt, ee)])
+    # sample(): the device decode of the drawn rows == the oracle's transitions
+    idx = torch.randint(0, rb.size, (256,), device=env.device,
+                        generator=torch.Generator(device=env.device).manual_seed(3))  # what sample() draws
+    smp = rb.sample(256, generator=torch.Generator(device=env.device).manual_seed(3))
+    slot_of = np.empty(cap, np.int64)
+    slot_of[order] = np.arange(cap)
+    k = slot_of[idx.cpu().numpy()]
+    np.testing.assert_array_equal(smp["obs"].cpu().numpy(), want_obs[k].reshape(256, -1))
+    np.testing.assert_array_equal(smp["next_obs"].cpu().numpy(), want_next[k].reshape(256, -1))
+    acts_want = np.asarray([hist[t][1][e] for t, e in zip(tt, ee)])
+    np.testing.assert_array_equal(smp["actions"].cpu().numpy(), acts_want[k])
+    # reset_env_every (train_jax.py:101-113), as TrainSegment.run ends: every stream continues; first code
+    env.reset(seed=None)
+    loop._first_obs()
+    o.reset(None)
+    assert_state(gpu_state(env), o.state(), "C3 code loop reset")
+    assert np.array_equal(decode_code(loop.code[0].cpu().numpy(), W), o.obs(3, 1)[:, 0]), "reset code"

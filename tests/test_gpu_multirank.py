@@ -130,3 +130,24 @@ def test_bench_two_ranks_gloo_whole_job_json():
     c5 = d["c5"]
     assert c5["config"]["num_envs_total"] == 2 * 1024 and c5["steps"] >= 200 and c5["n_gpus"] == 2
     assert c5["value"] == pytest.approx(2 * 1024 * c5["steps"] / (c5["ms_per_step"] * c5["steps"] / 1e3), rel=1e-6)
+
+
+def test_bench_gpus2_launches_its_own_ranks():
+    """a plain `bench.py --gpus 2` (no torchrun) starts
+    its own 2 ranks (here gloo, both on the one GPU) and relays rank 0's one
+    whole-job line: n_gpus 2, 2x the envs, and the north-star C5 sub-record
+    at 131,072 envs per rank (262,144 over the job)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(DRL_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", DRL_BENCH_PMC="0")
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "5",
+           "--envs", "4096", "--no-cpu-baseline", "--no-dqn", "--no-reset-bench", "--rollout-chunk", "0",
+           "--loop-segments", "0", "--cached-steps", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith('{"metric"'), r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["num_envs_total"] == 2 * 4096
+    assert d["config"]["parallelism"] == "env-shard x2"
+    assert d["c5"]["config"]["num_envs_total"] == 262144 and d["c5"]["n_gpus"] == 2
+    assert "torch.distributed.run" in r.stderr  # the launcher's own line
