@@ -858,29 +858,36 @@ class StepRunner:
                                    "step count"}}
 
 
-def measure_copy_peak(dev, nbytes: int = 2 << 30, reps: int = 6):
+def measure_copy_peak(dev, nbytes: int = 2 << 30, reps: int = 8):
     """the measured copy-kernel rate beside the 8 TB/s spec
-    (MI355X_MICROARCH.md: 6.29 TB/s for a float4 copy).  Two 2-GiB buffers
-    (past the 256-MiB Infinity Cache), `copy_` timed with HIP events; GB/s of
-    bytes read + written.  Also a read-only rate (`sum`)."""
-    n = nbytes // 4
-    a = torch.ones(n, dtype=torch.float32, device=dev)
+    (MI355X_MICROARCH.md: 6.29 TB/s for a float4 copy).  drl_hbm_probe (16-B
+    non-temporal accesses) over two 2-GiB buffers, past the 256-MiB Infinity
+    Cache, timed with HIP events on the launch stream: copy = GB/s of bytes
+    read + written, read = GB/s of a read-only pass."""
+    from dronerl_amd._native import lib
+    L = lib()
+    a = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
     b = torch.empty_like(a)
+    st = torch.cuda.current_stream(dev)
     out = {}
-    for name, fn, mult in (("copy", lambda: b.copy_(a), 2), ("read", lambda: a.sum(), 1)):
-        fn()
+    for name, mode, mult in (("copy", 0, 2), ("read", 1, 1)):
+        run = lambda: L.drl_hbm_probe(ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()),  # noqa: E731
+                                      nbytes, mode, ctypes.c_void_p(st.cuda_stream))
+        if run():
+            raise RuntimeError(L.drl_last_error().decode())
         torch.cuda.synchronize(dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
+        e0.record(st)
         for _ in range(reps):
-            fn()
-        e1.record()
+            run()
+        e1.record(st)
         torch.cuda.synchronize(dev)
         out[name] = mult * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
     del a, b
     torch.cuda.empty_cache()
     return {"copy_GBs": out["copy"], "read_GBs": out["read"],
-            "note": f"in-run probe: torch copy_ of {nbytes >> 20} MiB (read + write bytes) and sum (read) on this GPU"}
+            "note": f"in-run probe: drl_hbm_probe copy (read + write bytes) and read-only passes over {nbytes >> 20} "
+                    "MiB buffers (16-B non-temporal accesses) on this GPU"}
 
 
 def roofline(E, R, Wb, launch_s, refill, traffic, G=None, peak_measured=None):

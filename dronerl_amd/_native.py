@@ -39,7 +39,9 @@ EXPORTS = ["drl_abi_version", "drl_last_error", "drl_side_from_density", "drl_la
            "drl_env_errors",
            # DQN consumer
            "drl_qnet_packed_bytes", "drl_qnet_pack", "drl_qnet_act", "drl_qnet_act_synth", "drl_qnet_act_code",
-           "drl_replay_add"]
+           "drl_replay_add",
+           # measurement helper (the measured copy-kernel peak)
+           "drl_hbm_probe"]
 
 
 class DrlParams(ctypes.Structure):
@@ -123,8 +125,9 @@ def lib():
     L.drl_decode.argtypes = [P, S, vp, vp, vp, vp, vp, vp]
     L.drl_encode.argtypes = [P, S, vp, vp, vp, vp, vp, vp]
     L.drl_synth_actions.argtypes = [u64, u64, i64, i64, i32, vp, vp]
+    L.drl_hbm_probe.argtypes = [vp, vp, i64, i32, vp]
     for f in ["drl_layout_query", "drl_reset", "drl_step", "drl_step_ex", "drl_rollout", "drl_refill", "drl_mt_get", "drl_mt_set", "drl_obs", "drl_grid_obs", "drl_decode", "drl_encode",
-              "drl_synth_actions", "drl_obs_code", "drl_step_code", "drl_code_decode"]:
+              "drl_synth_actions", "drl_obs_code", "drl_step_code", "drl_code_decode", "drl_hbm_probe"]:
         getattr(L, f).restype = ctypes.c_int
     if L.drl_abi_version() != DRL_ABI_VERSION:
         raise DroneRLError("libdronerl.so ABI version mismatch; rebuild it")

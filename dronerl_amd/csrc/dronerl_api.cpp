@@ -508,6 +508,17 @@ int drl_code_decode(int32_t window_radius, const void* d_code, int64_t n, float*
     return e == hipSuccess ? 0 : hip_fail(e, "drl_code_decode launch");
 }
 
+int drl_hbm_probe(const void* d_src, void* d_dst, int64_t bytes, int32_t mode, hipStream_t stream) {
+    if (mode != 0 && mode != 1) return fail("mode must be 0 (copy) or 1 (read)");
+    if (bytes <= 0 || bytes % 16) return fail("bytes must be a positive multiple of 16");
+    if (!d_src || !d_dst) return fail("src / dst is NULL");
+    if ((uintptr_t)d_src % 16 || (uintptr_t)d_dst % 16) return fail("src and dst must be 16-byte aligned");
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipError_t e = drl::launch_hbm_probe(d_src, d_dst, bytes, mode, cus > 0 ? cus : 256, stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_hbm_probe launch");
+}
+
 int drl_encode(const drl_params* p, const drl_state* s, const int32_t* d_order, const int32_t* d_y, const int32_t* d_x,
                const int32_t* d_charge, const uint8_t* d_carry, hipStream_t stream) {
     drl_layout L;

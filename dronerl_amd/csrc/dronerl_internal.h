@@ -300,6 +300,7 @@ hipError_t launch_reset(const ResetArgs& a, hipStream_t s);
 hipError_t launch_decode(const uint32_t* drones, int64_t E, int N, int32_t* order, int32_t* y, int32_t* x,
                          int32_t* c, uint8_t* k, hipStream_t s);
 hipError_t launch_code_decode(const void* code, int64_t n, int W, float* obs, hipStream_t s);
+hipError_t launch_hbm_probe(const void* src, void* dst, int64_t bytes, int mode, int num_cus, hipStream_t s);
 hipError_t launch_grid_obs(const uint8_t* ground, const uint32_t* drones, int64_t E, int side, int N, int gstride,
                            float* out, hipStream_t s);
 hipError_t launch_encode(uint32_t* drones, int64_t E, int N, const int32_t* order, const int32_t* y,

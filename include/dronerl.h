@@ -233,6 +233,12 @@ int drl_step_code(const drl_params* p, const drl_state* s, const int32_t* d_acti
 /* Policy code rows -> drone index 0's observation, f32 [n][W][W][6] exactly
  * as drl_obs writes it (a replay buffer of codes decodes its samples). */
 int drl_code_decode(int32_t window_radius, const void* d_code, int64_t n, float* d_obs, hipStream_t stream);
+/* Measurement helper (the measured copy-kernel peak beside
+ * the spec): mode 0 copies `bytes` from d_src to d_dst, mode 1 only reads
+ * d_src (d_dst: a scratch buffer of >= 4 KiB per workgroup it may write).
+ * 16-B non-temporal accesses, 8 workgroups of 256 lanes per CU.  Time it with
+ * events on `stream`. */
+int drl_hbm_probe(const void* d_src, void* d_dst, int64_t bytes, int32_t mode, hipStream_t stream);
 /* drl_obs that also writes the policy code (d_code nullable); d_obs NULL:
  * the code alone (k ignored). */
 int drl_obs_code(const drl_params* p, const drl_state* s, int32_t k, float* d_obs, void* d_code, hipStream_t stream);

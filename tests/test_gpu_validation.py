@@ -131,3 +131,23 @@ def test_full_grid_respawn_raises_no_free_cell():
     e.step(torch.tensor([act], dtype=torch.int32, device="cuda:0"))
     with pytest.raises(DroneRLError, match="no free cell"):
         e.check_errors()
+
+
+def test_hbm_probe_copies_and_reads():
+    """drl_hbm_probe (bench.py's measured copy peak): the copy form copies every
+    byte (sizes not a multiple of the grid's stride included); both forms check
+    their arguments."""
+    import ctypes
+    from dronerl_amd._native import lib
+    L = lib()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for n in (16, 4096 * 16 + 48, (3 << 20) + 16 * 7):
+        src = torch.randint(0, 2**31, (n // 4,), dtype=torch.int32, device="cuda:0")
+        dst = torch.zeros_like(src)
+        assert L.drl_hbm_probe(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), n, 0, st) == 0
+        assert torch.equal(src, dst), n
+    scratch = torch.zeros(8 << 20, dtype=torch.uint8, device="cuda:0")
+    assert L.drl_hbm_probe(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(scratch.data_ptr()), n, 1, st) == 0
+    torch.cuda.synchronize()
+    assert L.drl_hbm_probe(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), 15, 0, st) != 0
+    assert L.drl_hbm_probe(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), 16, 2, st) != 0

@@ -71,9 +71,11 @@ def main():
         q = torch.zeros((E, 5), device="cuda")
         net.act(flat, 0.1, actions=a, q_out=q)
         torch.cuda.synchronize()
-        st = q.view(torch.int32).cpu().numpy().astype("int64")[: (E + 15) // 16]
+        rows = (E + 31) // 32 if args.input == "code" and args.hidden in ("128,64", "128,32") else (E + 15) // 16
+        st = q.view(torch.int32).cpu().numpy().astype("int64").reshape(-1)[: 5 * rows].reshape(rows, 5)
         import numpy as np
-        for i, name in enumerate(("layer0", "hidden", "epilogue")):
+        for i, name in enumerate(("layer0", "hidden" if rows == (E + 15) // 16 else "layer1",
+                                  "epilogue" if rows == (E + 15) // 16 else "layer2+epilogue")):
             v = st[:, i]
             print(f"stamps {name}: median {np.median(v):.0f} p10 {np.percentile(v, 10):.0f} "
                   f"p90 {np.percentile(v, 90):.0f} cycles (s_memtime)")
