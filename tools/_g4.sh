@@ -3,7 +3,7 @@
 # (2) the nibble-ground branch (worktree _wt/nib): the whole GPU suite, then the driver's bench line
 set -o pipefail
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp && mkdir -p gpurun_out
-ROOT=$PWD
+export ROOT=$PWD
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "code or qnet or dqn" > gpurun_out/g4_code3_tests.log 2>&1; rc=$?
 tail -3 gpurun_out/g4_code3_tests.log
 [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
