@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # DRL_LIB: an alternative build of the same library (tools/variants.py A/B runs)
 LIB_PATH = os.environ.get("DRL_LIB") or os.path.join(_HERE, "libdronerl.so")
 
-DRL_ABI_VERSION = 7  # include/dronerl.h
+DRL_ABI_VERSION = 8  # include/dronerl.h
 DRL_MT_WORDS = 1776  # per-env RNG row: two MT blocks + the respawn-candidate ring
 DRL_MT_RING = 1248
 DRL_MT_RING_END = 1760

@@ -183,9 +183,9 @@ int drl_env_get_state(drl_env* env, const drl_state_view* v, hipStream_t stream)
     return on_device(env, [&]() -> int {
         if (!v) return drl_internal_fail("view is NULL");
         const size_t E = (size_t)env->num_envs, cells = (size_t)env->L.cells;
-        if (v->ground && hip_check(hipMemcpy2DAsync(v->ground, cells, env->s.ground, env->L.ground_stride, cells, E,
-                                                    hipMemcpyDeviceToDevice, stream),
-                                   "ground copy"))
+        if (v->ground && hip_check(drl::launch_ground_unpack(env->s.ground, env->L.ground_stride, v->ground, (int)cells,
+                                                             (int64_t)E, stream),
+                                   "ground unpack"))
             return -1;
         if (drl_decode(&env->p, &env->s, v->order, v->y, v->x, v->charge, v->carry, stream)) return -1;
         if (v->mt && drl_mt_get(&env->p, &env->s, v->mt, stream)) return -1;
@@ -198,9 +198,9 @@ int drl_env_set_state(drl_env* env, const drl_state_view* v, hipStream_t stream)
         if (!v || !v->ground || !v->order || !v->y || !v->x || !v->charge || !v->carry || !v->mt)
             return drl_internal_fail("set_state needs every view field");
         const size_t E = (size_t)env->num_envs, cells = (size_t)env->L.cells;
-        if (hip_check(hipMemcpy2DAsync(env->s.ground, env->L.ground_stride, v->ground, cells, cells, E,
-                                       hipMemcpyDeviceToDevice, stream),
-                      "ground copy"))
+        if (hip_check(drl::launch_ground_pack(v->ground, (int)cells, env->s.ground, env->L.ground_stride, (int64_t)E,
+                                              stream),
+                      "ground pack"))
             return -1;
         if (drl_encode(&env->p, &env->s, v->order, v->y, v->x, v->charge, v->carry, stream)) return -1;
         if (drl_mt_set(&env->p, &env->s, v->mt, env->err, stream)) return -1;  // (then a refill)

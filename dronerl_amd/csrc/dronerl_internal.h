@@ -87,7 +87,10 @@ constexpr int OBS_U = 1;        // observation cells per lane per pass (stage: O
 namespace lay {
 constexpr int r16(int v) { return (v + 15) / 16 * 16; }
 constexpr int np(int n_drones) { return (n_drones + 7) / 8 * 8; }             // posidx entries
-constexpr int gstride(int side) { return r16(side * side); }                   // ground bytes
+// ground: packed in HBM, one nibble per cell (cell 2i in the low nibble of
+// byte i, 2i + 1 in the high one; ABI 8), unpacked to a byte per cell in LDS
+constexpr int pstride(int side) { return r16((side * side + 1) / 2); }         // HBM ground bytes per env
+constexpr int gstride(int side) { return 2 * pstride(side); }                  // LDS ground bytes per env
 constexpr int bm_bytes(int cells) { return r16((cells + 31) / 32 * 4); }       // occupancy bitmap
 constexpr int paint_bytes(int k, int w) { return k > 0 ? r16(k * w * w) : 0; }  // observation paint
 constexpr int nchg(int n_drones) { return 6 * n_drones + 2; }                  // changed-cell capacity
@@ -144,7 +147,7 @@ struct ObsGeom {
 };
 
 struct StepArgs {
-    int side, n_drones, gstride, kbits;
+    int side, n_drones, gstride, kbits;  // gstride: LDS ground bytes per env (2 x the packed HBM row)
     int charge, discharge;
     float r_pickup, r_delivery, r_crash, r_charge;
     int64_t E;
@@ -188,7 +191,7 @@ struct RefillArgs {
 };
 
 struct ResetArgs {
-    int side, n_drones, cells, gstride;
+    int side, n_drones, cells, gstride;  // gstride: packed HBM ground bytes per env (lay::pstride)
     int n_sky, n_pack, n_drop, n_stat;
     int64_t E;
     uint8_t* ground;
@@ -301,6 +304,8 @@ hipError_t launch_decode(const uint32_t* drones, int64_t E, int N, int32_t* orde
                          int32_t* c, uint8_t* k, hipStream_t s);
 hipError_t launch_code_decode(const void* code, int64_t n, int W, float* obs, hipStream_t s);
 hipError_t launch_hbm_probe(const void* src, void* dst, int64_t bytes, int mode, int num_cus, hipStream_t s);
+hipError_t launch_ground_unpack(const uint8_t* packed, int pstride, uint8_t* out, int cells, int64_t E, hipStream_t s);
+hipError_t launch_ground_pack(const uint8_t* in, int cells, uint8_t* packed, int pstride, int64_t E, hipStream_t s);
 hipError_t launch_grid_obs(const uint8_t* ground, const uint32_t* drones, int64_t E, int side, int N, int gstride,
                            float* out, hipStream_t s);
 hipError_t launch_encode(uint32_t* drones, int64_t E, int N, const int32_t* order, const int32_t* y,

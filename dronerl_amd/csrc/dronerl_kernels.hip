@@ -325,32 +325,79 @@ __device__ __forceinline__ WaveLds carve(l_u8* wb, int gpw, int P, const GEO& g)
     return w;
 }
 
-// Async copy of the wave's grounds (contiguous in HBM, env-major) into LDS:
-// global_load_lds_dwordx4, 1 KiB per wave-instruction, no VGPR round trip.
-__device__ __forceinline__ void stage_ground_dma(const uint8_t* __restrict__ src, int nbytes, l_u8* gl, int lane) {
-    const int nvec = nbytes / 16;
-    for (int v0 = 0; v0 < nvec; v0 += 64) {
-        if (v0 + lane < nvec)
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void*)(src + (uint32_t)(v0 + lane) * 16u),
-                (__attribute__((address_space(3))) void*)(gl + v0 * 16), 16, 0, 0);
+// The ground is packed in HBM (one nibble per cell, ABI 8: half the bytes of
+// the round-3 byte layout) and unpacked into a byte per cell in LDS: a packed
+// 16-B vector holds 32 cells, which go to 32 LDS bytes (the LDS row is twice
+// the packed row, so the wave's rows stay contiguous in both).
+__device__ __forceinline__ void nib_unpack_store(l_u8* dst, const uint4 v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t lo = w[k] & 0x0f0f0f0fu, hi = (w[k] >> 4) & 0x0f0f0f0fu;
+        o[2 * k] = __builtin_amdgcn_perm(hi, lo, 0x05010400u);      // cells 8k+0..3
+        o[2 * k + 1] = __builtin_amdgcn_perm(hi, lo, 0x07030602u);  // cells 8k+4..7
     }
+    reinterpret_cast<l_u4*>(dst)[0] = u32x4{o[0], o[1], o[2], o[3]};
+    reinterpret_cast<l_u4*>(dst)[1] = u32x4{o[4], o[5], o[6], o[7]};
 }
 
-// Compile-time variant: exactly NV vectors, unrolled, so the compiler can count
-// the outstanding loads (a runtime trip count forces a vmcnt(0) after the
-// loop).  Vectors past the wave's valid envs re-read the last valid vector
-// into LDS the wave does not use.
-template <int NV>
-__device__ __forceinline__ void stage_ground_dma_n(const uint8_t* __restrict__ src, int nbytes, l_u8* gl, int lane) {
-    const uint32_t last = (uint32_t)(nbytes / 16 - 1);
+// 32 LDS bytes (cells < 16) -> the packed 16-B vector
+__device__ __forceinline__ uint4 nib_pack_load(const l_u8* src) {
+    const u32x4 a = reinterpret_cast<const l_u4*>(src)[0], b = reinterpret_cast<const l_u4*>(src)[1];
+    const uint32_t c[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    uint32_t o[4];
 #pragma unroll
-    for (int v0 = 0; v0 < NV; v0 += 64) {
-        if (NV - v0 >= 64 || lane < NV - v0)
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void*)(src + min((uint32_t)(v0 + lane), last) * 16u),
-                (__attribute__((address_space(3))) void*)(gl + v0 * 16), 16, 0, 0);
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t t0 = c[2 * k] | (c[2 * k] >> 4), t1 = c[2 * k + 1] | (c[2 * k + 1] >> 4);
+        o[k] = __builtin_amdgcn_perm(t1, t0, 0x06040200u);  // bytes 0 and 2 of each
     }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// The wave's packed grounds (contiguous in HBM, env-major, nbytes) -> LDS,
+// runtime geometry: load, unpack, store.
+__device__ __forceinline__ void stage_ground_nib(const uint8_t* __restrict__ src, int nbytes, l_u8* gl, int lane) {
+    const int nvec = nbytes / 16;
+    for (int v = lane; v < nvec; v += 64) nib_unpack_store(gl + v * 32, reinterpret_cast<const uint4*>(src)[v]);
+}
+
+// Compile-time form in two halves: the loads (NV vectors, unrolled, so the
+// compiler counts them; vectors past the wave's valid envs re-read the last
+// valid vector and unpack into LDS the wave does not use) are issued with the
+// step's first loads, the unpack and LDS stores come after the claim scan,
+// which does not need the ground, so the loads' latency overlaps it.
+template <int NV>
+struct NibStage {
+    static constexpr int Q = (NV + 63) / 64;
+    uint4 v[Q];
+    __device__ __forceinline__ void load(const uint8_t* __restrict__ src, int nbytes, int lane) {
+        const uint32_t last = (uint32_t)(nbytes / 16 - 1);
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+            v[q] = reinterpret_cast<const uint4*>(src)[min((uint32_t)(64 * q + lane), last)];
+    }
+    __device__ __forceinline__ void store(l_u8* gl, int lane) const {
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+            if (NV % 64 == 0 || 64 * q + lane < NV) nib_unpack_store(gl + (64 * q + lane) * 32, v[q]);
+    }
+};
+
+// packed-ground nibble access in HBM (reset; grid observation)
+__device__ __forceinline__ uint32_t nib_get(const uint8_t* row, int cell) {
+    return (row[cell >> 1] >> ((cell & 1) * 4)) & 15u;
+}
+__device__ __forceinline__ void nib_or(uint8_t* row, int cell, uint32_t code) {  // the cell's nibble is 0
+    atomicOr(reinterpret_cast<uint32_t*>(row) + (cell >> 3), code << ((cell & 7) * 4));
+}
+__device__ __forceinline__ uint32_t nib_get_l2(uint8_t* row, int cell) {  // after nib_or: read at L2
+    const uint32_t w = __hip_atomic_load(reinterpret_cast<uint32_t*>(row) + (cell >> 3), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    return (w >> ((cell & 7) * 4)) & 15u;
+}
+__device__ __forceinline__ void nib_clear(uint8_t* row, int cell) {
+    atomicAnd(reinterpret_cast<uint32_t*>(row) + (cell >> 3), ~(15u << ((cell & 7) * 4)));
 }
 
 // 16-B observation store.  NT: streaming (global_store_dwordx4 ... nt), for
@@ -624,7 +671,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     // the wave's slices of the state (scalar bases)
     uint32_t* const drones_w = a.drones + wenv0 * N;
     uint32_t* const mt_w = a.mt + wenv0 * MT_WORDS;
-    uint8_t* const ground_w = a.ground + wenv0 * gstride;
+    uint8_t* const ground_w = a.ground + wenv0 * (gstride / 2);  // packed rows: half the LDS stride
     const uint32_t rl0 = (uint32_t)(grp0 * N);  // lane's env offset in [env][drone] arrays of the wave
 
     DRL_STAMP(0);
@@ -650,8 +697,10 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
 #else
     const int act_ld = a.actions[wenv0 * N + li0];
 #endif
-    if constexpr (GEO::kGstride > 0) stage_ground_dma_n<GPW * GEO::kGstride / 16>(ground_w, nenv_w * gstride, W.gl, lane0);
-    else stage_ground_dma(ground_w, nenv_w * gstride, W.gl, lane0);
+    // the packed grounds: loaded now, unpacked into LDS after the claim scan (compile-time geometry)
+    [[maybe_unused]] NibStage<(GEO::kGstride > 0 ? GPW * GEO::kGstride / 32 : 1)> nib;
+    if constexpr (GEO::kGstride > 0) nib.load(ground_w, nenv_w * (gstride / 2), lane0);
+    else stage_ground_nib(ground_w, nenv_w * (gstride / 2), W.gl, lane0);
     __builtin_amdgcn_sched_barrier(0);  // issue every load above before waiting for the MT index
     uint32_t mword = mi[0];  // the env's mt_index word: index, block, ring head / count
 #pragma unroll
@@ -773,8 +822,10 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     }
     const bool claimer = inb && !earlier;
     const bool crashA = active && !claimer;
-    // the ground DMA has landed: the compiler waits for LDS-DMA before LDS
-    // reads (and already did, at the first record use); wave_sync orders lanes
+    if constexpr (GEO::kGstride > 0) {
+        if (t == 0) nib.store(W.gl, lane0);  // (a rollout stages once)
+    }
+    // the grounds are in LDS; wave_sync orders lanes
     wave_sync();
 
     DRL_STAMP(2);
@@ -1179,7 +1230,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     if (!ROLL && env_ok) {
         const uint32_t nc = W.cnt[grp * 4];
         const l_u16* ch = W.chg + grp * nchg;
-        uint8_t* gdst = ground_w + (uint32_t)(grp * gstride);
+        uint8_t* gdst = ground_w + (uint32_t)(grp * (gstride / 2));
         // Changes per step <= 4N (N pickups/deliveries, 2N respawned packets and
         // dropzones, N pick-after-respawn) < the list's 6N + 2 entries, so the
         // list never overflows (chg_push drops past capacity regardless).  The
@@ -1187,7 +1238,10 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         // cost registers the whole kernel pays for.
 #ifndef DRL_DIAG_NO_GROUND_WB  // bytes-only diagnostic build (wrong state): no changed-cell write-back
 #pragma clang loop unroll(disable) vectorize(disable)
-        for (uint32_t q = j; q < min(nc, (uint32_t)nchg); q += P) gdst[ch[q]] = gl[ch[q]];
+        for (uint32_t q = j; q < min(nc, (uint32_t)nchg); q += P) {  // the cell's packed byte (both nibbles)
+            const uint32_t e = ch[q] & ~1u;
+            gdst[e >> 1] = (uint8_t)(gl[e] | (gl[e + 1] << 4));
+        }
 #endif
     }
     DRL_STAMP(5);
@@ -1215,9 +1269,8 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         wave_sync();
         if (active0) drones_w[rl0 + j0] = stash[lane0];
         if (env_ok0 && j0 == 0) a.mt_index[wenv0 + grp0] = mword;
-        const l_u4* src = reinterpret_cast<const l_u4*>(W.gl);
-        u32x4* dst = reinterpret_cast<u32x4*>(ground_w);
-        for (int v = lane0; v < nenv_w * gstride / 16; v += 64) dst[v] = src[v];
+        uint4* dst = reinterpret_cast<uint4*>(ground_w);
+        for (int v = lane0; v < nenv_w * gstride / 32; v += 64) dst[v] = nib_pack_load(W.gl + v * 32);
     }
 }
 
@@ -1271,7 +1324,7 @@ __global__ void __launch_bounds__(64) drl_obs_kernel(StepArgs a) {
     const bool env_ok = grp < nenv_w;
     const int N = g.n(), gstride = g.gstride();
     const WaveLds W = carve((l_u8*)smem, GPW, P, g);
-    stage_ground_dma(a.ground + wenv0 * gstride, nenv_w * gstride, W.gl, lane);
+    stage_ground_nib(a.ground + wenv0 * (gstride / 2), nenv_w * (gstride / 2), W.gl, lane);
     lds_zero(W.paint, GPW * g.lds_paint(), lane);
     const bool active = env_ok && j < N;
     const uint32_t rec = active ? a.drones[wenv0 * N + (uint32_t)(grp * N + j)] : 0u;
@@ -1415,6 +1468,7 @@ __global__ void __launch_bounds__(64) drl_reset_kernel(ResetArgs a) {
         for (int v = 0; v < a.gstride / 16; ++v) reinterpret_cast<uint4*>(grow)[v] = make_uint4(0u, 0u, 0u, 0u);
         for (int i = 0; i < GG; ++i) list[i] = (uint16_t)i;
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zeroed rows before the nibble ORs
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     int midx = own ? (a.reseed ? MT_N : min(mi_idx(w0), MT_N)) : MT_N;
     int n = GG;
@@ -1458,7 +1512,7 @@ __global__ void __launch_bounds__(64) drl_reset_kernel(ResetArgs a) {
     // skyscrapers: shuffle, pop from the end (env.py:58-66,83-84)
     DRL_SHUFFLE(n)
     if (own)
-        for (int t = 0; t < a.n_sky; ++t) grow[list[n - 1 - t]] = OBJ_SKYSCRAPER;
+        for (int t = 0; t < a.n_sky; ++t) nib_or(grow, list[n - 1 - t], OBJ_SKYSCRAPER);
     n -= a.n_sky;
 
     // drones: Random.sample(list[0:n], N) (random.py:480-504, env.py:88-89)
@@ -1493,27 +1547,28 @@ __global__ void __launch_bounds__(64) drl_reset_kernel(ResetArgs a) {
     // packets, dropzones, stations (env.py:91-96)
     DRL_SHUFFLE(n)
     if (own)
-        for (int t = 0; t < a.n_pack; ++t) grow[list[n - 1 - t]] = OBJ_PACKET;
+        for (int t = 0; t < a.n_pack; ++t) nib_or(grow, list[n - 1 - t], OBJ_PACKET);
     n -= a.n_pack;
     DRL_SHUFFLE(n)
     if (own)
-        for (int t = 0; t < a.n_drop; ++t) grow[list[n - 1 - t]] = OBJ_DROPZONE;
+        for (int t = 0; t < a.n_drop; ++t) nib_or(grow, list[n - 1 - t], OBJ_DROPZONE);
     n -= a.n_drop;
     DRL_SHUFFLE(n)
     if (own)
-        for (int t = 0; t < a.n_stat; ++t) grow[list[n - 1 - t]] = OBJ_STATION;
+        for (int t = 0; t < a.n_stat; ++t) nib_or(grow, list[n - 1 - t], OBJ_STATION);
     n -= a.n_stat;
 #undef DRL_SHUFFLE
 #undef DRL_DRAW_LOOP
 
     // drones in index order (dict order 0..N-1), then _pick_packets_after_respawn
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the placements' nibble ORs have landed
     if (own) {
         for (int d = 0; d < N; ++d) {
             const int cell = sel[d];
             int carry = 0;
-            if (grow[cell] == OBJ_PACKET) {
+            if (nib_get_l2(grow, cell) == OBJ_PACKET) {
                 carry = 1;
-                grow[cell] = OBJ_EMPTY;
+                nib_clear(grow, cell);
             }
             const uint32_t py = fdiv((uint32_t)cell, a.div_side);
             a.drones[env * N + d] = pack_drone((int)py, cell - (int)py * a.side, 100, carry, d);
@@ -1785,6 +1840,7 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
     }
     for (int v = lane; v < a.gstride / 16; v += 64) reinterpret_cast<uint4*>(grow)[v] = make_uint4(0u, 0u, 0u, 0u);
     for (int i = lane; i < GG; i += 64) list[i] = (uint16_t)i;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zeroed row before the nibble ORs
     uint32_t tcur = temper(x[__builtin_amdgcn_readfirstlane(rot)]);
     wave_sync();
 
@@ -1797,7 +1853,7 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
     uint32_t mine = 0xffffffffu;  // set branch: lane q < N holds selection q
     auto place = [&](int count, uint8_t code) __attribute__((always_inline)) {  // pop `count` from the end
         wave_sync();
-        for (int t = lane; t < count; t += 64) grow[list[n - 1 - t]] = code;
+        for (int t = lane; t < count; t += 64) nib_or(grow, list[n - 1 - t], code);  // (packed row: atomic ORs)
         n -= count;
     };
     // finish phases that need no (more) draws; set up the next one
@@ -1922,9 +1978,10 @@ __global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
     if (lane < N) {
         const int cell = sel[lane];
         int carry = 0;
-        if (grow[cell] == OBJ_PACKET) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the placements' ORs have landed
+        if (nib_get_l2(grow, cell) == OBJ_PACKET) {
             carry = 1;
-            grow[cell] = OBJ_EMPTY;
+            nib_clear(grow, cell);
         }
         const uint32_t py = fdiv((uint32_t)cell, a.div_side);
         a.drones[env * N + lane] = pack_drone((int)py, cell - (int)py * a.side, 100, carry, lane);
@@ -1958,7 +2015,7 @@ __global__ void __launch_bounds__(256) drl_grid_obs_kernel(const uint8_t* __rest
     const uint8_t* g = ground + e * gstride;
     float2* o = reinterpret_cast<float2*>(out + e * (int64_t)cells * 6);
     for (int c = threadIdx.x; c < cells; c += blockDim.x) {
-        const uint32_t obj = g[c], a = air[c];
+        const uint32_t obj = nib_get(g, c), a = air[c];
         o[3 * c] = make_float2(a ? 1.0f : 0.0f, (obj == OBJ_PACKET || (a & 0x80u)) ? 1.0f : 0.0f);
         o[3 * c + 1] = make_float2(obj == OBJ_DROPZONE ? 1.0f : 0.0f, obj == OBJ_STATION ? 1.0f : 0.0f);
         o[3 * c + 2] = make_float2(a ? div100((int)(a & 0x7fu) - 1) : 0.0f, obj == OBJ_SKYSCRAPER ? 1.0f : 0.0f);
@@ -2325,6 +2382,40 @@ hipError_t launch_decode(const uint32_t* drones, int64_t E, int N, int32_t* orde
     const int64_t total = E * N;
     hipLaunchKernelGGL(drl_decode_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, drones, total, N,
                        order, y, x, c, k);
+    return hipGetLastError();
+}
+
+// packed grounds <-> a byte per cell (drl_env_get_state / drl_env_set_state)
+__global__ void drl_ground_unpack_kernel(const uint8_t* __restrict__ packed, int pstride, uint8_t* __restrict__ out,
+                                         int cells, int64_t total) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int64_t e = i / cells;
+    const int c = (int)(i - e * cells);
+    out[i] = (uint8_t)nib_get(packed + e * pstride, c);
+}
+__global__ void drl_ground_pack_kernel(const uint8_t* __restrict__ in, int cells, uint8_t* __restrict__ packed,
+                                       int pstride, int64_t total) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one packed byte
+    if (i >= total) return;
+    const int64_t e = i / pstride;
+    const int b = (int)(i - e * pstride), c0 = 2 * b;
+    const uint8_t* row = in + e * cells;
+    const uint32_t lo = c0 < cells ? (row[c0] & 15u) : 0u, hi = c0 + 1 < cells ? (row[c0 + 1] & 15u) : 0u;
+    packed[i] = (uint8_t)(lo | (hi << 4));
+}
+hipError_t launch_ground_unpack(const uint8_t* packed, int pstride, uint8_t* out, int cells, int64_t E, hipStream_t s) {
+    const int64_t total = E * cells;
+    if (total <= 0) return hipSuccess;
+    hipLaunchKernelGGL(drl_ground_unpack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, packed, pstride,
+                       out, cells, total);
+    return hipGetLastError();
+}
+hipError_t launch_ground_pack(const uint8_t* in, int cells, uint8_t* packed, int pstride, int64_t E, hipStream_t s) {
+    const int64_t total = E * pstride;
+    if (total <= 0) return hipSuccess;
+    hipLaunchKernelGGL(drl_ground_pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, in, cells, packed,
+                       pstride, total);
     return hipGetLastError();
 }
 

@@ -30,11 +30,31 @@ def _stream(device: torch.device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+def unpack_ground(packed: torch.Tensor, side: int) -> torch.Tensor:
+    """Packed ground rows [E, ground_stride] -> object codes uint8 [E, side, side]."""
+    E = packed.shape[0]
+    cells = torch.stack((packed & 15, packed >> 4), dim=-1).reshape(E, -1)
+    return cells[:, :side * side].reshape(E, side, side)
+
+
+def pack_ground(ground: torch.Tensor, stride: int) -> torch.Tensor:
+    """Object codes [E, cells] (uint8, < 16) -> packed rows [E, stride] (zero padding)."""
+    E = ground.shape[0]
+    g = ground.reshape(E, -1)
+    if g.numel() and int(g.max()) > 15:
+        raise ValueError("ground codes must be < 16")
+    full = torch.zeros((E, 2 * stride), dtype=torch.uint8, device=g.device)
+    full[:, :g.shape[1]] = g
+    return full[:, 0::2] | (full[:, 1::2] << 4)
+
+
 @dataclass
 class DroneEnvState:
     """Device state of E envs (structure of arrays, env-major; include/dronerl.h).
 
-    ground : uint8 [E, ground_stride]  object code per cell, row-major (first side*side bytes)
+    ground : uint8 [E, ground_stride]  object codes, row-major, two cells per byte (cell k in the
+                                       low nibble of byte k // 2 when k is even, the high one when
+                                       odd; include/dronerl.h ABI 8): decode() / set_state() convert
     drones : int32 [E, n_drones]       packed u32 records in dict order O
     mt     : int32 [E, 1776]           two MT19937 blocks + the respawn-candidate ring
     mt_index: int32 [E]                CPython's MT index (bits 0-9), the block holding the
@@ -284,7 +304,7 @@ class BatchedDeliveryDrones:
         check(lib().drl_decode(ctypes.byref(self._cp), ctypes.byref(s), _ptr(out["order"]), _ptr(out["y"]),
                                _ptr(out["x"]), _ptr(out["charge"]), _ptr(out["carrying"]), _stream(self.device)),
               "drl_decode")
-        out["ground"] = self.state.ground[:, :G * G].view(E, G, G)
+        out["ground"] = unpack_ground(self.state.ground, G)
         out["mt_index"] = self.mt_words_device()[:, 624]
         return out
 
@@ -295,8 +315,7 @@ class BatchedDeliveryDrones:
         as_t = lambda a, dt: torch.as_tensor(a, dtype=dt).to(dev).reshape(E, -1).contiguous()
         g = as_t(ground, torch.uint8)
         assert g.shape[1] == G * G
-        self.state.ground.zero_()
-        self.state.ground[:, :G * G].copy_(g)
+        self.state.ground.copy_(pack_ground(g, self.state.ground.shape[1]))
         o, yy, xx, ch = (as_t(v, torch.int32) for v in (order, y, x, charge))
         k = as_t(carrying, torch.uint8)
         if not torch.equal(o.sort(1).values, torch.arange(N, device=dev, dtype=torch.int32).expand(E, N)):

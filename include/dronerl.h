@@ -46,7 +46,7 @@ extern "C" {
 
 typedef struct ihipStream_t* hipStream_t;
 
-#define DRL_ABI_VERSION 7
+#define DRL_ABI_VERSION 8
 /* Per-env RNG row of `mt` (u32 words, 7104 B):
  *   [0, 624)     MT19937 block 0     the env's CPython stream lives in block
  *   [624, 1248)  MT19937 block 1     mt_index.par; the other block holds the
@@ -103,7 +103,7 @@ typedef struct drl_layout {
     int32_t side;
     int32_t n_drones;
     int32_t cells;          /* side*side */
-    int32_t ground_stride;  /* bytes per env in `ground` (cells rounded up to 16) */
+    int32_t ground_stride;  /* bytes per env in `ground`: ceil(cells / 2) rounded up to 16 (packed nibbles) */
     int32_t drone_stride;   /* u32 records per env in `drones` (== n_drones) */
     int32_t mt_stride;      /* u32 words per env in `mt` (== DRL_MT_WORDS) */
     int32_t obs_window;     /* 2*radius+1 */
@@ -115,7 +115,11 @@ typedef struct drl_layout {
 } drl_layout;
 
 /* Device state of num_envs envs (structure of arrays, env-major).
- *  ground : u8  [E][ground_stride]  object code per cell (row-major y*side+x)
+ *  ground : u8  [E][ground_stride]  object code per cell (row-major k = y*side+x), packed
+ *           two cells per byte (ABI 8): cell k in bits 4*(k&1)..+3 of byte k/2
+ *           (the codes are < 8; half the HBM bytes of a byte per cell; the
+ *           kernels unpack into LDS).  drl_env_get_state / set_state and
+ *           BatchedDeliveryDrones.decode / set_state convert to a byte per cell.
  *  drones : u32 [E][n_drones]       one record per drone in dict order:
  *           bits 0-7 y, 8-15 x, 16-23 charge, 24 carrying, 25-31 drone index
  *  mt     : u32 [E][DRL_MT_WORDS]   two MT19937 blocks + the candidate ring (above)

@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol():
     exported = set(re.findall(r"\s(drl_\w+)$", out, re.M))
     missing = [f for f in fns if f not in exported]
     assert not missing, missing
-    assert lib().drl_abi_version() == 7
+    assert lib().drl_abi_version() == 8
 
 
 def test_library_is_gfx950_code_object():
@@ -56,7 +56,7 @@ def test_side_from_density_matches_reference_formula(n, density, side):
 def test_layout_and_validation():
     L = EnvParams(n_drones=8, grid_size=16).layout()
     assert (L.cells, L.ground_stride, L.drone_stride, L.mt_stride, L.obs_window, L.obs_floats) == \
-        (256, 256, 8, 1776, 7, 294)
+        (256, 128, 8, 1776, 7, 294)  # ground: two cells per byte (ABI 8)
     assert L.step_group_lanes == 8
     assert (L.cand_slots, L.refill_every) == (512, 32)
     L = EnvParams(n_drones=32, grid_size=64).layout()
@@ -64,7 +64,7 @@ def test_layout_and_validation():
     # half a block's worth of candidates (156 pairs at power-of-two sides) at ~1.53 + 0.06 N per step
     assert L.refill_every == 22
     L = EnvParams(n_drones=1, grid_size=5).layout()
-    assert L.ground_stride == 32
+    assert L.ground_stride == 16  # 25 cells -> 13 bytes -> 16
     with pytest.raises(ValueError, match="Not enough positions"):
         EnvParams(n_drones=8, grid_size=8).layout()  # 80 objects on 64 cells
     with pytest.raises(ValueError):
@@ -137,3 +137,21 @@ def test_refill_cadence_override_must_be_positive(monkeypatch, val, ok):
     else:
         with pytest.raises(ValueError, match="DRL_REFILL_EVERY"):
             p.layout()
+
+
+def test_ground_pack_roundtrip():
+    """The packed-nibble ground (ABI 8) round-trips through env.py's host-side
+    conversions for odd and even cell counts."""
+    from dronerl_amd.env import pack_ground, unpack_ground
+    g = torch.Generator().manual_seed(0)
+    for side in (5, 8, 13, 16, 64):
+        E = 7
+        ground = torch.randint(0, 6, (E, side * side), dtype=torch.uint8, generator=g)
+        stride = ((side * side + 1) // 2 + 15) // 16 * 16
+        packed = pack_ground(ground, stride)
+        assert packed.shape == (E, stride)
+        assert torch.equal(packed[:, 0], ground[:, 0] | (ground[:, 1] << 4))
+        assert torch.equal(unpack_ground(packed, side).reshape(E, -1), ground)
+        assert not packed[:, (side * side + 1) // 2:].any()  # zero padding
+    with pytest.raises(ValueError):
+        pack_ground(torch.full((1, 4), 16, dtype=torch.uint8), 16)
