@@ -1222,7 +1222,10 @@ __global__ void __launch_bounds__(64 * QN_CODE2_WAVES) drl_qnet_act_code2_kernel
 //  * Layer 1's fragments (from L2) are double-buffered per K-slice, the first
 //    slice's issued during layer 0's last slice; the output layer's fragments
 //    and biases during layer 1's last slice.
-constexpr int QC3_PD = 8;  // fragment reads in flight per wave (ring of QC3_PD + 2)
+#ifndef DRL_QC3_PD
+#define DRL_QC3_PD 8
+#endif
+constexpr int QC3_PD = DRL_QC3_PD;  // fragment reads in flight per wave (ring of QC3_PD + 2)
 
 typedef uint32_t q3u4 __attribute__((ext_vector_type(4)));
 
@@ -1383,6 +1386,12 @@ __global__ void __launch_bounds__(64 * QN_CODE2_WAVES) drl_qnet_act_code3_kernel
                 if constexpr (S % (2 * NT0) == 0) {
                     if (first) slice_ready(std::integral_constant<int, t>{});
                 }
+#ifdef DRL_DIAG_QC3_HALFLDS  // timing diagnostic (wrong results): odd steps re-read the even step's fragment
+                if constexpr (S % 2 == 1) {
+                    ring[S % RS] = ring[(S - 1) % RS];
+                    asm volatile("ds_read_b32 %0, %1 offset:0" : "=v"(ring[S % RS][0]) : "v"(base[0]));
+                } else
+#endif
                 qc3_read<(hl * FLO + (m * KP + t) * 64) * 16>(ring[S % RS], base);
             }
         };
@@ -1395,7 +1404,11 @@ __global__ void __launch_bounds__(64 * QN_CODE2_WAVES) drl_qnet_act_code3_kernel
             const f16x8 w = q3_f16(ring[S % RS]);
 #pragma unroll
             for (int h = 0; h < TP; ++h)
+#ifdef DRL_DIAG_QC3_NOMFMA  // timing diagnostic (wrong results): a VALU stand-in for each MFMA
+                acc[h][m] = ((t == 0 && hl == 0) ? z4 : acc[h][m]) + (float)w[h] * (float)(hl ? bl[t & 1][h] : bh[t & 1][h])[m];
+#else
                 acc[h][m] = MFMA_F16(w, hl ? bl[t & 1][h] : bh[t & 1][h], (t == 0 && hl == 0) ? z4 : acc[h][m], 0, 0, 0);
+#endif
             issue(std::integral_constant<int, S + QC3_PD>{});
             if constexpr (S % (2 * NT0) == 3 && t + 1 < KP) {  // the next slice's inputs, between MFMAs
                 decode(std::integral_constant<int, t + 1>{}, bh[(t + 1) & 1], bl[(t + 1) & 1]);
