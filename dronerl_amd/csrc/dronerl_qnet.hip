@@ -1298,6 +1298,9 @@ __global__ void __launch_bounds__(64 * QN_CODE2_WAVES) drl_qnet_act_code3_kernel
     // costs a vmcnt(0) while any DMA is in flight: slices 0 and 1 go first, then the codes, one
     // vmcnt(0) for all of them, then the other slices (they land while slices 0-1 compute).
     auto dma = [&](int t) __attribute__((always_inline)) {
+#ifdef DRL_DIAG_QC3_NOSTAGE  // timing diagnostic (wrong results): no weight staging
+        return;
+#endif
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int v0 = h * FLO + (wave * KP + t) * 64;
@@ -1558,6 +1561,345 @@ __global__ void __launch_bounds__(64 * QN_CODE2_WAVES) drl_qnet_act_code3_kernel
     }
 }
 
+// ------------------------------------------------ act from the code, v4 ---
+// drl_qnet_act_code4_kernel: the benchmark nets (layer 0's hi + lo fragments
+// the LDS image, 8 unit tiles, two hidden layers, the second 16 * NT1 wide) at
+// ONE wave per SIMD: four waves per workgroup, one workgroup per CU, 512
+// registers per wave, four 16-env tiles (64 envs) per wave pass.
+// What the v3 kernel (two waves per SIMD, two tiles) showed (profiles/r04_act/):
+// at its 256-register cap it spilled (84 B of scratch: VMEM reloads whose
+// vmcnt waits drain every older load), a wave's layer 0 ran 18.6k cycles for
+// 5.1k cycles of MFMA issue, and the output layer + epilogue another 4.7k with
+// 16 of 64 lanes active.  Staging the 160 KB image on every CU costs about
+// nothing (tools/stage_probe: an LDS-DMA kernel staging 160 KB per CU times
+// like an empty launch), so the layout of the image stays and the work per
+// fragment read doubles instead:
+//  * each layer-0 fragment read (ds_read_b128, 1 KB) feeds four MFMAs (one per
+//    tile); the accumulators of the four tiles (128 registers) and the later
+//    layers' weights (output layer and biases: resident from the kernel start;
+//    layer 1: double-buffered per K-slice, the first issued during layer 0's
+//    last slice) fit without spilling;
+//  * one accumulator per (tile, unit tile) as in v3 (lo weights times
+//    x * 2^-11, exact in fp16), the slice's inputs decoded one tile at a time
+//    between the MFMAs of the previous slice (steps 2, 5, 8, 11), the lo inputs
+//    once per slice;
+//  * the epilogue runs once per pass on all 64 lanes: lane (c, g) takes env c
+//    of tile g (its Q rows gathered with 8 shuffles per tile), so the argmax,
+//    the exploration hash and the stores are not repeated per tile on 16 lanes.
+#ifndef DRL_QC4_PD
+#define DRL_QC4_PD 6
+#endif
+constexpr int QC4_PD = DRL_QC4_PD;  // layer-0 fragment reads in flight per wave (ring of QC4_PD + 2)
+constexpr int QC4_WAVES = 4;
+#ifndef DRL_QC4_L2AT
+#define DRL_QC4_L2AT 1  // layer-1 K-slice during which the output layer's weights are loaded
+#endif
+
+template <int NT0, int WN, int NT1>
+__global__ void __launch_bounds__(64 * QC4_WAVES) __attribute__((amdgpu_waves_per_eu(1, 1)))
+drl_qnet_act_code4_kernel(QnetArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint4 wl[];
+    constexpr int TP = 4, NW = QC4_WAVES;
+    constexpr int CPG = lay::code_cpg(WN), CPG8 = lay::code_cpg8(WN);
+    constexpr int NV = CPG8 / 8;                 // 16-B code vectors per lane group
+    constexpr int NB = 5 * CPG;                  // slots of the 0/1 channels
+    constexpr int KP = lay::code_kt(WN);         // layer 0's K-slices
+    constexpr int KT1 = NT0 / 2, KT2 = NT1 / 2;  // K-slices of layer 1 and of the output layer
+    constexpr int SPS = 2 * NT0;                 // steps (fragment reads) per slice: hi m = 0.., then lo m = 0..
+    constexpr int STEPS = KP * SPS;
+    constexpr int PD = QC4_PD, RS = PD + 2;
+    constexpr int FLO = NT0 * KP * 64;           // uint4 offset of the lo fragments (lo0_lds layout)
+    static_assert(8 * KP > 6 * CPG, "no padding slot for layer 0's bias");
+    static_assert(2 * FLO * 16 <= 160 * 1024, "layer 0 must fit the LDS");
+    static_assert(NT0 == 2 * NW, "wave w stages unit tiles 2w and 2w + 1");
+    static_assert(SPS >= 12, "the four tiles' decodes sit at steps 2, 5, 8, 11 of a slice");
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int c = lane & 15, g = lane >> 4;
+    const int64_t ntiles = (a.E + 15) / 16;
+    const int64_t ngroups = (ntiles + TP - 1) / TP;
+    const int64_t gstride = (int64_t)gridDim.x * NW;
+    constexpr float kLo = 1.0f / 2048.0f;
+    const uint4* const code = reinterpret_cast<const uint4*>(a.obs);
+    auto load_codes = [&](int64_t tile, uint32_t (&dst)[4 * NV]) __attribute__((always_inline)) {
+        const int64_t env = min(tile * 16 + c, a.E - 1);
+        const uint4* src = code + env * (4 * NV) + g * NV;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const uint4 q = src[v];
+            dst[4 * v + 0] = q.x;
+            dst[4 * v + 1] = q.y;
+            dst[4 * v + 2] = q.z;
+            dst[4 * v + 3] = q.w;
+        }
+    };
+    const int64_t grp0 = (int64_t)blockIdx.x * NW + wave;
+#ifdef DRL_QC_STAMPS
+    const uint64_t t_entry = __builtin_amdgcn_s_memtime();
+#endif
+    const auto pbuf = __builtin_amdgcn_make_buffer_rsrc((void*)a.packed, 0, a.total_bytes, 0x00020000);
+    const int lane16 = lane * 16;
+    auto frag_ld = [&](int frag_u4) __attribute__((always_inline)) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(pbuf, lane16, frag_u4 * 16, 0);
+        uint4 r;
+        __builtin_memcpy(&r, &v, 16);
+        return r;
+    };
+    auto bias4 = [&](int off) __attribute__((always_inline)) {
+        f32x4 r;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(pbuf, 16 * g, a.bias_vec * 16 + off * 4, 0);
+        __builtin_memcpy(&r, &v, 16);
+        return r;
+    };
+    // the output layer's fragments and biases (loaded during layer 1)
+    auto ld2 = [&](uint4 (&f2h)[KT2], uint4 (&f2l)[KT2], f32x4 (&b1)[KT2][2], f32x4& bq) __attribute__((always_inline)) {
+        const int fl = a.frag_off[2], flo = a.frag_lo_off[2], bo = a.bias_off[1];
+#pragma unroll
+        for (int u = 0; u < KT2; ++u) {
+            f2h[u] = frag_ld(fl + u * 64);
+            f2l[u] = frag_ld(flo + u * 64);
+            b1[u][0] = bias4(bo + 32 * u);
+            b1[u][1] = bias4(bo + 32 * u + 16);
+        }
+        bq = bias4(a.bias_off[2]);
+    };
+    // staging in slice order: wave w copies unit tiles 2w and 2w + 1, hi and lo (4 fragments per slice).
+    // Slices < KE go before the codes; one forced vmcnt(0) covers them, the codes and the loads above
+    // (the compiler would wait for an LDS-DMA with vmcnt(0) anyway), then the other slices.
+    auto dma = [&](int t) __attribute__((always_inline)) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int v0 = h * FLO + ((2 * wave + u) * KP + t) * 64;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(a.packed + v0 + lane),
+                                                 (__attribute__((address_space(3))) void*)(wl + v0), 16, 0, 0);
+            }
+    };
+    constexpr int KE = KP < 2 ? KP : 2;
+#pragma unroll
+    for (int t = 0; t < KE; ++t) dma(t);
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t cw[TP][4 * NV];
+#pragma unroll
+    for (int h = 0; h < TP; ++h) load_codes(TP * (grp0 < ngroups ? grp0 : 0) + h, cw[h]);
+#pragma unroll
+    for (int h = 0; h < TP; ++h)
+#pragma unroll
+        for (int i = 0; i < 4 * NV; ++i) asm volatile("s_waitcnt vmcnt(0)" : "+v"(cw[h][i]));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = KE; t < KP; ++t) dma(t);
+    __builtin_amdgcn_sched_barrier(0);
+    auto slice_ready = [&](auto t_c) __attribute__((always_inline)) {
+        constexpr int T = decltype(t_c)::value;
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(T < KE ? 0 : 4 * (KP - 1 - T)) : "memory");
+    };
+    bool bad = false;
+    const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+    const uint32_t base[3] = {(uint32_t)lane16, (uint32_t)lane16 + 65536u, (uint32_t)lane16 + 131072u};
+    // slice t's B operand of tile h from the codes (x exact in fp16: 0, 1 or a charge <= 100); the code rows'
+    // padding cells are zero (write_obs_wave), and so are their weights
+    auto decode = [&](auto t_c, int h, f16x8& bh) __attribute__((always_inline)) {
+        constexpr int t = decltype(t_c)::value;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int sl = 8 * t + j;
+            const int l = sl < NB ? sl / 5 : sl - NB;
+            const int ch = sl < NB ? (sl % 5 < 4 ? sl % 5 : 5) : 4;
+            float x = (sl == 6 * CPG && g == 0) ? 1.0f : 0.0f;  // the bias slot (drl_qnet_pack)
+            if (sl < 6 * CPG) x = code_channel((cw[h][l >> 1] >> (16 * (l & 1))) & 0xffffu, ch);
+            bh[j] = (_Float16)x;
+        }
+    };
+
+    bool first = true;
+    if (grp0 >= ngroups) {  // no group: still take part in the staging barriers
+        qc3_for<0, KP>([&](auto t_c) { slice_ready(t_c); });
+    }
+    for (int64_t grp = grp0; grp < ngroups; grp += gstride) {
+#ifdef DRL_QC_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t ts0 = __builtin_amdgcn_s_memtime();
+#endif
+        const int64_t ngrp = grp + gstride;
+        f32x4 acc[TP][NT0];
+        f16x8 bh[2][TP], bl[TP];  // [slice parity][tile]
+        q3u4 ring[RS];
+#pragma unroll
+        for (int h = 0; h < TP; ++h) decode(std::integral_constant<int, 0>{}, h, bh[0][h]);
+        uint4 f1[2][2][NT1];  // layer 1's fragments: [buffer][hi / lo][unit tile]
+        auto ld1 = [&](int t, int b) __attribute__((always_inline)) {
+            const int fl = a.frag_off[1], flo = a.frag_lo_off[1];
+#pragma unroll
+            for (int m = 0; m < NT1; ++m) {
+                f1[b][0][m] = frag_ld(fl + (m * KT1 + t) * 64);
+                f1[b][1][m] = frag_ld(flo + (m * KT1 + t) * 64);
+            }
+        };
+        // ---- layer 0: STEPS fragment reads, PD ahead of their MFMAs
+        auto issue = [&](auto s_c) __attribute__((always_inline)) {
+            constexpr int S = decltype(s_c)::value;
+            if constexpr (S < STEPS) {
+                constexpr int t = S / SPS, hl = (S / NT0) & 1, m = S % NT0;
+                if constexpr (S % SPS == 0) {
+                    if (first) slice_ready(std::integral_constant<int, t>{});
+                }
+                qc3_read<(hl * FLO + (m * KP + t) * 64) * 16>(ring[S % RS], base);
+            }
+        };
+        qc3_for<0, PD>([&](auto s_c) { issue(s_c); });
+        qc3_for<0, STEPS>([&](auto s_c) {
+            constexpr int S = decltype(s_c)::value;
+            constexpr int t = S / SPS, st = S % SPS, hl = (S / NT0) & 1, m = S % NT0;
+            constexpr int after = (S + PD - 1 < STEPS ? S + PD - 1 : STEPS - 1) - S;
+            if constexpr (st == NT0) {  // the lo inputs of this slice
+#pragma unroll
+                for (int h = 0; h < TP; ++h) bl[h] = bh[t & 1][h] * (_Float16)kLo;
+            }
+            qc3_wait<after>(ring[S % RS]);
+            const f16x8 w = q3_f16(ring[S % RS]);
+#pragma unroll
+            for (int h = 0; h < TP; ++h)
+                acc[h][m] = MFMA_F16(w, hl ? bl[h] : bh[t & 1][h], (t == 0 && hl == 0) ? z4 : acc[h][m], 0, 0, 0);
+            issue(std::integral_constant<int, S + PD>{});
+            if constexpr (t + 1 < KP && (st == 2 || st == 5 || st == 8 || st == 11)) {
+                constexpr int h = (st - 2) / 3;
+                decode(std::integral_constant<int, t + 1>{}, h, bh[(t + 1) & 1][h]);
+            }
+            if constexpr (t + 1 == KP && st == 3) {  // the codes are dead: the next group's in flight
+#pragma unroll
+                for (int h = 0; h < TP; ++h) load_codes(TP * (ngrp < ngroups ? ngrp : grp) + h, cw[h]);
+            }
+            if constexpr (t + 1 == KP && st == 6) ld1(0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        first = false;
+#ifdef DRL_QC_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t ts1 = __builtin_amdgcn_s_memtime();
+#endif
+        // ---- layer 1 (bias folded into layer 0); K-slice t's inputs split from layer 0's unit tiles 2t, 2t + 1
+        f32x4 bcc[TP][NT1], bcl[TP][NT1];
+        uint4 f2h[KT2], f2l[KT2];
+        f32x4 b1[KT2][2], bq;
+#pragma unroll
+        for (int t = 0; t < KT1; ++t) {
+            if (t + 1 < KT1) ld1(t + 1, (t + 1) & 1);
+            if (t == DRL_QC4_L2AT) ld2(f2h, f2l, b1, bq);
+            f16x8 ah[TP], al[TP];
+#pragma unroll
+            for (int h = 0; h < TP; ++h) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = fmaxf(acc[h][2 * t + (j >> 2)][j & 3], 0.0f);
+                split_f16(v, ah[h], al[h], bad);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int m = 0; m < NT1; ++m) {
+                const f16x8 wh = as_f16x8(f1[t & 1][0][m]), wo = as_f16x8(f1[t & 1][1][m]);
+#pragma unroll
+                for (int h = 0; h < TP; ++h) {
+                    bcc[h][m] = MFMA_F16(wh, ah[h], t == 0 ? z4 : bcc[h][m], 0, 0, 0);
+                    bcl[h][m] = MFMA_F16(wh, al[h], t == 0 ? z4 : bcl[h][m], 0, 0, 0);
+                    bcl[h][m] = MFMA_F16(wo, ah[h], bcl[h][m], 0, 0, 0);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#ifdef DRL_QC_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t ts2 = __builtin_amdgcn_s_memtime();
+#endif
+        // ---- the output layer
+        f32x4 qf[TP];
+#pragma unroll
+        for (int h = 0; h < TP; ++h) {
+            f16x8 ah2[KT2], al2[KT2];
+#pragma unroll
+            for (int s2 = 0; s2 < KT2; ++s2) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int m = 2 * s2 + (j >> 2), i = j & 3;
+                    v[j] = fmaxf((bcc[h][m][i] + bcl[h][m][i] * kLo) + b1[s2][j >> 2][i], 0.0f);
+                }
+                split_f16(v, ah2[s2], al2[s2], bad);
+            }
+            f32x4 qc, ql;
+#pragma unroll
+            for (int t = 0; t < KT2; ++t) {
+                const f16x8 wh = as_f16x8(f2h[t]), wo = as_f16x8(f2l[t]);
+                qc = MFMA_F16(wh, ah2[t], t == 0 ? z4 : qc, 0, 0, 0);
+                ql = MFMA_F16(wh, al2[t], t == 0 ? z4 : ql, 0, 0, 0);
+                ql = MFMA_F16(wo, ah2[t], ql, 0, 0, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) qf[h][i] = (qc[i] + ql[i] * kLo) + bq[i];
+        }
+        // ---- epsilon-greedy act, one env per lane: lane (c, g) takes env c of tile g, whose Q rows 4g' + i
+        // sit in lane (c, g') register i of qf[g]
+        float q[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int src = c + 16 * (i >> 2);
+            float v = __shfl(qf[0][i & 3], src);
+#pragma unroll
+            for (int h = 1; h < TP; ++h) {
+                const float u = __shfl(qf[h][i & 3], src);
+                v = g == h ? u : v;
+            }
+            q[i] = v;
+        }
+        {
+            const int64_t env = (TP * grp + g) * 16 + c;
+            if (env < a.E) {
+                int best = 0;
+                for (int i = 1; i < a.n_actions; ++i) best = q[i] > q[best] ? i : best;
+                const uint64_t ge = (uint64_t)(a.env_offset + env);
+                const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (ge << 8) ^ 0xa5ull));
+                const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
+                const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
+                a.actions[env * a.action_stride] = (u < a.epsilon) ? rnd : best;
+#ifndef DRL_QC_STAMPS
+                if (a.q)
+                    for (int i = 0; i < a.n_actions; ++i) a.q[env * a.n_actions + i] = q[i];
+#endif
+            }
+        }
+#ifdef DRL_QC_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t ts3 = __builtin_amdgcn_s_memtime();
+        if (lane == 0 && a.q) {
+            uint32_t* st = reinterpret_cast<uint32_t*>(a.q) + grp * 5;
+            st[0] = (uint32_t)(ts1 - ts0);
+            st[1] = (uint32_t)(ts2 - ts1);
+            st[2] = (uint32_t)(ts3 - ts2);
+            st[3] = (uint32_t)(ts0 - t_entry);
+            st[4] = (uint32_t)(ts3 - t_entry);
+        }
+#endif
+    }
+    bad |= lane == 0 && reinterpret_cast<const int32_t*>(a.packed + a.status_vec)[0] != 0;  // pack range flag
+    if (__ballot(bad) && lane == 0 && a.err) atomicOr(a.err, DRL_ERR_QNET_RANGE);
+    if (a.synth_n > 1) {  // as in drl_qnet_act_kernel (TP 16-env tiles per group)
+        const uint32_t nd = (uint32_t)a.synth_n - 1u;
+        const uint32_t per = (uint32_t)(TP * 16) * nd;
+        for (int64_t gg = grp0; gg < ngroups; gg += gstride) {
+            for (uint32_t k = (uint32_t)lane; k < per; k += 64u) {
+                const uint32_t el = k / nd;
+                const int64_t env = TP * 16 * gg + el;
+                const uint64_t drone = 1u + (k - el * nd);
+                if (env < a.E) {
+                    const uint64_t ctr = (a.synth_step << 40) ^ ((uint64_t)(a.env_offset + env) << 8) ^ drone;
+                    const uint64_t hh = qn_splitmix64(a.synth_seed ^ qn_splitmix64(ctr));
+                    a.actions[env * a.action_stride + (int64_t)drone] = (int32_t)(((hh >> 32) * 5ull) >> 32);
+                }
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------ add_many ---
 // Transition i of the batch goes to slot (cursor + i) % capacity; with more
 // transitions than slots only the last `capacity` are written (what a
@@ -1665,16 +2007,24 @@ hipError_t launch_qnet_act_code(const QnetArgs& a, int window, int num_cus, hipS
 #define QN_CODE_LAUNCH(NT, W)                                                                                   \
     if (a.lo0_lds) hipLaunchKernelGGL((drl_qnet_act_code_kernel<NT, true, W, 0>), grid, block, lds, s, a);     \
     else hipLaunchKernelGGL((drl_qnet_act_code_kernel<NT, false, W, 0>), grid, block, lds, s, a)
-    static const bool v3 = [] {  // DRL_QN_CODE3=0: the round-3 kernel (A/B knob)
-        const char* e = getenv("DRL_QN_CODE3");
-        return !(e && e[0] == '0');
+    static const int ver = [] {  // DRL_QN_CODE=2|3: an earlier kernel (A/B knob; DRL_QN_CODE3=0 = 2)
+        const char* e = getenv("DRL_QN_CODE");
+        const char* e3 = getenv("DRL_QN_CODE3");
+        if (e && (e[0] == '2' || e[0] == '3')) return e[0] - '0';
+        return (e3 && e3[0] == '0') ? 2 : 4;
     }();
+    const bool v3 = ver >= 3;
+    const int64_t ng4 = (nt + 3) / 4;  // drl_qnet_act_code4_kernel: four tiles per wave, four waves per workgroup
+    int64_t nb4 = (ng4 + QC4_WAVES - 1) / QC4_WAVES;
+    if (nb4 > num_cus) nb4 = num_cus;
+    const dim3 grid4((unsigned)nb4), block4(64 * QC4_WAVES);
     // drl_qnet_act_code3_kernel: the lo0_lds layout (layer 0's hi then lo fragments from offset 0) with
     // 8 waves of 128 units and a window whose layer 0 fits the LDS (5x5, 7x7)
     const bool c3ok = v3 && a.lo0_lds && a.frag_off[0] == 0 && window <= 7 &&
                       a.frag_lo_off[0] == 8 * lay::code_kt(window) * 64 && blocks_ok(a);
 #define QN_CODE_SPEC(W)                                                                                         \
-    if (c3ok && W <= 7) hipLaunchKernelGGL((drl_qnet_act_code3_kernel<8, (W <= 7 ? W : 7), 4>), grid2, block2, lds, s, a); \
+    if (c3ok && W <= 7 && ver == 4) hipLaunchKernelGGL((drl_qnet_act_code4_kernel<8, (W <= 7 ? W : 7), 4>), grid4, block4, lds, s, a); \
+    else if (c3ok && W <= 7) hipLaunchKernelGGL((drl_qnet_act_code3_kernel<8, (W <= 7 ? W : 7), 4>), grid2, block2, lds, s, a); \
     else if (a.lo0_lds) hipLaunchKernelGGL((drl_qnet_act_code2_kernel<8, true, W, 4>), grid2, block2, lds, s, a);   \
     else hipLaunchKernelGGL((drl_qnet_act_code2_kernel<8, false, W, 4>), grid2, block2, lds, s, a)
     const bool spec = a.n_hidden == 2 && a.nt[0] == 8 && a.nt[1] == 4;  // 128 -> 64 hidden

@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--input", default="obs", choices=["obs", "code"], help="code: drl_qnet_act_code (f32)")
     ap.add_argument("--synth", action="store_true", help="also write drones 1..7's synthetic actions (act_synth)")
     ap.add_argument("--stamps", action="store_true", help="library built with -DDRL_QC_STAMPS: phase cycles")
+    ap.add_argument("--group", type=int, default=64,
+                    help="envs per wave pass of the stamped code act (64: v4 kernel, 32: DRL_QN_CODE=2|3)")
     ap.add_argument("--flush", action="store_true",
                     help="overwrite 256 MB between launches (cold L2/MALL, as after a step) and time each launch")
     args = ap.parse_args()
@@ -71,7 +73,8 @@ def main():
         q = torch.zeros((E, 5), device="cuda")
         net.act(flat, 0.1, actions=a, q_out=q)
         torch.cuda.synchronize()
-        rows = (E + 31) // 32 if args.input == "code" and args.hidden in ("128,64", "128,32") else (E + 15) // 16
+        gr = args.group if args.input == "code" and args.hidden in ("128,64", "128,32") else 16
+        rows = (E + gr - 1) // gr
         st = q.view(torch.int32).cpu().numpy().astype("int64").reshape(-1)[: 5 * rows].reshape(rows, 5)
         import numpy as np
         for i, name in enumerate(("layer0", "hidden" if rows == (E + 15) // 16 else "layer1",
