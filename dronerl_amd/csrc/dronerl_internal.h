@@ -109,6 +109,14 @@ constexpr int code_cpg8(int W) { return (code_cpg(W) + 7) / 8 * 8; }
 constexpr int code_bytes(int W) { return 4 * code_cpg8(W) * 2; }
 // layer 0's K-slices of a code-input net: 6 channels x code_cpg slots per lane group, 8 per slice, padded to the
 // act kernels' slice ring
+// layer 0's K order of a policy-code net, per lane group (drl_qnet_pack and every code act): slot sl <
+// 6 * cpg holds observation channel code_slot_ch of the group's cell code_slot_cell.  The cell pairs (2p, 2p + 1),
+// one dword of the code row each, take 12 consecutive slots, channel-major (slots 12p + 2ch, 12p + 2ch + 1), so
+// one dword of the MFMA B operand is one channel of one code dword (drl_qnet_act_code4_kernel builds it with
+// packed 16-bit operations); an odd count's last cell takes the 6 slots after the pairs; slot 6 * cpg carries
+// the bias (lane group 0) and the slots after it are zero.
+constexpr int code_slot_cell(int cpg, int sl) { return sl < 6 * (cpg & ~1) ? 2 * (sl / 12) + (sl & 1) : cpg - 1; }
+constexpr int code_slot_ch(int cpg, int sl) { return sl < 6 * (cpg & ~1) ? (sl % 12) / 2 : sl - 6 * (cpg - 1); }
 constexpr int code_kt(int W) { return ((6 * code_cpg(W) + 7) / 8 + DRL_QN_RING - 1) / DRL_QN_RING * DRL_QN_RING; }
 constexpr int qn_ring = DRL_QN_RING;    // act kernel: K-slices in flight per wave (layer-0 slices padded to a multiple)
 constexpr int qn_waves = DRL_QN_WAVES;  // act kernel: waves per workgroup (one workgroup per CU)

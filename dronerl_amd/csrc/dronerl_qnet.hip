@@ -61,8 +61,7 @@ __global__ void drl_qnet_pack_kernel(QnetPack p) {
         int k = 32 * t + frag_k(g, j);
         if (l == 0 && p.code_w > 0) {  // the policy code's K order (drl_qnet_act_code_kernel)
             const int cpg = lay::code_cpg(p.code_w), cells = p.code_w * p.code_w, sl = 8 * t + j;
-            const int lc = sl < 5 * cpg ? sl / 5 : sl - 5 * cpg;
-            const int ch = sl < 5 * cpg ? (sl % 5 < 4 ? sl % 5 : 5) : 4;
+            const int lc = lay::code_slot_cell(cpg, sl), ch = lay::code_slot_ch(cpg, sl);
             const bool ok = sl < 6 * cpg && lc < cpg && g * cpg + lc < cells;
             k = ok ? (g * cpg + lc) * 6 + ch : p.in[l];  // (in[l]: a zero weight)
             // the first padding slot of lane group 0 carries the bias (input 1)
@@ -612,7 +611,6 @@ __global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(Qn
     extern __shared__ __attribute__((aligned(16))) uint4 wl[];
     constexpr int CPG = lay::code_cpg(WN), CPG8 = lay::code_cpg8(WN), CELLS = WN * WN;
     constexpr int NV = CPG8 / 8;                 // 16-B code vectors per lane group
-    constexpr int NB = 5 * CPG;                  // slots of the 0/1 channels
     constexpr int KP = lay::code_kt(WN);         // layer 0's K-slices (host: QnetLayout::kt[0])
     static_assert(8 * KP > 6 * CPG, "no padding slot for layer 0's bias");
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -706,8 +704,7 @@ __global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(Qn
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int sl = 8 * t + j;  // compile-time slot
-                const int l = sl < NB ? sl / 5 : sl - NB;
-                const int ch = sl < NB ? (sl % 5 < 4 ? sl % 5 : 5) : 4;
+                const int l = lay::code_slot_cell(CPG, sl), ch = lay::code_slot_ch(CPG, sl);
                 float x = (sl == 6 * CPG && g == 0) ? 1.0f : 0.0f;  // the bias slot (drl_qnet_pack)
                 if (sl < 6 * CPG) {
                     const uint32_t cd = (cs[l >> 1] >> (16 * (l & 1))) & 0xffffu;
@@ -937,7 +934,6 @@ __global__ void __launch_bounds__(64 * QN_CODE2_WAVES) drl_qnet_act_code2_kernel
     constexpr int TP = 2;
     constexpr int CPG = lay::code_cpg(WN), CPG8 = lay::code_cpg8(WN), CELLS = WN * WN;
     constexpr int NV = CPG8 / 8;                 // 16-B code vectors per lane group
-    constexpr int NB = 5 * CPG;                  // slots of the 0/1 channels
     constexpr int KP = lay::code_kt(WN);         // layer 0's K-slices
     constexpr int KT1 = NT0 / 2, KT2 = NT1 / 2;  // K-slices of layer 1 and of the output layer
     static_assert(8 * KP > 6 * CPG, "no padding slot for layer 0's bias");
@@ -1024,8 +1020,7 @@ __global__ void __launch_bounds__(64 * QN_CODE2_WAVES) drl_qnet_act_code2_kernel
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int sl = 8 * t + j;  // compile-time slot
-                    const int l = sl < NB ? sl / 5 : sl - NB;
-                    const int ch = sl < NB ? (sl % 5 < 4 ? sl % 5 : 5) : 4;
+                    const int l = lay::code_slot_cell(CPG, sl), ch = lay::code_slot_ch(CPG, sl);
                     float x = (sl == 6 * CPG && g == 0) ? 1.0f : 0.0f;  // the bias slot (drl_qnet_pack)
                     if (sl < 6 * CPG) {
                         const uint32_t cd = (cw[h][l >> 1] >> (16 * (l & 1))) & 0xffffu;
@@ -1259,7 +1254,6 @@ __global__ void __launch_bounds__(64 * QN_CODE2_WAVES) drl_qnet_act_code3_kernel
     constexpr int TP = 2;
     constexpr int CPG = lay::code_cpg(WN), CPG8 = lay::code_cpg8(WN), CELLS = WN * WN;
     constexpr int NV = CPG8 / 8;                 // 16-B code vectors per lane group
-    constexpr int NB = 5 * CPG;                  // slots of the 0/1 channels
     constexpr int KP = lay::code_kt(WN);         // layer 0's K-slices
     constexpr int KT1 = NT0 / 2, KT2 = NT1 / 2;  // K-slices of layer 1 and of the output layer
     constexpr int STEPS = KP * 2 * NT0;          // layer-0 fragment reads per group: slice-major, hi then lo
@@ -1354,8 +1348,7 @@ __global__ void __launch_bounds__(64 * QN_CODE2_WAVES) drl_qnet_act_code3_kernel
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int sl = 8 * t + j;  // compile-time slot
-                const int l = sl < NB ? sl / 5 : sl - NB;
-                const int ch = sl < NB ? (sl % 5 < 4 ? sl % 5 : 5) : 4;
+                const int l = lay::code_slot_cell(CPG, sl), ch = lay::code_slot_ch(CPG, sl);
                 float x = (sl == 6 * CPG && g == 0) ? 1.0f : 0.0f;  // the bias slot (drl_qnet_pack)
                 if (sl < 6 * CPG) {
                     const uint32_t cd = (cw[h][l >> 1] >> (16 * (l & 1))) & 0xffffu;
@@ -1566,34 +1559,129 @@ __global__ void __launch_bounds__(64 * QN_CODE2_WAVES) drl_qnet_act_code3_kernel
 // the LDS image, 8 unit tiles, two hidden layers, the second 16 * NT1 wide) at
 // ONE wave per SIMD: four waves per workgroup, one workgroup per CU, 512
 // registers per wave, four 16-env tiles (64 envs) per wave pass.
-// What the v3 kernel (two waves per SIMD, two tiles) showed (profiles/r04_act/):
-// at its 256-register cap it spilled (84 B of scratch: VMEM reloads whose
-// vmcnt waits drain every older load), a wave's layer 0 ran 18.6k cycles for
-// 5.1k cycles of MFMA issue, and the output layer + epilogue another 4.7k with
-// 16 of 64 lanes active.  Staging the 160 KB image on every CU costs about
+// What the v3 kernel (two waves per SIMD, two tiles) and the first v4 showed
+// (profiles/r04_act/): staging the 160 KB image on every CU costs about
 // nothing (tools/stage_probe: an LDS-DMA kernel staging 160 KB per CU times
-// like an empty launch), so the layout of the image stays and the work per
-// fragment read doubles instead:
-//  * each layer-0 fragment read (ds_read_b128, 1 KB) feeds four MFMAs (one per
-//    tile); the accumulators of the four tiles (128 registers) and the later
-//    layers' weights (output layer and biases: resident from the kernel start;
-//    layer 1: double-buffered per K-slice, the first issued during layer 0's
-//    last slice) fit without spilling;
-//  * one accumulator per (tile, unit tile) as in v3 (lo weights times
-//    x * 2^-11, exact in fp16), the slice's inputs decoded one tile at a time
-//    between the MFMAs of the previous slice (steps 2, 5, 8, 11), the lo inputs
-//    once per slice;
-//  * the epilogue runs once per pass on all 64 lanes: lane (c, g) takes env c
-//    of tile g (its Q rows gathered with 8 shuffles per tile), so the argmax,
-//    the exploration hash and the stores are not repeated per tile on 16 lanes.
+// like an empty launch); the phases were VALU-bound, not MFMA- or LDS-bound:
+// per 64-env pass, layer 0 issued 1,346 VALU beside its 640 MFMAs (the
+// per-slot channel decode, ~6 instructions per K slot), layer 1 892 beside 192
+// (the f32 -> fp16 hi/lo split), the output layer and the epilogue 1,127 (the
+// split again, the exploration hash and per-tile epilogues on 16 of 64 lanes).
+// With one wave per SIMD an MFMA leaves room for about two VALU instructions,
+// so this kernel
+//  * decodes the code two slots per instruction: the K order (lay::code_slot_*)
+//    makes a dword of the B operand one channel of one code dword (two cells),
+//    computed with packed 16-bit operations: the object channels by one
+//    v_perm_b32 lookup each (fp16 1.0's high byte 0x3C in a byte table indexed
+//    by the object), the drone flag by a min and a multiply, the charge by a
+//    saturating subtract and the fp16 magic 1024 + n; one dword per step (four
+//    MFMAs), the lo inputs (x * 2^-11, exact) beside it;
+//  * splits with v_cvt_pk_f16_f32 and checks the range through a running
+//    maximum (one compare per pass instead of one per value), the next K
+//    slice's split beside the current slice's MFMAs;
+//  * computes the exploration draw (two splitmix64) at the start of the pass
+//    and runs the argmax once per pass on all 64 lanes: lane (c, g) takes env c
+//    of tile g, its Q rows gathered with shuffles.
 #ifndef DRL_QC4_PD
 #define DRL_QC4_PD 6
 #endif
 constexpr int QC4_PD = DRL_QC4_PD;  // layer-0 fragment reads in flight per wave (ring of QC4_PD + 2)
 constexpr int QC4_WAVES = 4;
-#ifndef DRL_QC4_L2AT
-#define DRL_QC4_L2AT 1  // layer-1 K-slice during which the output layer's weights are loaded
-#endif
+
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+template <class T, class F>
+__device__ __forceinline__ T qc4_as(const F v) {
+    static_assert(sizeof(T) == sizeof(F), "bit cast");
+    T r;
+    __builtin_memcpy(&r, &v, sizeof(T));
+    return r;
+}
+
+// object channels: v_perm_b32 byte tables (bytes 0-3 from the second operand, 4-7 from the first) with
+// 0x3C at the object's code; selector: byte 1 (3) = the object of the dword's low (high) cell, bytes 0 and 2
+// = 0x0C (a zero byte)
+__device__ __forceinline__ uint32_t qc4_obj_sel(uint32_t w) { return ((w & 0x00070007u) << 8) | 0x000C000Cu; }
+template <int OBJ>
+__device__ __forceinline__ uint32_t qc4_obj(uint32_t sel) {
+    constexpr uint32_t hi = OBJ >= 4 ? 0x3Cu << (8 * (OBJ - 4)) : 0u, lo = OBJ < 4 ? 0x3Cu << (8 * OBJ) : 0u;
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+// channel CH (wrappers.py:10-31, code_channel) of both cells of code dword w, as two fp16 (the charge as the
+// integer c: the packed weights carry the 1/100)
+template <int CH>
+__device__ __forceinline__ uint32_t qc4_channel(uint32_t w) {
+    if constexpr (CH == 0) {  // a drone: air != 0, i.e. (charge + 1) != 0 in bits 3-9
+        const u16x2 m = __builtin_elementwise_min(qc4_as<u16x2>(w & 0x03F803F8u), (u16x2){8, 8});
+        return qc4_as<uint32_t>(m * (u16x2){0x780, 0x780});  // 8 * 0x780 = 0x3C00
+    } else if constexpr (CH == 1) {  // a packet on the ground or carried
+        const u16x2 cr = qc4_as<u16x2>(w & 0x04000400u) * (u16x2){15, 15};  // 0x400 * 15 = 0x3C00
+        return qc4_obj<OBJ_PACKET>(qc4_obj_sel(w)) | qc4_as<uint32_t>(cr);
+    } else if constexpr (CH == 2) {
+        return qc4_obj<OBJ_DROPZONE>(qc4_obj_sel(w));
+    } else if constexpr (CH == 3) {
+        return qc4_obj<OBJ_STATION>(qc4_obj_sel(w));
+    } else if constexpr (CH == 4) {  // the charge c = (air & 0x7f) - 1 (0 without a drone), as fp16 (1024 + c) - 1024
+        const u16x2 c1 = qc4_as<u16x2>((w >> 3) & 0x007F007Fu);
+        const u16x2 c = __builtin_elementwise_sub_sat(c1, (u16x2){1, 1});
+        const f16x2 f = qc4_as<f16x2>(qc4_as<uint32_t>(c) | 0x64006400u);
+        return qc4_as<uint32_t>(f - (f16x2){(_Float16)1024.0f, (_Float16)1024.0f});
+    } else {
+        return qc4_obj<OBJ_SKYSCRAPER>(qc4_obj_sel(w));
+    }
+}
+template <int CH>
+__device__ __forceinline__ uint32_t qc4_channel_lo16(uint32_t w) {  // channel CH of the dword's low cell only
+    return qc4_channel<CH>(w & 0xffffu) & 0xffffu;
+}
+
+// B dword D (slots 2D, 2D + 1) of a lane group's K order from the code word qc4_word<CPG, D> of its
+// CPG cells (two per word)
+template <int CPG, int D>
+constexpr int qc4_word() { return D < 6 * (CPG / 2) ? D / 6 : CPG / 2; }
+template <int CPG, int D>
+__device__ __forceinline__ uint32_t qc4_bdword(const uint32_t w, bool bias_group) {
+    constexpr int NP = CPG / 2;  // cell pairs
+    if constexpr (D < 6 * NP) {
+        return qc4_channel<D % 6>(w);
+    } else if constexpr (D < 3 * CPG) {  // the odd count's last cell (the low half of its code word): two channels
+        constexpr int ch = 2 * (D - 6 * NP);
+        return qc4_channel_lo16<ch>(w) | (qc4_channel_lo16<ch + 1>(w) << 16);
+    } else if constexpr (D == 3 * CPG) {  // slot 6 * CPG: the bias (input 1.0 in lane group 0)
+        return bias_group ? 0x3C00u : 0u;
+    } else {
+        return 0u;
+    }
+}
+
+// ReLU of an f32 as an integer max on its bits (negative floats are negative ints: no NaN canonicalisation, one
+// instruction); the split of 8 ReLU'd activations into fp16 hi = fp16(r) (v_cvt_pk_f16_f32) and lo =
+// fp16((r - hi) * 2^11) (v_fma_mix{lo,hi}_f16 on hi and r * 2^11: one rounding of the exact difference), and the
+// running maximum of the activations' bits (non-negative floats order as unsigned ints) for the range flag
+__device__ __forceinline__ float qc4_relu(float v) {
+    return __builtin_bit_cast(float, __builtin_elementwise_max(__builtin_bit_cast(int32_t, v), 0));
+}
+__device__ __forceinline__ void qc4_split(const float (&r)[8], f16x8& hi, f16x8& lo, uint32_t& mx) {
+    const float m2k = -2048.0f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float a = r[2 * k], b = r[2 * k + 1];
+        const f16x2 h = {(_Float16)a, (_Float16)b};
+        const uint32_t hw = qc4_as<uint32_t>(h);
+        uint32_t lw;
+        asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=&v"(lw) : "v"(hw), "v"(m2k), "v"(a * 2048.0f));
+        asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+            : "+v"(lw) : "v"(hw), "v"(m2k), "v"(b * 2048.0f));
+        const f16x2 l = qc4_as<f16x2>(lw);
+        hi[2 * k] = h[0];
+        hi[2 * k + 1] = h[1];
+        lo[2 * k] = l[0];
+        lo[2 * k + 1] = l[1];
+        mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(__builtin_bit_cast(uint32_t, a),
+                                                                     __builtin_bit_cast(uint32_t, b)));
+    }
+}
 
 template <int NT0, int WN, int NT1>
 __global__ void __launch_bounds__(64 * QC4_WAVES) __attribute__((amdgpu_waves_per_eu(1, 1)))
@@ -1602,7 +1690,6 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
     constexpr int TP = 4, NW = QC4_WAVES;
     constexpr int CPG = lay::code_cpg(WN), CPG8 = lay::code_cpg8(WN);
     constexpr int NV = CPG8 / 8;                 // 16-B code vectors per lane group
-    constexpr int NB = 5 * CPG;                  // slots of the 0/1 channels
     constexpr int KP = lay::code_kt(WN);         // layer 0's K-slices
     constexpr int KT1 = NT0 / 2, KT2 = NT1 / 2;  // K-slices of layer 1 and of the output layer
     constexpr int SPS = 2 * NT0;                 // steps (fragment reads) per slice: hi m = 0.., then lo m = 0..
@@ -1612,25 +1699,26 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
     static_assert(8 * KP > 6 * CPG, "no padding slot for layer 0's bias");
     static_assert(2 * FLO * 16 <= 160 * 1024, "layer 0 must fit the LDS");
     static_assert(NT0 == 2 * NW, "wave w stages unit tiles 2w and 2w + 1");
-    static_assert(SPS >= 12, "the four tiles' decodes sit at steps 2, 5, 8, 11 of a slice");
+    static_assert(SPS == 4 * TP, "one B dword of one tile per step: 4 dwords x TP tiles per slice");
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int c = lane & 15, g = lane >> 4;
     const int64_t ntiles = (a.E + 15) / 16;
     const int64_t ngroups = (ntiles + TP - 1) / TP;
     const int64_t gstride = (int64_t)gridDim.x * NW;
     constexpr float kLo = 1.0f / 2048.0f;
+    const f16x2 kLo2 = {(_Float16)kLo, (_Float16)kLo};
     const uint4* const code = reinterpret_cast<const uint4*>(a.obs);
-    auto load_codes = [&](int64_t tile, uint32_t (&dst)[4 * NV]) __attribute__((always_inline)) {
+    auto load_vec = [&](int64_t tile, int v, uint32_t (&dst)[4 * NV]) __attribute__((always_inline)) {
         const int64_t env = min(tile * 16 + c, a.E - 1);
-        const uint4* src = code + env * (4 * NV) + g * NV;
+        const uint4 q = code[env * (4 * NV) + g * NV + v];
+        dst[4 * v + 0] = q.x;
+        dst[4 * v + 1] = q.y;
+        dst[4 * v + 2] = q.z;
+        dst[4 * v + 3] = q.w;
+    };
+    auto load_codes = [&](int64_t tile, uint32_t (&dst)[4 * NV]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            const uint4 q = src[v];
-            dst[4 * v + 0] = q.x;
-            dst[4 * v + 1] = q.y;
-            dst[4 * v + 2] = q.z;
-            dst[4 * v + 3] = q.w;
-        }
+        for (int v = 0; v < NV; ++v) load_vec(tile, v, dst);
     };
     const int64_t grp0 = (int64_t)blockIdx.x * NW + wave;
 #ifdef DRL_QC_STAMPS
@@ -1663,8 +1751,8 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
         bq = bias4(a.bias_off[2]);
     };
     // staging in slice order: wave w copies unit tiles 2w and 2w + 1, hi and lo (4 fragments per slice).
-    // Slices < KE go before the codes; one forced vmcnt(0) covers them, the codes and the loads above
-    // (the compiler would wait for an LDS-DMA with vmcnt(0) anyway), then the other slices.
+    // Slices < KE go before the codes; one forced vmcnt(0) covers them and the codes (the compiler would wait
+    // for an LDS-DMA with vmcnt(0) anyway), then the other slices.
     auto dma = [&](int t) __attribute__((always_inline)) {
 #pragma unroll
         for (int h = 0; h < 2; ++h)
@@ -1675,42 +1763,35 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
                                                  (__attribute__((address_space(3))) void*)(wl + v0), 16, 0, 0);
             }
     };
+    // issue order: every tile's first code vector (the inputs of slices 0..5 at a 7x7 window), slices 0 and 1,
+    // the other code vectors, the other slices; slice t is readable once this wave's loads up to its DMAs have
+    // landed (in-order vmcnt) and every wave's (the barrier)
     constexpr int KE = KP < 2 ? KP : 2;
+    uint32_t cw[TP][4 * NV];
+    const int64_t gl0 = grp0 < ngroups ? grp0 : 0;
+#pragma unroll
+    for (int h = 0; h < TP; ++h) load_vec(TP * gl0 + h, 0, cw[h]);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < KE; ++t) dma(t);
     __builtin_amdgcn_sched_barrier(0);
-    uint32_t cw[TP][4 * NV];
 #pragma unroll
-    for (int h = 0; h < TP; ++h) load_codes(TP * (grp0 < ngroups ? grp0 : 0) + h, cw[h]);
+    for (int v = 1; v < NV; ++v)
 #pragma unroll
-    for (int h = 0; h < TP; ++h)
-#pragma unroll
-        for (int i = 0; i < 4 * NV; ++i) asm volatile("s_waitcnt vmcnt(0)" : "+v"(cw[h][i]));
+        for (int h = 0; h < TP; ++h) load_vec(TP * gl0 + h, v, cw[h]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = KE; t < KP; ++t) dma(t);
     __builtin_amdgcn_sched_barrier(0);
     auto slice_ready = [&](auto t_c) __attribute__((always_inline)) {
         constexpr int T = decltype(t_c)::value;
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(T < KE ? 0 : 4 * (KP - 1 - T)) : "memory");
+        constexpr int N = T < KE ? 4 * (KP - KE) + TP * (NV - 1) : 4 * (KP - 1 - T);
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(N) : "memory");
     };
-    bool bad = false;
+    uint32_t mx = 0;  // bits of the largest activation split into fp16 (DRL_ERR_QNET_RANGE at >= 65520)
     const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
     const uint32_t base[3] = {(uint32_t)lane16, (uint32_t)lane16 + 65536u, (uint32_t)lane16 + 131072u};
-    // slice t's B operand of tile h from the codes (x exact in fp16: 0, 1 or a charge <= 100); the code rows'
-    // padding cells are zero (write_obs_wave), and so are their weights
-    auto decode = [&](auto t_c, int h, f16x8& bh) __attribute__((always_inline)) {
-        constexpr int t = decltype(t_c)::value;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int sl = 8 * t + j;
-            const int l = sl < NB ? sl / 5 : sl - NB;
-            const int ch = sl < NB ? (sl % 5 < 4 ? sl % 5 : 5) : 4;
-            float x = (sl == 6 * CPG && g == 0) ? 1.0f : 0.0f;  // the bias slot (drl_qnet_pack)
-            if (sl < 6 * CPG) x = code_channel((cw[h][l >> 1] >> (16 * (l & 1))) & 0xffffu, ch);
-            bh[j] = (_Float16)x;
-        }
-    };
+    const bool bias_group = g == 0;
 
     bool first = true;
     if (grp0 >= ngroups) {  // no group: still take part in the staging barriers
@@ -1722,12 +1803,31 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
         const uint64_t ts0 = __builtin_amdgcn_s_memtime();
 #endif
         const int64_t ngrp = grp + gstride;
+        const int64_t env = (TP * grp + g) * 16 + c;  // the env whose action this lane writes (tile g, column c)
         f32x4 acc[TP][NT0];
-        f16x8 bh[2][TP], bl[TP];  // [slice parity][tile]
+        uint32_t bh[2][TP][4], bl[2][TP][4];  // B operands: [slice parity][tile][dword]
         q3u4 ring[RS];
+        if (first) slice_ready(std::integral_constant<int, 0>{});  // (the codes of slice 0 too)
+        qc3_for<0, 4>([&](auto d_c) {
+            constexpr int D = decltype(d_c)::value;
 #pragma unroll
-        for (int h = 0; h < TP; ++h) decode(std::integral_constant<int, 0>{}, h, bh[0][h]);
+            for (int h = 0; h < TP; ++h) {
+                bh[0][h][D] = qc4_bdword<CPG, D>(cw[h][qc4_word<CPG, D>()], bias_group);
+                bl[0][h][D] = qc4_as<uint32_t>(qc4_as<f16x2>(bh[0][h][D]) * kLo2);
+            }
+        });
+        // the exploration draw (independent of Q): rnd when u < epsilon, else -1
+        int explore;
+        {
+            const uint64_t ge = (uint64_t)(a.env_offset + env);
+            const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (ge << 8) ^ 0xa5ull));
+            const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
+            const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
+            explore = (u < a.epsilon) ? rnd : -1;
+        }
         uint4 f1[2][2][NT1];  // layer 1's fragments: [buffer][hi / lo][unit tile]
+        uint4 f2h[KT2], f2l[KT2];  // the output layer's, and the biases
+        f32x4 b1[KT2][2], bq;
         auto ld1 = [&](int t, int b) __attribute__((always_inline)) {
             const int fl = a.frag_off[1], flo = a.frag_lo_off[1];
 #pragma unroll
@@ -1741,7 +1841,7 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
             constexpr int S = decltype(s_c)::value;
             if constexpr (S < STEPS) {
                 constexpr int t = S / SPS, hl = (S / NT0) & 1, m = S % NT0;
-                if constexpr (S % SPS == 0) {
+                if constexpr (S % SPS == 0 && t > 0) {
                     if (first) slice_ready(std::integral_constant<int, t>{});
                 }
                 qc3_read<(hl * FLO + (m * KP + t) * 64) * 16>(ring[S % RS], base);
@@ -1752,25 +1852,32 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
             constexpr int S = decltype(s_c)::value;
             constexpr int t = S / SPS, st = S % SPS, hl = (S / NT0) & 1, m = S % NT0;
             constexpr int after = (S + PD - 1 < STEPS ? S + PD - 1 : STEPS - 1) - S;
-            if constexpr (st == NT0) {  // the lo inputs of this slice
-#pragma unroll
-                for (int h = 0; h < TP; ++h) bl[h] = bh[t & 1][h] * (_Float16)kLo;
-            }
             qc3_wait<after>(ring[S % RS]);
             const f16x8 w = q3_f16(ring[S % RS]);
 #pragma unroll
-            for (int h = 0; h < TP; ++h)
-                acc[h][m] = MFMA_F16(w, hl ? bl[h] : bh[t & 1][h], (t == 0 && hl == 0) ? z4 : acc[h][m], 0, 0, 0);
+            for (int h = 0; h < TP; ++h) {
+                f16x8 x;
+                __builtin_memcpy(&x, hl ? bl[t & 1][h] : bh[t & 1][h], 16);
+                acc[h][m] = MFMA_F16(w, x, (t == 0 && hl == 0) ? z4 : acc[h][m], 0, 0, 0);
+            }
             issue(std::integral_constant<int, S + PD>{});
-            if constexpr (t + 1 < KP && (st == 2 || st == 5 || st == 8 || st == 11)) {
-                constexpr int h = (st - 2) / 3;
-                decode(std::integral_constant<int, t + 1>{}, h, bh[(t + 1) & 1][h]);
+            if constexpr (t + 1 < KP) {  // dword st % 4 of tile st / 4 of the next slice's inputs, pinned to this
+                // step (empty asm on its input and outputs) so that it issues between this step's MFMAs
+                constexpr int h = st / 4, dd = st % 4, D = 4 * (t + 1) + dd;
+                uint32_t w = cw[h][qc4_word<CPG, D>()];
+                asm volatile("" : "+v"(w));
+                uint32_t xh = qc4_bdword<CPG, D>(w, bias_group);
+                uint32_t xl = qc4_as<uint32_t>(qc4_as<f16x2>(xh) * kLo2);
+                asm volatile("" : "+v"(xh), "+v"(xl));
+                bh[(t + 1) & 1][h][dd] = xh;
+                bl[(t + 1) & 1][h][dd] = xl;
             }
             if constexpr (t + 1 == KP && st == 3) {  // the codes are dead: the next group's in flight
 #pragma unroll
                 for (int h = 0; h < TP; ++h) load_codes(TP * (ngrp < ngroups ? ngrp : grp) + h, cw[h]);
             }
             if constexpr (t + 1 == KP && st == 6) ld1(0, 0);
+            if constexpr (t + 1 == KP && st == 9) ld2(f2h, f2l, b1, bq);
             __builtin_amdgcn_sched_barrier(0);
         });
         first = false;
@@ -1778,62 +1885,69 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
         __builtin_amdgcn_sched_barrier(0);
         const uint64_t ts1 = __builtin_amdgcn_s_memtime();
 #endif
-        // ---- layer 1 (bias folded into layer 0); K-slice t's inputs split from layer 0's unit tiles 2t, 2t + 1
+        // ---- layer 1 (bias folded into layer 0); K-slice t's inputs split from layer 0's unit tiles 2t, 2t + 1,
+        // the next slice's split beside this slice's MFMAs
         f32x4 bcc[TP][NT1], bcl[TP][NT1];
-        uint4 f2h[KT2], f2l[KT2];
-        f32x4 b1[KT2][2], bq;
-#pragma unroll
-        for (int t = 0; t < KT1; ++t) {
-            if (t + 1 < KT1) ld1(t + 1, (t + 1) & 1);
-            if (t == DRL_QC4_L2AT) ld2(f2h, f2l, b1, bq);
-            f16x8 ah[TP], al[TP];
+        f16x8 ah[2][TP], al[2][TP];
+        auto split1 = [&](int t, int b) __attribute__((always_inline)) {
 #pragma unroll
             for (int h = 0; h < TP; ++h) {
                 float v[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = fmaxf(acc[h][2 * t + (j >> 2)][j & 3], 0.0f);
-                split_f16(v, ah[h], al[h], bad);
+                for (int j = 0; j < 8; ++j) v[j] = qc4_relu(acc[h][2 * t + (j >> 2)][j & 3]);
+                qc4_split(v, ah[b][h], al[b][h], mx);
             }
+        };
+        split1(0, 0);
+#pragma unroll
+        for (int t = 0; t < KT1; ++t) {
+            if (t + 1 < KT1) ld1(t + 1, (t + 1) & 1);
+
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int m = 0; m < NT1; ++m) {
                 const f16x8 wh = as_f16x8(f1[t & 1][0][m]), wo = as_f16x8(f1[t & 1][1][m]);
 #pragma unroll
                 for (int h = 0; h < TP; ++h) {
-                    bcc[h][m] = MFMA_F16(wh, ah[h], t == 0 ? z4 : bcc[h][m], 0, 0, 0);
-                    bcl[h][m] = MFMA_F16(wh, al[h], t == 0 ? z4 : bcl[h][m], 0, 0, 0);
-                    bcl[h][m] = MFMA_F16(wo, ah[h], bcl[h][m], 0, 0, 0);
+                    bcc[h][m] = MFMA_F16(wh, ah[t & 1][h], t == 0 ? b1[m >> 1][m & 1] : bcc[h][m], 0, 0, 0);
+                    bcl[h][m] = MFMA_F16(wh, al[t & 1][h], t == 0 ? z4 : bcl[h][m], 0, 0, 0);
+                    bcl[h][m] = MFMA_F16(wo, ah[t & 1][h], bcl[h][m], 0, 0, 0);
                 }
             }
+            if (t + 1 < KT1) split1(t + 1, (t + 1) & 1);
             __builtin_amdgcn_sched_barrier(0);
         }
 #ifdef DRL_QC_STAMPS
         __builtin_amdgcn_sched_barrier(0);
         const uint64_t ts2 = __builtin_amdgcn_s_memtime();
 #endif
-        // ---- the output layer
+        // ---- the output layer: tile h's split beside tile h - 1's MFMAs
         f32x4 qf[TP];
-#pragma unroll
-        for (int h = 0; h < TP; ++h) {
-            f16x8 ah2[KT2], al2[KT2];
+        f16x8 ah2[2][KT2], al2[2][KT2];
+        auto split2 = [&](int h, int b) __attribute__((always_inline)) {
 #pragma unroll
             for (int s2 = 0; s2 < KT2; ++s2) {
                 float v[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int m = 2 * s2 + (j >> 2), i = j & 3;
-                    v[j] = fmaxf((bcc[h][m][i] + bcl[h][m][i] * kLo) + b1[s2][j >> 2][i], 0.0f);
+                    v[j] = qc4_relu(bcc[h][m][i] + bcl[h][m][i] * kLo);  // (layer 1's bias: bcc's initial value)
                 }
-                split_f16(v, ah2[s2], al2[s2], bad);
+                qc4_split(v, ah2[b][s2], al2[b][s2], mx);
             }
+        };
+        split2(0, 0);
+#pragma unroll
+        for (int h = 0; h < TP; ++h) {
             f32x4 qc, ql;
 #pragma unroll
             for (int t = 0; t < KT2; ++t) {
                 const f16x8 wh = as_f16x8(f2h[t]), wo = as_f16x8(f2l[t]);
-                qc = MFMA_F16(wh, ah2[t], t == 0 ? z4 : qc, 0, 0, 0);
-                ql = MFMA_F16(wh, al2[t], t == 0 ? z4 : ql, 0, 0, 0);
-                ql = MFMA_F16(wo, ah2[t], ql, 0, 0, 0);
+                qc = MFMA_F16(wh, ah2[h & 1][t], t == 0 ? z4 : qc, 0, 0, 0);
+                ql = MFMA_F16(wh, al2[h & 1][t], t == 0 ? z4 : ql, 0, 0, 0);
+                ql = MFMA_F16(wo, ah2[h & 1][t], ql, 0, 0, 0);
             }
+            if (h + 1 < TP) split2(h + 1, (h + 1) & 1);
 #pragma unroll
             for (int i = 0; i < 4; ++i) qf[h][i] = (qc[i] + ql[i] * kLo) + bq[i];
         }
@@ -1851,21 +1965,20 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
             }
             q[i] = v;
         }
-        {
-            const int64_t env = (TP * grp + g) * 16 + c;
-            if (env < a.E) {
-                int best = 0;
-                for (int i = 1; i < a.n_actions; ++i) best = q[i] > q[best] ? i : best;
-                const uint64_t ge = (uint64_t)(a.env_offset + env);
-                const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (ge << 8) ^ 0xa5ull));
-                const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
-                const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
-                a.actions[env * a.action_stride] = (u < a.epsilon) ? rnd : best;
-#ifndef DRL_QC_STAMPS
-                if (a.q)
-                    for (int i = 0; i < a.n_actions; ++i) a.q[env * a.n_actions + i] = q[i];
-#endif
+        if (env < a.E) {
+            int best = 0;
+            float bv = q[0];
+#pragma unroll
+            for (int i = 1; i < 8; ++i) {
+                const bool b = i < a.n_actions && q[i] > bv;
+                best = b ? i : best;
+                bv = b ? q[i] : bv;
             }
+            a.actions[env * a.action_stride] = explore >= 0 ? explore : best;
+#ifndef DRL_QC_STAMPS
+            if (a.q)
+                for (int i = 0; i < a.n_actions; ++i) a.q[env * a.n_actions + i] = q[i];
+#endif
         }
 #ifdef DRL_QC_STAMPS
         __builtin_amdgcn_sched_barrier(0);
@@ -1880,6 +1993,7 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
         }
 #endif
     }
+    bool bad = mx >= 0x477ff000u;  // 65520.0f (NaN cannot reach a split: see split_f16)
     bad |= lane == 0 && reinterpret_cast<const int32_t*>(a.packed + a.status_vec)[0] != 0;  // pack range flag
     if (__ballot(bad) && lane == 0 && a.err) atomicOr(a.err, DRL_ERR_QNET_RANGE);
     if (a.synth_n > 1) {  // as in drl_qnet_act_kernel (TP 16-env tiles per group)

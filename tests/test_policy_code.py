@@ -166,7 +166,9 @@ def _f32_forward(net, x):
 @pytest.mark.parametrize("side,n,radius,E,hidden", [(16, 8, 3, 65536, (128, 64)), (16, 8, 3, 1000, (32, 32)),
                                                     (32, 16, 3, 4096, (64,)), (16, 8, 3, 333, (128, 128, 128)),
                                                     (8, 3, 2, 777, (96, 32)), (16, 8, 4, 2048, (64, 32)),
-                                                    (16, 8, 4, 500, (96, 32)), (16, 8, 2, 31, (64, 64, 32))])
+                                                    (16, 8, 4, 500, (96, 32)), (16, 8, 2, 31, (64, 64, 32)),
+                                                    (8, 3, 2, 777, (128, 64)), (16, 8, 3, 100, (128, 64)),
+                                                    (32, 16, 3, 131072, (128, 64))])
 def test_qnet_act_code_matches_f32_forward(side, n, radius, E, hidden):
     """Q from the code == an f32 forward of drone 0's observation (and the
     obs-input f32 kernel's Q) within Q_TOL; greedy = the f32 argmax wherever

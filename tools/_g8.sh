@@ -7,7 +7,7 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout
 tail -15 gpurun_out/g8_tests.log
 [ $rc -ne 0 ] && exit $rc
 for r in 1 2; do
-  for v in prod v3 v2 pd4 pd10; do
+  for v in prod v3; do
     case $v in
       prod) timeout -k 10 120 python tools/time_act.py --precision f32 --input code ;;
       v3) DRL_QN_CODE=3 timeout -k 10 120 python tools/time_act.py --precision f32 --input code ;;
