@@ -1587,6 +1587,15 @@ __global__ void __launch_bounds__(64 * QN_CODE2_WAVES) drl_qnet_act_code3_kernel
 #endif
 constexpr int QC4_PD = DRL_QC4_PD;  // layer-0 fragment reads in flight per wave (ring of QC4_PD + 2)
 constexpr int QC4_WAVES = 4;
+#ifndef DRL_QC4_PIN
+#define DRL_QC4_PIN 0  // A/B knob: empty-asm pins keeping each step's decode between its MFMAs
+#endif
+#ifndef DRL_QC4_EARLYVEC
+#define DRL_QC4_EARLYVEC 0  // A/B knob: slice 0 waits only for the first code vector of each tile
+#endif
+#ifndef DRL_QC4_IGLP
+#define DRL_QC4_IGLP 0  // A/B knob: sched_group_barrier MFMA / 2 VALU interleave per step
+#endif
 
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
@@ -1707,10 +1716,17 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
     const int64_t gstride = (int64_t)gridDim.x * NW;
     constexpr float kLo = 1.0f / 2048.0f;
     const f16x2 kLo2 = {(_Float16)kLo, (_Float16)kLo};
-    const uint4* const code = reinterpret_cast<const uint4*>(a.obs);
+    // the codes through a buffer resource: 32-bit lane offsets (the launch keeps E * code bytes < 2^31), so no
+    // 64-bit lane address stays live across layer 0 for the next pass's loads
+    const auto crsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a.obs, 0, (int)(a.E * (64 * NV)), 0x00020000);
     auto load_vec = [&](int64_t tile, int v, uint32_t (&dst)[4 * NV]) __attribute__((always_inline)) {
-        const int64_t env = min(tile * 16 + c, a.E - 1);
-        const uint4 q = code[env * (4 * NV) + g * NV + v];
+        uint32_t ln;  // the lane index, recomputed here (opaque): nothing lane-dependent is kept for these loads
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+        const uint32_t env = (uint32_t)min(tile * 16 + (int64_t)(ln & 15u), a.E - 1);
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(
+            crsrc, (int)(env * (64u * NV) + ((ln >> 4) * NV + (uint32_t)v) * 16u), 0, 0);
+        uint4 q;
+        __builtin_memcpy(&q, &r, 16);
         dst[4 * v + 0] = q.x;
         dst[4 * v + 1] = q.y;
         dst[4 * v + 2] = q.z;
@@ -1769,6 +1785,7 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
     constexpr int KE = KP < 2 ? KP : 2;
     uint32_t cw[TP][4 * NV];
     const int64_t gl0 = grp0 < ngroups ? grp0 : 0;
+#if DRL_QC4_EARLYVEC
 #pragma unroll
     for (int h = 0; h < TP; ++h) load_vec(TP * gl0 + h, 0, cw[h]);
     __builtin_amdgcn_sched_barrier(0);
@@ -1779,13 +1796,26 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
     for (int v = 1; v < NV; ++v)
 #pragma unroll
         for (int h = 0; h < TP; ++h) load_vec(TP * gl0 + h, v, cw[h]);
+    constexpr int NE0 = 4 * (KP - KE) + TP * (NV - 1);  // vector ops younger than the slice-0 inputs
+#else
+#pragma unroll
+    for (int t = 0; t < KE; ++t) dma(t);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int h = 0; h < TP; ++h) load_codes(TP * gl0 + h, cw[h]);
+#pragma unroll
+    for (int h = 0; h < TP; ++h)
+#pragma unroll
+        for (int i = 0; i < 4 * NV; ++i) asm volatile("s_waitcnt vmcnt(0)" : "+v"(cw[h][i]));
+    constexpr int NE0 = 4 * (KP - KE);
+#endif
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = KE; t < KP; ++t) dma(t);
     __builtin_amdgcn_sched_barrier(0);
     auto slice_ready = [&](auto t_c) __attribute__((always_inline)) {
         constexpr int T = decltype(t_c)::value;
-        constexpr int N = T < KE ? 4 * (KP - KE) + TP * (NV - 1) : 4 * (KP - 1 - T);
+        constexpr int N = T < KE ? NE0 : 4 * (KP - 1 - T);
         asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(N) : "memory");
     };
     uint32_t mx = 0;  // bits of the largest activation split into fp16 (DRL_ERR_QNET_RANGE at >= 65520)
@@ -1804,6 +1834,10 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
 #endif
         const int64_t ngrp = grp + gstride;
         const int64_t env = (TP * grp + g) * 16 + c;  // the env whose action this lane writes (tile g, column c)
+        uint32_t ncw[TP][4 * NV];
+#ifdef DRL_QC_STAMPS
+        uint32_t slice_ts[KP];
+#endif
         f32x4 acc[TP][NT0];
         uint32_t bh[2][TP][4], bl[2][TP][4];  // B operands: [slice parity][tile][dword]
         q3u4 ring[RS];
@@ -1865,19 +1899,35 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
                 // step (empty asm on its input and outputs) so that it issues between this step's MFMAs
                 constexpr int h = st / 4, dd = st % 4, D = 4 * (t + 1) + dd;
                 uint32_t w = cw[h][qc4_word<CPG, D>()];
+#if DRL_QC4_PIN
                 asm volatile("" : "+v"(w));
+#endif
+#ifdef DRL_DIAG_QC4_NODECODE  // timing diagnostic (wrong results): no channel decode in the loop
+                uint32_t xh = w;
+#else
                 uint32_t xh = qc4_bdword<CPG, D>(w, bias_group);
+#endif
                 uint32_t xl = qc4_as<uint32_t>(qc4_as<f16x2>(xh) * kLo2);
+#if DRL_QC4_PIN
                 asm volatile("" : "+v"(xh), "+v"(xl));
+#endif
                 bh[(t + 1) & 1][h][dd] = xh;
                 bl[(t + 1) & 1][h][dd] = xl;
             }
-            if constexpr (t + 1 == KP && st == 3) {  // the codes are dead: the next group's in flight
+            // the last slice: layer 1's first fragments and the output layer's weights (the next pass's codes
+            // follow in layer 1, after ld1(1): waiting for f1[0] then waits for neither)
+            if constexpr (t + 1 == KP && st == 3) ld1(0, 0);
+            if constexpr (t + 1 == KP && st == 6) ld2(f2h, f2l, b1, bq);
+#if DRL_QC4_IGLP
 #pragma unroll
-                for (int h = 0; h < TP; ++h) load_codes(TP * (ngrp < ngroups ? ngrp : grp) + h, cw[h]);
+            for (int i = 0; i < TP; ++i) {  // one MFMA, then two VALU, per MFMA of the step
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
             }
-            if constexpr (t + 1 == KP && st == 6) ld1(0, 0);
-            if constexpr (t + 1 == KP && st == 9) ld2(f2h, f2l, b1, bq);
+#endif
+#ifdef DRL_QC_STAMPS
+            if constexpr (st == SPS - 1) slice_ts[t] = (uint32_t)(__builtin_amdgcn_s_memtime() - ts0);
+#endif
             __builtin_amdgcn_sched_barrier(0);
         });
         first = false;
@@ -1902,7 +1952,11 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
 #pragma unroll
         for (int t = 0; t < KT1; ++t) {
             if (t + 1 < KT1) ld1(t + 1, (t + 1) & 1);
-
+            if (t + 1 == KT1 && ngrp < ngroups) {  // the next pass's codes, into their own registers and younger than
+                // every layer-1 fragment (the compiler's wait counts for those then ignore them); copied at the end
+#pragma unroll
+                for (int h = 0; h < TP; ++h) load_codes(TP * ngrp + h, ncw[h]);
+            }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int m = 0; m < NT1; ++m) {
@@ -1990,8 +2044,16 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
             st[2] = (uint32_t)(ts3 - ts2);
             st[3] = (uint32_t)(ts0 - t_entry);
             st[4] = (uint32_t)(ts3 - t_entry);
+            uint32_t* sl = reinterpret_cast<uint32_t*>(a.q) + ngroups * 5 + grp * KP;
+            for (int t = 0; t < KP; ++t) sl[t] = slice_ts[t];
         }
 #endif
+        if (ngrp < ngroups) {
+#pragma unroll
+            for (int h = 0; h < TP; ++h)
+#pragma unroll
+                for (int i = 0; i < 4 * NV; ++i) cw[h][i] = ncw[h][i];
+        }
     }
     bool bad = mx >= 0x477ff000u;  // 65520.0f (NaN cannot reach a split: see split_f16)
     bad |= lane == 0 && reinterpret_cast<const int32_t*>(a.packed + a.status_vec)[0] != 0;  // pack range flag
@@ -2134,10 +2196,11 @@ hipError_t launch_qnet_act_code(const QnetArgs& a, int window, int num_cus, hipS
     const dim3 grid4((unsigned)nb4), block4(64 * QC4_WAVES);
     // drl_qnet_act_code3_kernel: the lo0_lds layout (layer 0's hi then lo fragments from offset 0) with
     // 8 waves of 128 units and a window whose layer 0 fits the LDS (5x5, 7x7)
+    const bool c4ok = a.E * (int64_t)lay::code_bytes(window) < (1ll << 31);  // (v4: 32-bit code offsets)
     const bool c3ok = v3 && a.lo0_lds && a.frag_off[0] == 0 && window <= 7 &&
                       a.frag_lo_off[0] == 8 * lay::code_kt(window) * 64 && blocks_ok(a);
 #define QN_CODE_SPEC(W)                                                                                         \
-    if (c3ok && W <= 7 && ver == 4) hipLaunchKernelGGL((drl_qnet_act_code4_kernel<8, (W <= 7 ? W : 7), 4>), grid4, block4, lds, s, a); \
+    if (c3ok && W <= 7 && ver == 4 && c4ok) hipLaunchKernelGGL((drl_qnet_act_code4_kernel<8, (W <= 7 ? W : 7), 4>), grid4, block4, lds, s, a); \
     else if (c3ok && W <= 7) hipLaunchKernelGGL((drl_qnet_act_code3_kernel<8, (W <= 7 ? W : 7), 4>), grid2, block2, lds, s, a); \
     else if (a.lo0_lds) hipLaunchKernelGGL((drl_qnet_act_code2_kernel<8, true, W, 4>), grid2, block2, lds, s, a);   \
     else hipLaunchKernelGGL((drl_qnet_act_code2_kernel<8, false, W, 4>), grid2, block2, lds, s, a)

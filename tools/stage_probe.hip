@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void g_void;
@@ -26,7 +27,7 @@ __global__ void __launch_bounds__(512) k_dma(const uint4* __restrict__ src, int 
         __builtin_amdgcn_global_load_lds((g_void*)(src + k * 64 + lane), (lds_void*)(wl + k * 64), 16, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0 && wl[(n_kb - 1) * 64 + 7].x == 0xdeadbeef) out[0] = 1;
+    if (threadIdx.x == 0 && blockIdx.x == 0) out[1] = wl[(n_kb - 1) * 64 + 7].x;
 }
 
 // register loads, then ds_write_b128
@@ -52,13 +53,23 @@ __global__ void __launch_bounds__(512) k_reg(const uint4* __restrict__ src, int 
     if (threadIdx.x == 0 && wl[(n_kb - 1) * 64 + 7].x == 0xdeadbeef) out[0] = 1;
 }
 
+static void check(const char* what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        printf("%s: %s\n", what, hipGetErrorString(e));
+        exit(1);
+    }
+}
+
 template <class F>
 static float time_it(F f, int reps = 100, uint4* junk = nullptr, size_t junk_bytes = 0) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
     for (int i = 0; i < 5; ++i) f();
+    check("launch");
     hipDeviceSynchronize();
+    check("sync");
     if (!junk) {
         hipEventRecord(a, 0);
         for (int i = 0; i < reps; ++i) f();
@@ -92,11 +103,13 @@ int main() {
     const size_t jb = 256u << 20;
     hipMalloc(&junk, jb);
     int dev = 0, cus = 0;
+    for (void* k : {(void*)k_empty, (void*)k_dma, (void*)k_reg})
+        hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     printf("CUs %d\n", cus);
     for (int waves : {4, 8}) {
-        for (int kb : {16, 64, 128, 160}) {
+        for (int kb : {8, 16, 32, 64, 96, 128, 160}) {
             const size_t lds = (size_t)kb * 1024;
             const dim3 g(cus), blk(64 * waves);
             const float te = time_it([&] { hipLaunchKernelGGL(k_empty, g, blk, lds, 0, d); });
@@ -109,6 +122,9 @@ int main() {
                    waves, kb, te, td, kb * 1024.0 / ((td - te) * 1e3), tr, tef, tdf);
         }
     }
+    int h[2] = {0, 0};
+    hipMemcpy(h, d, 8, hipMemcpyDeviceToHost);
+    printf("LDS word after the DMA: %08x (expect 01010101)\n", h[1]);
     printf("done\n");
     return 0;
 }

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--input", default="obs", choices=["obs", "code"], help="code: drl_qnet_act_code (f32)")
     ap.add_argument("--synth", action="store_true", help="also write drones 1..7's synthetic actions (act_synth)")
     ap.add_argument("--stamps", action="store_true", help="library built with -DDRL_QC_STAMPS: phase cycles")
+    ap.add_argument("--slices", type=int, default=0, help="v4 stamps: layer-0 slices per pass to print (10 at 7x7)")
     ap.add_argument("--group", type=int, default=64,
                     help="envs per wave pass of the stamped code act (64: v4 kernel, 32: DRL_QN_CODE=2|3)")
     ap.add_argument("--flush", action="store_true",
@@ -82,6 +83,16 @@ def main():
             v = st[:, i]
             print(f"stamps {name}: median {np.median(v):.0f} p10 {np.percentile(v, 10):.0f} "
                   f"p90 {np.percentile(v, 90):.0f} cycles (s_memtime)")
+        nw = min(rows, 1024)  # the first pass of every wave (256 CUs x 4 waves) vs later passes
+        if rows > nw:
+            for lab, sel in (("first pass", st[:nw]), ("later passes", st[nw:])):
+                print(f"  {lab}: " + " ".join(f"{n} {np.median(sel[:, i]):.0f}" for i, n in
+                                              enumerate(("layer0", "layer1", "layer2+epi"))))
+        if args.slices:  # v4 stamps build: per-slice layer-0 times after the 5-word rows
+            allw = q.view(torch.int32).cpu().numpy().astype("int64").reshape(-1)
+            sl = allw[5 * rows: 5 * rows + args.slices * rows].reshape(rows, args.slices)
+            print("layer-0 slice ends (median cycles since the pass start): " +
+                  " ".join(f"{np.median(sl[:, i]):.0f}" for i in range(args.slices)))
         t0 = st[:, 3] & 0xffffffff
         t3 = st[:, 4] & 0xffffffff
         print(f"tile start since kernel entry: min {t0.min()} median {np.median(t0):.0f} max {t0.max()}; "
