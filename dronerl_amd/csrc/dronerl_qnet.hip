@@ -1593,6 +1593,9 @@ constexpr int QC4_WAVES = 4;
 #ifndef DRL_QC4_EARLYVEC
 #define DRL_QC4_EARLYVEC 0  // A/B knob: slice 0 waits only for the first code vector of each tile
 #endif
+#ifndef DRL_QC4_DMALOOP
+#define DRL_QC4_DMALOOP 0  // A/B knob: stage slices >= 2 inside layer 0 (measured slower: 17.6 vs 16.5 us at C3)
+#endif
 #ifndef DRL_QC4_IGLP
 #define DRL_QC4_IGLP 0  // A/B knob: sched_group_barrier MFMA / 2 VALU interleave per step
 #endif
@@ -1750,7 +1753,9 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
     };
     auto bias4 = [&](int off) __attribute__((always_inline)) {
         f32x4 r;
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(pbuf, 16 * g, a.bias_vec * 16 + off * 4, 0);
+        uint32_t ln;  // (the lane index recomputed, opaque: its offset is not kept in a register across layer 0)
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(pbuf, (int)((ln >> 4) * 16u), a.bias_vec * 16 + off * 4, 0);
         __builtin_memcpy(&r, &v, 16);
         return r;
     };
@@ -1810,12 +1815,29 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
     constexpr int NE0 = 4 * (KP - KE);
 #endif
     __builtin_amdgcn_sched_barrier(0);
+#if DRL_QC4_DMALOOP
+    // slices >= KE are staged inside the first pass's layer 0: slice s's four fragments at steps 1, 5, 9, 13 of
+    // slice s - 2 (one LDS-DMA instruction holds the issuing wave ~60-180 cycles: all 32 in the prologue kept
+    // every wave ~5k cycles from its first MFMA).  slice_ready(T) runs at step 16 T - PD, when slice T + 1's
+    // fragments issued at steps <= 16 - PD of slice T - 1 are younger than slice T's.
+    static_assert(!DRL_QC4_EARLYVEC && KE == 2, "DMALOOP stages slices >= 2 in the loop");
+    constexpr int NDY = (1 <= 16 - PD) + (5 <= 16 - PD) + (9 <= 16 - PD) + (13 <= 16 - PD);
+    if (grp0 >= ngroups) {  // a wave without a pass still stages its fragments
+#pragma unroll
+        for (int t = KE; t < KP; ++t) dma(t);
+    }
+#else
 #pragma unroll
     for (int t = KE; t < KP; ++t) dma(t);
+#endif
     __builtin_amdgcn_sched_barrier(0);
     auto slice_ready = [&](auto t_c) __attribute__((always_inline)) {
         constexpr int T = decltype(t_c)::value;
+#if DRL_QC4_DMALOOP
+        constexpr int N = T == 0 ? 0 : (T + 1 < KP ? NDY : 0);
+#else
         constexpr int N = T < KE ? NE0 : 4 * (KP - 1 - T);
+#endif
         asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(N) : "memory");
     };
     uint32_t mx = 0;  // bits of the largest activation split into fp16 (DRL_ERR_QNET_RANGE at >= 65520)
@@ -1894,6 +1916,16 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
                 __builtin_memcpy(&x, hl ? bl[t & 1][h] : bh[t & 1][h], 16);
                 acc[h][m] = MFMA_F16(w, x, (t == 0 && hl == 0) ? z4 : acc[h][m], 0, 0, 0);
             }
+#if DRL_QC4_DMALOOP
+            if constexpr (t + 2 < KP && (st == 1 || st == 5 || st == 9 || st == 13)) {  // slice t + 2's fragment
+                if (first) {  // (through the buffer resource: a uniform offset, no 64-bit lane address)
+                    constexpr int k = st / 4, h = k >> 1, u = k & 1;
+                    const int v0 = h * FLO + ((2 * wave + u) * KP + t + 2) * 64;
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(pbuf, (__attribute__((address_space(3))) void*)(wl + v0), 16,
+                                                             lane16, v0 * 16, 0, 0);
+                }
+            }
+#endif
             issue(std::integral_constant<int, S + PD>{});
             if constexpr (t + 1 < KP) {  // dword st % 4 of tile st / 4 of the next slice's inputs, pinned to this
                 // step (empty asm on its input and outputs) so that it issues between this step's MFMAs
