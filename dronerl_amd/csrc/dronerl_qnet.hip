@@ -1596,6 +1596,9 @@ constexpr int QC4_WAVES = 4;
 #ifndef DRL_QC4_DMALOOP
 #define DRL_QC4_DMALOOP 0  // A/B knob: stage slices >= 2 inside layer 0 (measured slower: 17.6 vs 16.5 us at C3)
 #endif
+#ifndef DRL_QC4_IGLP1
+#define DRL_QC4_IGLP1 0  // A/B knob: sched_group_barrier MFMA / 3 VALU interleave of layer 1
+#endif
 #ifndef DRL_QC4_IGLP
 #define DRL_QC4_IGLP 0  // A/B knob: sched_group_barrier MFMA / 2 VALU interleave per step
 #endif
@@ -2001,6 +2004,15 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
                 }
             }
             if (t + 1 < KT1) split1(t + 1, (t + 1) & 1);
+#if DRL_QC4_IGLP1
+            if (t + 1 < KT1) {  // the next slice's split interleaved with this slice's MFMAs: 1 MFMA, 3 VALU
+#pragma unroll
+                for (int i = 0; i < 3 * TP * NT1; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                }
+            }
+#endif
             __builtin_amdgcn_sched_barrier(0);
         }
 #ifdef DRL_QC_STAMPS
