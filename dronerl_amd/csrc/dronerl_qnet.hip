@@ -1596,6 +1596,9 @@ constexpr int QC4_WAVES = 4;
 #ifndef DRL_QC4_DMALOOP
 #define DRL_QC4_DMALOOP 0  // A/B knob: stage slices >= 2 inside layer 0 (measured slower: 17.6 vs 16.5 us at C3)
 #endif
+#ifndef DRL_QC4_EARLYSPLIT
+#define DRL_QC4_EARLYSPLIT 1  // layer 1's first split inside layer 0's last slice (16.33-16.53 vs 16.44-16.75 us, g19)
+#endif
 #ifndef DRL_QC4_IGLP1
 #define DRL_QC4_IGLP1 0  // A/B knob: sched_group_barrier MFMA / 3 VALU interleave of layer 1
 #endif
@@ -1895,6 +1898,17 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
                 f1[b][1][m] = frag_ld(flo + (m * KT1 + t) * 64);
             }
         };
+        f16x8 ah[2][TP], al[2][TP];  // layer 1's inputs: [K-slice parity][tile]
+        auto split1_tile = [&](int t, int b, int h) __attribute__((always_inline)) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = qc4_relu(acc[h][2 * t + (j >> 2)][j & 3]);
+            qc4_split(v, ah[b][h], al[b][h], mx);
+        };
+        auto split1 = [&](int t, int b) __attribute__((always_inline)) {
+#pragma unroll
+            for (int h = 0; h < TP; ++h) split1_tile(t, b, h);
+        };
         // ---- layer 0: STEPS fragment reads, PD ahead of their MFMAs
         auto issue = [&](auto s_c) __attribute__((always_inline)) {
             constexpr int S = decltype(s_c)::value;
@@ -1953,6 +1967,11 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
             // follow in layer 1, after ld1(1): waiting for f1[0] then waits for neither)
             if constexpr (t + 1 == KP && st == 3) ld1(0, 0);
             if constexpr (t + 1 == KP && st == 6) ld2(f2h, f2l, b1, bq);
+#if DRL_QC4_EARLYSPLIT
+            // layer 1's first K-slice reads unit tiles 0 and 1, final after this slice's steps 8 and 9: tile
+            // st - 11's split beside the last steps' MFMAs
+            if constexpr (t + 1 == KP && st >= 11 && st - 11 < TP) split1_tile(0, 0, st - 11);
+#endif
 #if DRL_QC4_IGLP
 #pragma unroll
             for (int i = 0; i < TP; ++i) {  // one MFMA, then two VALU, per MFMA of the step
@@ -1973,17 +1992,9 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
         // ---- layer 1 (bias folded into layer 0); K-slice t's inputs split from layer 0's unit tiles 2t, 2t + 1,
         // the next slice's split beside this slice's MFMAs
         f32x4 bcc[TP][NT1], bcl[TP][NT1];
-        f16x8 ah[2][TP], al[2][TP];
-        auto split1 = [&](int t, int b) __attribute__((always_inline)) {
-#pragma unroll
-            for (int h = 0; h < TP; ++h) {
-                float v[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = qc4_relu(acc[h][2 * t + (j >> 2)][j & 3]);
-                qc4_split(v, ah[b][h], al[b][h], mx);
-            }
-        };
+#if !DRL_QC4_EARLYSPLIT
         split1(0, 0);
+#endif
 #pragma unroll
         for (int t = 0; t < KT1; ++t) {
             if (t + 1 < KT1) ld1(t + 1, (t + 1) & 1);
