@@ -40,9 +40,10 @@ def test_committed_traffic_is_read_plus_doubled_fetch(cfg):
     assert bench.load_traffic(cfg) == d["hbm_bytes_per_launch"]
     G, N, E, K = bench.CONFIGS[cfg]
     R, W = bench.algorithmic_bytes(G, N, K)
-    # measured traffic per env-step within a factor of 2 of the algorithmic bytes
+    # measured traffic per env-step within a factor of 2 of the algorithmic bytes; the lower bound takes the
+    # ground as packed (ABI 8: G^2 / 2 bytes read) and not written back whole (only changed cells are)
     per = d["hbm_bytes_per_launch"] / E
-    assert 0.5 * (R + W) < per < 2.0 * (R + W)
+    assert 0.5 * (R - G * G // 2 + W - G * G) < per < 2.0 * (R + W)
 
 
 def test_cpu_baseline_record():
