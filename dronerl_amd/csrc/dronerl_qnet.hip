@@ -574,9 +574,9 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_f32_kernel(QnetArg
 // two MFMAs per tile and slice (hi and lo weights) instead of three.  The
 // products differ from W * fl(c / 100) by the rounding of fl(W / 100) and
 // fl(c / 100), ~1e-7 relative: far inside the f32 act's 1e-5 bound.
-// One workgroup per CU (the net fills the LDS); the kernel's ~140 VGPRs leave
-// room for 3 waves per SIMD, so a workgroup runs up to 12 waves (the obs act's
-// 4 hide its observation reads behind a register ring instead).
+// One workgroup per CU (the net fills the LDS); the kernel's ~140 VGPRs would
+// leave room for 3 waves per SIMD, but __launch_bounds__ caps a workgroup at
+// QN_CODE_MAXW = 8 waves (DRL_QN_CODE_WAVES is clamped to it).
 #ifndef DRL_QN_CODE2_WAVES
 #define DRL_QN_CODE2_WAVES 8  // drl_qnet_act_code2_kernel: 2 waves per SIMD (its ~230 VGPRs)
 #endif
