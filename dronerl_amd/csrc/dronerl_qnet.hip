@@ -2157,6 +2157,27 @@ __global__ void __launch_bounds__(256) drl_replay_add_kernel(ReplayArgs a, FastD
     }
 }
 
+// The same with one thread per 16-B chunk, for rows that are whole 16-B vectors at 16-B aligned addresses (the
+// 128-B policy-code rows): a quarter of the threads of the float2 form, whose launch was latency-bound (5 us for
+// 10,000 code-row transitions in the C3 train loop, profiles/r04_final/loop_*).
+__global__ void __launch_bounds__(256) drl_replay_add16_kernel(ReplayArgs a, FastDiv dcols, uint32_t total) {
+    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+    if (k >= total) return;
+    const uint32_t D4 = (uint32_t)a.obs_floats / 4u;
+    const uint32_t r = __umulhi(k, dcols.m), col = k - r * D4;  // D4 >= 2
+    const int64_t i = a.first + r;
+    const int64_t slot = (a.cursor + i) % a.capacity;
+    const uint4 o = reinterpret_cast<const uint4*>(a.obs + i * a.obs_stride)[col];
+    const uint4 nx = reinterpret_cast<const uint4*>(a.next_obs + i * a.next_obs_stride)[col];
+    reinterpret_cast<uint4*>(a.buf_obs + slot * a.obs_floats)[col] = o;
+    reinterpret_cast<uint4*>(a.buf_next_obs + slot * a.obs_floats)[col] = nx;
+    if (col == 0) {
+        a.buf_actions[slot] = a.actions[i * a.action_stride];
+        a.buf_rewards[slot] = a.rewards[i * a.reward_stride];
+        a.buf_dones[slot] = a.dones[i * a.done_stride];
+    }
+}
+
 __global__ void drl_replay_add_rows_kernel(ReplayArgs a) {  // fallback for huge batches: block per row
     const int64_t i = a.first + blockIdx.x;
     if (i >= a.n) return;
@@ -2286,7 +2307,13 @@ hipError_t launch_replay_add(const ReplayArgs& a, hipStream_t s) {
     if (rows <= 0) return hipSuccess;
     const uint64_t D2 = (uint64_t)a.obs_floats / 2;
     const uint64_t total = (uint64_t)rows * D2;
-    if (D2 >= 2 && total * D2 < (1ull << 32)) {  // multiply-shift row index exact (FastDiv bound)
+    const uint64_t D4 = (uint64_t)a.obs_floats / 4, total4 = (uint64_t)rows * D4;
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
+    if (a.obs_floats % 4 == 0 && D4 >= 2 && a.obs_stride % 4 == 0 && a.next_obs_stride % 4 == 0 && al16(a.obs) &&
+        al16(a.next_obs) && al16(a.buf_obs) && al16(a.buf_next_obs) && total4 * D4 < (1ull << 32)) {
+        hipLaunchKernelGGL(drl_replay_add16_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, s, a,
+                           make_fastdiv((uint32_t)D4), (uint32_t)total4);
+    } else if (D2 >= 2 && total * D2 < (1ull << 32)) {  // multiply-shift row index exact (FastDiv bound)
         hipLaunchKernelGGL(drl_replay_add_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a,
                            make_fastdiv((uint32_t)D2), (uint32_t)total);
     } else {
