@@ -92,7 +92,10 @@ int step_group_lanes(int n_drones, int gstride, int cells, int window) {
 // actions (tools/ring_usage.py): mean 2.06 / 2.56 / 3.44 and at most 17 at N =
 // 8 / 16 / 32, i.e. about 1.53 + 0.06 N, and up to ~2.2x the mean over 16
 // steps.  A refill every half block's worth of mean use (at most 32 steps)
-// keeps the heaviest envs off the dry-ring path: 32 at C3 and C4, 22 at C5.
+// keeps the heaviest envs off the dry-ring path.  Round 4 (block-conversion
+// refill, profiles/r04_refill/): 0.62 of a block's mean use, capped at 48 --
+// 48 at C3 (3.24-3.25e9 env-steps/s against 3.20e9 at 32 and 3.19e9 at 64),
+// 38 at C4, 28 at C5 (22, 32: 9.07-9.11e8 alike, 44: 8.98e8).
 // The bytes per step do not depend on the cadence (each block is converted
 // once); only the launch count and the dry-ring risk do.  DRL_REFILL_EVERY
 // overrides it (A/B runs) with a positive step count; anything else is
@@ -105,8 +108,8 @@ int refill_cadence(int n_drones, int side) {
         return (end != v && *end == 0 && r > 0 && r <= 1 << 20) ? (int)r : -1;
     }
     const double per_block = (DRL_MT_BLOCK1 / 2.0) * side / (double)(1 << bit_length((uint32_t)side));
-    const int r = (int)(0.5 * per_block / (1.53 + 0.06 * n_drones));
-    return r < 1 ? 1 : (r > 32 ? 32 : r);
+    const int r = (int)(0.62 * per_block / (1.53 + 0.06 * n_drones));
+    return r < 1 ? 1 : (r > 48 ? 48 : r);
 }
 
 int validate(const drl_params* p, drl_layout* L) {

@@ -58,11 +58,11 @@ def test_layout_and_validation():
     assert (L.cells, L.ground_stride, L.drone_stride, L.mt_stride, L.obs_window, L.obs_floats) == \
         (256, 128, 8, 1776, 7, 294)  # ground: two cells per byte (ABI 8)
     assert L.step_group_lanes == 8
-    assert (L.cand_slots, L.refill_every) == (512, 32)
+    assert (L.cand_slots, L.refill_every) == (512, 48)  # 0.62 of a block's mean use, capped at 48 (round 4)
     L = EnvParams(n_drones=32, grid_size=64).layout()
     assert L.step_group_lanes in (32, 64) and L.step_lds_bytes <= 160 * 1024
-    # half a block's worth of candidates (156 pairs at power-of-two sides) at ~1.53 + 0.06 N per step
-    assert L.refill_every == 22
+    # 0.62 of a block's worth of candidates (156 pairs at power-of-two sides) at ~1.53 + 0.06 N per step
+    assert L.refill_every == 28
     L = EnvParams(n_drones=1, grid_size=5).layout()
     assert L.ground_stride == 16  # 25 cells -> 13 bytes -> 16
     with pytest.raises(ValueError, match="Not enough positions"):
