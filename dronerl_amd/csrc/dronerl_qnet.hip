@@ -1599,6 +1599,9 @@ constexpr int QC4_WAVES = 4;
 #ifndef DRL_QC4_EARLYSPLIT
 #define DRL_QC4_EARLYSPLIT 1  // layer 1's first split inside layer 0's last slice (16.33-16.53 vs 16.44-16.75 us, g19)
 #endif
+#ifndef DRL_QC4_EARLYNEXT
+#define DRL_QC4_EARLYNEXT 1  // the second pass's codes loaded in the prologue (see the kernel)
+#endif
 #ifndef DRL_QC4_IGLP1
 #define DRL_QC4_IGLP1 0  // A/B knob: sched_group_barrier MFMA / 3 VALU interleave of layer 1
 #endif
@@ -1837,12 +1840,25 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
     for (int t = KE; t < KP; ++t) dma(t);
 #endif
     __builtin_amdgcn_sched_barrier(0);
+    uint32_t ncw[TP][4 * NV];  // the next pass's codes
+#if DRL_QC4_EARLYNEXT
+    // the second pass's codes, youngest of the prologue's loads (the slice waits below count them), in flight from
+    // the start: in the train loop they come from HBM, and a prefetch during the first pass's layer 1 left their
+    // latency exposed at the second pass's start (C5 act 42 us in the loop against 28 back to back).
+    // Unconditional (past the last pass the first pass's again, from L2), so every wait count is static.
+#pragma unroll
+    for (int h = 0; h < TP; ++h) load_codes(TP * (grp0 + gstride < ngroups ? grp0 + gstride : gl0) + h, ncw[h]);
+    constexpr int NNX = TP * NV;
+#else
+    constexpr int NNX = 0;
+#endif
+    __builtin_amdgcn_sched_barrier(0);
     auto slice_ready = [&](auto t_c) __attribute__((always_inline)) {
         constexpr int T = decltype(t_c)::value;
 #if DRL_QC4_DMALOOP
         constexpr int N = T == 0 ? 0 : (T + 1 < KP ? NDY : 0);
 #else
-        constexpr int N = T < KE ? NE0 : 4 * (KP - 1 - T);
+        constexpr int N = (T < KE ? NE0 : 4 * (KP - 1 - T)) + NNX;
 #endif
         asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(N) : "memory");
     };
@@ -1862,7 +1878,6 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
 #endif
         const int64_t ngrp = grp + gstride;
         const int64_t env = (TP * grp + g) * 16 + c;  // the env whose action this lane writes (tile g, column c)
-        uint32_t ncw[TP][4 * NV];
 #ifdef DRL_QC_STAMPS
         uint32_t slice_ts[KP];
 #endif
@@ -1998,7 +2013,8 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
 #pragma unroll
         for (int t = 0; t < KT1; ++t) {
             if (t + 1 < KT1) ld1(t + 1, (t + 1) & 1);
-            if (t + 1 == KT1 && ngrp < ngroups) {  // the next pass's codes, into their own registers and younger than
+            if (t + 1 == KT1 && ngrp < ngroups && !(DRL_QC4_EARLYNEXT && grp == grp0)) {  // the next pass's codes (the
+                // first pass's successor was loaded in the prologue), into their own registers and younger than
                 // every layer-1 fragment (the compiler's wait counts for those then ignore them); copied at the end
 #pragma unroll
                 for (int h = 0; h < TP; ++h) load_codes(TP * ngrp + h, ncw[h]);
