@@ -1600,7 +1600,7 @@ constexpr int QC4_WAVES = 4;
 #define DRL_QC4_EARLYSPLIT 1  // layer 1's first split inside layer 0's last slice (16.33-16.53 vs 16.44-16.75 us, g19)
 #endif
 #ifndef DRL_QC4_EARLYNEXT
-#define DRL_QC4_EARLYNEXT 1  // the second pass's codes loaded in the prologue (see the kernel)
+#define DRL_QC4_EARLYNEXT 0  // A/B knob: the second pass's codes loaded in the prologue (C5 act in the loop 41.4 vs 42.0 us, C3 loop 45.8 vs 45.1-45.4: not kept)
 #endif
 #ifndef DRL_QC4_IGLP1
 #define DRL_QC4_IGLP1 0  // A/B knob: sched_group_barrier MFMA / 3 VALU interleave of layer 1
