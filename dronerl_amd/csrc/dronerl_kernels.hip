@@ -1802,10 +1802,15 @@ __device__ __forceinline__ void fy_run(const FyLds& f, uint32_t (&x)[10], int& m
 // of the current tempered 64-word chunk, so the shuffle chain is uniform
 // scalar control flow plus single-lane LDS swaps.  Same draws, same order,
 // same results as the lane kernel (and the reference).
-__global__ void __launch_bounds__(64) drl_reset_wave_kernel(ResetArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int lane = threadIdx.x;
-    const int64_t env = blockIdx.x;
+// WPB waves per workgroup, each its own env and LDS image (no workgroup barrier): a CU runs at most 16
+// workgroups, so one-wave workgroups cap it at 16 resets in flight where the LDS would hold more (small grids).
+template <int WPB>
+__global__ void __launch_bounds__(64 * WPB) drl_reset_wave_kernel(ResetArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
+    const int lane = threadIdx.x & 63;
+    const int wv = WPB > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
+    unsigned char* const smem = smem_all + (size_t)wv * a.wave_lds;
+    const int64_t env = (int64_t)blockIdx.x * WPB + wv;
     if (env >= a.E || (a.mask != nullptr && a.mask[env] == 0)) return;  // whole wave, uniform
     FyLds f;
     f.bmap = reinterpret_cast<uint32_t*>(smem);  // batched shuffle: one bit per cell (repeated j's)
@@ -2369,7 +2374,21 @@ extern "C" int drl_debug_set_stamps(void* p) {
 
 hipError_t launch_reset(const ResetArgs& a, hipStream_t s) {
     if (a.wave_per_env) {
-        hipLaunchKernelGGL(drl_reset_wave_kernel, dim3((unsigned)a.E), dim3(64), a.wave_lds, s, a);
+        // waves (envs) per workgroup: 4 on large grids (C5 2.00e7 vs 1.91e7 resets/s), 1 below (C3 / C4 alike
+        // within noise at 1, 2, 4; profiles/r04_reset/); DRL_RESET_WPB = 1, 2 or 4 overrides (A/B knob)
+        static const int wpb_env = [] {
+            const char* e = getenv("DRL_RESET_WPB");
+            const int v = e ? atoi(e) : 0;
+            return (v == 1 || v == 2 || v == 4) ? v : 0;
+        }();
+        const int wpb = wpb_env ? wpb_env : (a.cells >= 4096 ? 4 : 1);
+        const unsigned nb = (unsigned)((a.E + wpb - 1) / wpb);
+        if (wpb == 4 && 4 * (size_t)a.wave_lds <= 160 * 1024)
+            hipLaunchKernelGGL(drl_reset_wave_kernel<4>, dim3(nb), dim3(256), 4 * (size_t)a.wave_lds, s, a);
+        else if (wpb == 2 && 2 * (size_t)a.wave_lds <= 160 * 1024)
+            hipLaunchKernelGGL(drl_reset_wave_kernel<2>, dim3(nb), dim3(128), 2 * (size_t)a.wave_lds, s, a);
+        else
+            hipLaunchKernelGGL(drl_reset_wave_kernel<1>, dim3((unsigned)a.E), dim3(64), a.wave_lds, s, a);
     } else {
         const int64_t blocks = (a.E + a.lanes - 1) / a.lanes;
         hipLaunchKernelGGL(drl_reset_kernel, dim3((unsigned)blocks), dim3(64), a.block_lds, s, a);
