@@ -16,7 +16,7 @@ HOSTSAN := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
            -Xarch_host -fno-sanitize-recover=undefined -Xarch_host -fno-omit-frame-pointer
 CSRC := dronerl_amd/csrc
 SRCS := $(CSRC)/dronerl_kernels.hip $(CSRC)/dronerl_api.cpp $(CSRC)/dronerl_env.cpp $(CSRC)/dronerl_qnet.hip \
-        $(CSRC)/dronerl_qnet_api.cpp
+        $(CSRC)/dronerl_qnet_api.cpp $(CSRC)/dronerl_learn.hip
 DEPS := $(SRCS) $(CSRC)/dronerl_internal.h include/dronerl.h
 
 asan: build/asan/liboracle.so build/asan/libdronerl.so

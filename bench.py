@@ -100,6 +100,31 @@ def needs_launch(args) -> bool:
     return args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.pmc_child
 
 
+def visible_gpus():
+    """GPUs the ranks could use, counted without touching the HIP runtime (the
+    launcher stays GPU-free): the KFD topology's GPU nodes (simd_count > 0),
+    narrowed by HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES.
+    None when the topology is unreadable (no check then)."""
+    import glob
+    n = 0
+    nodes = glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties")
+    if not nodes:
+        return None
+    for f in nodes:
+        try:
+            for ln in open(f):
+                k, _, v = ln.partition(" ")
+                if k == "simd_count" and int(v) > 0:
+                    n += 1
+        except (OSError, ValueError):
+            return None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def launch_ranks(argv, n: int) -> int:
     """Run the N-rank job as a child process (this process never initialises
     the GPU: argument parsing only), forward its output, print rank 0's JSON
@@ -107,10 +132,12 @@ def launch_ranks(argv, n: int) -> int:
     the job's exit code: torch.distributed.run fails when any rank fails; a
     clean job without a JSON line is an error too."""
     import subprocess
-    if DIST_BACKEND == "nccl" and torch.cuda.device_count() < n:  # (device_count does not initialise HIP)
-        print(f"bench.py --gpus {n}: only {torch.cuda.device_count()} GPU(s) visible; nccl needs one GPU per rank "
-              "(DRL_DIST_BACKEND=gloo shares devices)", file=sys.stderr)
-        return 2
+    if DIST_BACKEND == "nccl":
+        have = visible_gpus()
+        if have is not None and have < n:
+            print(f"bench.py --gpus {n}: only {have} GPU(s) visible; nccl needs one GPU per rank "
+                  "(DRL_DIST_BACKEND=gloo shares devices)", file=sys.stderr)
+            return 2
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
     cmd = launcher_command(argv, n, free_port())
     print("bench.py launcher: " + " ".join(cmd[1:]), file=sys.stderr, flush=True)
@@ -352,7 +379,8 @@ def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream,
     separately from the env step.  (1) drl_qnet_act alone on the resident obs
     (dense 294->128->64->5 on MFMA, epsilon-greedy, writes actions[:, 0]):
     HBM-bound on reading the obs (E * W*W*6 f32); (2) the train_jax.py:42-64
-    loop shape per step: act -> step + obs -> replay add_many (capacity 10000).
+    loop shape per step: act -> step + obs -> replay add_many (capacity
+    MEMORY_SIZE), without the learner (train_loop_bench has it).
     `precision` is the loop's (f32: the reference's nets); both acts are
     timed alone, and the f32 act from the policy code (drl_qnet_act_code,
     128 B per env read instead of 1,176).  `input` is the loop act's."""
@@ -360,7 +388,7 @@ def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream,
     E = env.num_envs
     D = obs[0].numel()
     net = QNetwork(D, (128, 64), device=env.device, generator=torch.Generator().manual_seed(0), precision=precision)
-    rb = ReplayBuffer(10000, D, env.device)
+    rb = ReplayBuffer(MEMORY_SIZE, D, env.device)
     flat = obs.reshape(E, -1)
     a0 = actions[0]
     for t in range(warmup):
@@ -378,7 +406,7 @@ def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream,
                         precision="f32", input="code")
         bufs = [env.new_code(), env.new_code()]
         env.get_code(out=bufs[0])
-        rb = ReplayBuffer(10000, D, env.device, code_radius=env.params.window_radius)
+        rb = ReplayBuffer(MEMORY_SIZE, D, env.device, code_radius=env.params.window_radius)
     ev[2].record(stream)
     for t in range(steps):
         cur, nxt = bufs[t & 1], bufs[(t + 1) & 1]
@@ -446,9 +474,10 @@ def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream,
                              "the f32 forward",
             "loop_us_per_step": loop_s * 1e6, "loop_env_steps_per_s": E / loop_s,
             "loop": (f"act(code_t, f32) -> step + drone 0 policy code -> replay add_many(code_t, a, r, "
-                     "code_t+1, done) of code rows (sample() decodes), capacity 10000") if input == "code" else
+                     f"code_t+1, done) of code rows, capacity {MEMORY_SIZE}; no learner (train_loop has it)")
+                    if input == "code" else
                     (f"act(obs_t, {precision}) -> step + obs(K=1) -> replay add_many(obs_t, a, r, obs_t+1, done), "
-                     "capacity 10000")}
+                     f"capacity {MEMORY_SIZE}; no learner (train_loop has it)")}
 
 
 MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense f16/bf16 MFMA (MI355X_MICROARCH.md; the 16x16x32 f16 form: 16 cycles)
@@ -539,18 +568,25 @@ def rollout_bench(env, actions, K, warmup_steps, steps, chunk: int, R: int, Wb: 
                                  "state is read and written once per launch, so HBM traffic per step is lower"}}
 
 
+# train_jax.py:351 --memory_size: the replay capacity of the train loops
+MEMORY_SIZE = 100_000
+
 # diagnostic: the train loop's step with streaming observation stores (A/B of
 # env.step()'s store mode where the act kernel reads the observation next)
 LOOP_OBS_STREAM = {"0": False, "1": True}.get(os.environ.get("DRL_LOOP_OBS_STREAM", ""))
 
 
 class TrainSegment:
-    """One segment of the train_jax.py:38-113 loop minus the learner (SURVEY.md
-    §8 D2; C5: "multi-step loop, hipGraph of step+obs+act"): per step,
-    synthetic actions for every drone, the epsilon-greedy DQN action for drone
-    0 (dense 294->128->64->5), step + obs(K=1), replay add_many of the drone-0
-    transition; after `seg` steps a reset of every env (reset_env_every,
-    train_jax.py:101-113) and its first observation.
+    """One segment of the train_jax.py:38-113 scan loop (C5:
+    "multi-step loop, hipGraph of step+obs+act"): per step, synthetic actions
+    for every drone, the epsilon-greedy DQN action for drone 0 (dense
+    294->128->64->5, epsilon read from the learner's device counter), step +
+    obs(K=1), replay add_many of the drone-0 transition into the reference's
+    100,000-slot memory (train_jax.py:173, --memory_size), and the learner
+    block (:68-98, drl_dqn_train: sample 8 rows + train_step + Adam, the target
+    update every 10 steps, the epsilon decay every 5, step + 1); after `seg`
+    steps a reset of every env (reset_env_every, train_jax.py:101-113) and its
+    first observation.  learn=False drops the learner (epsilon fixed at 0.1).
 
     fused=True: the synthetic actions of drones 1..N-1 are written by the act
     launch itself (drl_qnet_act_synth), one kernel fewer per step with the
@@ -560,7 +596,9 @@ class TrainSegment:
     side streams, joined to the act -> step chain by events; so does the
     respawn-candidate refill (env.step()'s cadence, launched on its own branch
     after the step it follows: it overlaps the next act, and the next step
-    waits for it).  Observations, actions,
+    waits for it).  The learner follows the add of its step on the main
+    stream (it samples the ring the add fills), and the next act follows the
+    learner (it acts with the updated net).  Observations, actions,
     rewards and dones rotate through 3 buffers, so step t only waits for the
     replay add of step t-2 and the actions of step t are drawn while step t-1
     runs.  parallel=False issues the same calls in the same order on one
@@ -568,8 +606,9 @@ class TrainSegment:
     (tests/test_gpu_parity.py::test_train_segment_parallel_matches_serial)."""
 
     def __init__(self, env, seg: int, parallel: bool = False, net=None, rb=None, fused: bool = True,
-                 precision: str = "f32", input: str = "obs"):
-        from dronerl_amd.dqn import QNetwork, ReplayBuffer
+                 precision: str = "f32", input: str = "obs", learn: bool = True, capacity: int = MEMORY_SIZE,
+                 hp=None):
+        from dronerl_amd.dqn import DQNHParams, DQNLearner, QNetwork, ReplayBuffer
         E, N, dev = env.num_envs, env.n_drones, env.device
         W = env.layout.obs_window
         D = W * W * 6
@@ -586,7 +625,9 @@ class TrainSegment:
         self.NB = 3 if parallel else 2
         self.net = net or QNetwork(D, (128, 64), device=dev, generator=torch.Generator().manual_seed(0),
                                    precision=precision, input=input)
-        self.rb = rb or ReplayBuffer(10000, D, dev, code_radius=env.params.window_radius if input == "code" else 0)
+        self.rb = rb or ReplayBuffer(capacity, D, dev, code_radius=env.params.window_radius if input == "code" else 0)
+        self.learner = DQNLearner(self.net, hp or DQNHParams(), generator=torch.Generator().manual_seed(1)) \
+            if learn else None
         self.acts = [torch.empty((E, N), dtype=torch.int32, device=dev) for _ in range(self.NB)]
         self.rewards = [torch.empty((E, N), dtype=torch.float32, device=dev) for _ in range(self.NB)]
         self.dones = [torch.empty((E, N), dtype=torch.uint8, device=dev) for _ in range(self.NB)]
@@ -609,7 +650,8 @@ class TrainSegment:
     def _act_step(self, t, before_step=None):
         b, nb = t % self.NB, (t + 1) % self.NB
         x = self.code[b] if self.input == "code" else self.obs[b].reshape(self.E, -1)
-        self.net.act(x, 0.1, seed=7, step=t, env_offset=self.env.env_offset,
+        eps = self.learner.epsilon if self.learner is not None else 0.1
+        self.net.act(x, eps, seed=7, step=t, env_offset=self.env.env_offset,
                      actions=self.acts[b], synth=(2024, t) if self.fused else None)
         if before_step is not None:  # (parallel: the refill branch joins here)
             before_step()
@@ -623,6 +665,10 @@ class TrainSegment:
         b, nb = t % self.NB, (t + 1) % self.NB
         self.rb.add_many(self.obs[b], self.acts[b], self.rewards[b], self.obs[nb], self.dones[b])
 
+    def _learn(self):
+        if self.learner is not None:
+            self.learner.train(self.rb)
+
     def run(self):
         main = torch.cuda.current_stream(self.env.device)
         if not self.parallel:
@@ -631,6 +677,7 @@ class TrainSegment:
                     self._synth(t)
                 self._act_step(t)
                 self._replay(t)
+                self._learn()
         else:
             ev_syn = [torch.cuda.Event() for _ in range(self.seg)]
             ev_step = [torch.cuda.Event() for _ in range(self.seg)]
@@ -670,6 +717,9 @@ class TrainSegment:
                         self.s_rep.wait_event(ev_step[t])
                         self._replay(t)
                         ev_rep[t].record(self.s_rep)
+                    if self.learner is not None:  # samples the ring the add fills; the next act reads its net
+                        main.wait_event(ev_rep[t])
+                        self._learn()
                 main.wait_stream(self.s_syn)
                 main.wait_stream(self.s_rep)
                 main.wait_stream(self.s_ref)
@@ -681,13 +731,15 @@ class TrainSegment:
 
 
 def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fused: bool = True,
-                     precision: str = "f32", input: str = "obs"):
+                     precision: str = "f32", input: str = "obs", learn: bool = True):
     """TrainSegment captured once as a HIP graph (no host work per step) and
-    replayed.  Counters (action stream step, epsilon draws, replay cursor) are
-    baked into the capture, so replays repeat them: the work per step is the
-    same, the action stream repeats every segment."""
+    replayed.  The host-side counters (action stream step, exploration draws,
+    replay cursor) are baked into the capture, so replays repeat them: the
+    work per step is the same, the action stream repeats every segment.  The
+    learner's counters (step, Adam count, epsilon, sampled rows) live on the
+    device and continue across replays."""
     dev = env.device
-    loop = TrainSegment(env, seg, parallel=parallel, fused=fused, precision=precision, input=input)
+    loop = TrainSegment(env, seg, parallel=parallel, fused=fused, precision=precision, input=input, learn=learn)
     side = torch.cuda.Stream(dev)
     side.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(side):
@@ -709,15 +761,28 @@ def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fus
     loop.net.check_errors()  # (an f32 act's range flag lives in the net)
     dt = e0.elapsed_time(e1) / 1e3
     E = env.num_envs
+    lr = loop.learner
+    learner = None
+    if lr is not None:
+        c = lr.counters()
+        learner = {"batch": lr.hp.batch, "learning_rate": lr.hp.learning_rate, "gamma": lr.hp.gamma,
+                   "tau": lr.hp.tau, "target_update_interval": lr.hp.target_update_interval,
+                   "epsilon_decay_every": lr.hp.epsilon_decay_every, "epsilon_decay": lr.hp.decay(),
+                   "replay_capacity": loop.rb.capacity, "steps_taken": c["step"], "adam_steps": c["count"],
+                   "epsilon_after": c["epsilon"], "last_loss": c["loss"],
+                   "note": "drl_dqn_train every step: sample + train_step (TD-MSE backward) + optax Adam, target "
+                           "update and epsilon decay on the device (train_jax.py:68-98)"}
     branches = (("replay add_many" if fused else "synthetic actions and replay add_many") +
                 " on parallel graph branches, 3 rotating buffers" if parallel else "one stream") + \
         ("; synthetic actions inside the act launch" if fused else "")
     return {"env_steps_per_s": E * seg * reps / dt, "us_per_step": dt / (seg * reps) * 1e6,
             "segments": reps, "steps_per_segment": seg, "precision": precision, "input": input,
-            "loop": f"hipGraph of {seg} x [synth actions -> qnet act (drone 0, {precision}, input {input}) -> "
-                    f"step + {'drone 0 policy code' if input == 'code' else 'obs(K=1)'} -> "
-                    f"replay add_many{' (code rows)' if input == 'code' else ''}] + reset + obs, replayed {reps}x "
-                    f"({branches}; learner not included)"}
+            "learner": learner,
+            "loop": f"hipGraph of {seg} x [synth actions -> qnet act (drone 0, {precision}, input {input}, device "
+                    f"epsilon) -> step + {'drone 0 policy code' if input == 'code' else 'obs(K=1)'} -> "
+                    f"replay add_many{' (code rows)' if input == 'code' else ''} into {loop.rb.capacity} slots"
+                    f"{' -> learner (drl_dqn_train)' if learn else ''}] + reset + obs, replayed {reps}x "
+                    f"({branches}{'' if learn else '; learner not included'})"}
 
 
 def loop_input(args, env) -> str:
@@ -860,10 +925,11 @@ class StepRunner:
 
 def measure_copy_peak(dev, nbytes: int = 2 << 30, reps: int = 8):
     """the measured copy-kernel rate beside the 8 TB/s spec
-    (MI355X_MICROARCH.md: 6.29 TB/s for a float4 copy).  drl_hbm_probe (16-B
-    non-temporal accesses) over two 2-GiB buffers, past the 256-MiB Infinity
-    Cache, timed with HIP events on the launch stream: copy = GB/s of bytes
-    read + written, read = GB/s of a read-only pass."""
+    (MI355X_MICROARCH.md: 6.29 TB/s for a float4 copy).  drl_hbm_probe is that
+    plain float4 copy (one 16-B element per lane, a grid over the buffer),
+    run over two 2-GiB buffers (past the 256-MiB Infinity Cache); each launch
+    is timed alone with HIP events on the launch stream and the best one is
+    the rate: copy = GB/s of bytes read + written, read = a read-only pass."""
     from dronerl_amd._native import lib
     L = lib()
     a = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
@@ -876,18 +942,29 @@ def measure_copy_peak(dev, nbytes: int = 2 << 30, reps: int = 8):
         if run():
             raise RuntimeError(L.drl_last_error().decode())
         torch.cuda.synchronize(dev)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(st)
-        for _ in range(reps):
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for e0, e1 in ev:
+            e0.record(st)
             run()
-        e1.record(st)
+            e1.record(st)
         torch.cuda.synchronize(dev)
-        out[name] = mult * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+        best = min(e0.elapsed_time(e1) for e0, e1 in ev) / 1e3
+        out[name] = mult * nbytes / best / 1e9
     del a, b
     torch.cuda.empty_cache()
     return {"copy_GBs": out["copy"], "read_GBs": out["read"],
-            "note": f"in-run probe: drl_hbm_probe copy (read + write bytes) and read-only passes over {nbytes >> 20} "
-                    "MiB buffers (16-B non-temporal accesses) on this GPU"}
+            "note": f"in-run probe: drl_hbm_probe, a plain float4 copy (read + write bytes) and a read-only pass "
+                    f"over {nbytes >> 20} MiB buffers on this GPU, best of {reps} launches each"}
+
+
+def measured_peak(peak_measured, *rates):
+    """The measured HBM peak the *_vs_measured_peak fractions divide by: the
+    best of the probe's copy and read rates and of any kernel's own measured
+    traffic rate (a kernel that out-runs the probe sets the peak), so every
+    such fraction is <= 1 (tests/test_bench_contract.py)."""
+    cands = [("drl_hbm_probe copy", peak_measured["copy_GBs"]), ("drl_hbm_probe read", peak_measured["read_GBs"])]
+    cands += [(name, r) for name, r in rates if r]
+    return max(cands, key=lambda c: c[1])
 
 
 def roofline(E, R, Wb, launch_s, refill, traffic, G=None, peak_measured=None):
@@ -896,26 +973,32 @@ def roofline(E, R, Wb, launch_s, refill, traffic, G=None, peak_measured=None):
     launch duration (HIP events on the launch stream).  `traffic` = measured
     HBM bytes per launch (PMC); frac_measured = traffic / launch / peak, the
     fraction of the HBM peak the kernel actually moves (<= 1 by construction).
-    frac_ceiling = R / (R + W - G^2): the frac of a kernel that reads R and
-    writes only the outputs every step must write (observation, rewards,
-    dones, records), no ground write-back (the survey's W counts all G^2
-    ground bytes; a step writes only the changed cells), at the spec peak --
-    a true upper bound of frac.  peak_measured: the in-run copy probe
-    (frac_vs_measured_peak = achieved / its rate).  with_refill adds the
-    refill share per step."""
+    frac_ceiling = R / ((R - G^2/2) + (W - G^2)): the frac of a kernel that
+    moves only its obligatory bytes at the spec peak -- the ground as stored
+    (two cells per byte, ABI 8: R counts G^2 but G^2/2 are read), the outputs
+    every step must write (observation, rewards, dones, records), no ground
+    write-back (the survey's W counts all G^2 ground bytes; a step writes only
+    the changed cells).  It bounds frac for any launch at or below the spec
+    peak, and exceeds 1 where R's ground count exceeds the stored bytes (C5).
+    peak_measured: the in-run probe (measured_peak: frac_vs_measured_peak =
+    achieved / the best measured rate).  with_refill adds the refill share per
+    step."""
     achieved = E * R / launch_s / 1e9
-    ceiling = R / (R + Wb - (G * G if G else 0))
+    ceiling = R / (R - (G * G - (G * G + 1) // 2 if G else 0) + Wb - (G * G if G else 0))
     out = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
            "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": "drl_step_kernel",
            "avg_launch_us": launch_s * 1e6, "algorithmic_read_bytes_per_env_step": R,
            "algorithmic_write_bytes_per_env_step": Wb, "frac_ceiling": ceiling,
            "note": "frac counts SURVEY.md §8 D3's read bytes R only (achieved = E*R / avg drl_step launch); "
-                   "frac_ceiling = R/(R + W - G^2) bounds it (the obligatory outputs moved at the spec peak, no "
-                   "ground write-back). traffic = measured HBM bytes per drl_step launch (2*FETCH_SIZE + "
+                   "frac_ceiling = R/((R - G^2/2) + (W - G^2)) bounds it (the obligatory bytes -- the packed ground, "
+                   "the outputs -- moved at the spec peak, no ground write-back). traffic = measured HBM bytes per drl_step launch (2*FETCH_SIZE + "
                    "WRITE_SIZE), frac_measured = traffic / avg launch / peak"}
+    kernel_rate = traffic["drl_step_kernel"]["bytes_per_launch"] / launch_s / 1e9 if traffic else None
     if peak_measured:
-        out["peak_measured"] = peak_measured["copy_GBs"]
-        out["frac_vs_measured_peak"] = achieved / peak_measured["copy_GBs"]
+        src, peak = measured_peak(peak_measured, ("drl_step_kernel traffic", kernel_rate))
+        out["peak_measured"] = peak
+        out["peak_measured_source"] = src
+        out["frac_vs_measured_peak"] = achieved / peak
         out["peak_measured_detail"] = peak_measured
     per_step_s = launch_s + refill["per_step_us"] / 1e6
     out["with_refill"] = {"us_per_step": per_step_s * 1e6, "achieved": E * R / per_step_s / 1e9,
@@ -925,7 +1008,7 @@ def roofline(E, R, Wb, launch_s, refill, traffic, G=None, peak_measured=None):
         out["traffic"] = st["bytes_per_launch"]
         out["frac_measured"] = st["bytes_per_launch"] / launch_s / 1e9 / PEAK_HBM_GBS
         if peak_measured:
-            out["frac_measured_vs_measured_peak"] = st["bytes_per_launch"] / launch_s / 1e9 / peak_measured["copy_GBs"]
+            out["frac_measured_vs_measured_peak"] = kernel_rate / out["peak_measured"]
         out["traffic_detail"] = dict(st, source=traffic.get("source"), envs=traffic.get("envs"))
         rf = traffic.get("drl_refill_list_kernel") or traffic.get("drl_refill_kernel")
         if rf and refill["every"] > 0:

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # DRL_LIB: an alternative build of the same library (tools/variants.py A/B runs)
 LIB_PATH = os.environ.get("DRL_LIB") or os.path.join(_HERE, "libdronerl.so")
 
-DRL_ABI_VERSION = 8  # include/dronerl.h
+DRL_ABI_VERSION = 9  # include/dronerl.h
 DRL_MT_WORDS = 1776  # per-env RNG row: two MT blocks + the respawn-candidate ring
 DRL_MT_RING = 1248
 DRL_MT_RING_END = 1760
@@ -39,7 +39,9 @@ EXPORTS = ["drl_abi_version", "drl_last_error", "drl_side_from_density", "drl_la
            "drl_env_errors",
            # DQN consumer
            "drl_qnet_packed_bytes", "drl_qnet_pack", "drl_qnet_act", "drl_qnet_act_synth", "drl_qnet_act_code",
-           "drl_replay_add",
+           "drl_replay_add", "drl_qnet_act_eps",
+           # DQN learner (train_step / update_target / update_epsilon / sample)
+           "drl_dqn_layout_query", "drl_dqn_init", "drl_dqn_train",
            # measurement helper (the measured copy-kernel peak)
            "drl_hbm_probe"]
 

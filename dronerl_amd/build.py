@@ -14,7 +14,7 @@ LIB = os.path.join(HERE, "libdronerl.so")
 HASH = LIB + ".srchash"
 SOURCES = [os.path.join(CSRC, "dronerl_kernels.hip"), os.path.join(CSRC, "dronerl_api.cpp"),
            os.path.join(CSRC, "dronerl_env.cpp"), os.path.join(CSRC, "dronerl_qnet.hip"),
-           os.path.join(CSRC, "dronerl_qnet_api.cpp")]
+           os.path.join(CSRC, "dronerl_qnet_api.cpp"), os.path.join(CSRC, "dronerl_learn.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, "dronerl_internal.h"), os.path.join(REPO, "include", "dronerl.h")]
 ARCH = os.environ.get("DRL_OFFLOAD_ARCH", "gfx950")
 

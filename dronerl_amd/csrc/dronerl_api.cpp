@@ -516,9 +516,8 @@ int drl_hbm_probe(const void* d_src, void* d_dst, int64_t bytes, int32_t mode, h
     if (bytes <= 0 || bytes % 16) return fail("bytes must be a positive multiple of 16");
     if (!d_src || !d_dst) return fail("src / dst is NULL");
     if ((uintptr_t)d_src % 16 || (uintptr_t)d_dst % 16) return fail("src and dst must be 16-byte aligned");
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    hipError_t e = drl::launch_hbm_probe(d_src, d_dst, bytes, mode, cus > 0 ? cus : 256, stream);
+    if (bytes / 16 >= ((int64_t)1 << 40)) return fail("bytes too large");
+    hipError_t e = drl::launch_hbm_probe(d_src, d_dst, bytes, mode, 0, stream);
     return e == hipSuccess ? 0 : hip_fail(e, "drl_hbm_probe launch");
 }
 

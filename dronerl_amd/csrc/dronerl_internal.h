@@ -259,6 +259,7 @@ struct QnetPack {
 
 struct QnetArgs {
     int in_features, kt0, n_hidden, n_actions, precision;
+    const float* eps_ptr;           // non-NULL: epsilon read from device memory (drl_qnet_act_eps; a learner's counter)
     int nt[QN_MAX_LAYERS];
     int frag_off[QN_MAX_LAYERS], bias_off[QN_MAX_LAYERS];
     int frag_total, lds_vec, n_bias;
@@ -300,7 +301,100 @@ struct ReplayArgs {
     uint8_t* buf_dones;
 };
 
+// K index within a 32-wide slice of MFMA fragment element j for lane group g
+// (dronerl_qnet.hip's header comment).
+__host__ __device__ constexpr int qn_frag_k(int g, int j) { return j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4); }
+
+// Element e of layer l's hi fragments in drl_qnet_pack's numbering (fragment
+// m * kt + t, lane, j) -> the weight W_l[row][k] it holds.  k == -1: layer 0's
+// bias (the first padding slot of a code net's lane group 0); k outside
+// [0, in) or row >= out: a zero pad.  Every real weight has exactly one slot.
+struct PackSlot {
+    int row, k;
+};
+__host__ __device__ inline PackSlot qnet_pack_slot(int l, int64_t e, int kt, int code_w, int in) {
+    const int j = (int)(e & 7), lane = (int)((e >> 3) & 63);
+    const int64_t frag = e >> 9;
+    const int m = (int)(frag / kt), t = (int)(frag % kt);
+    const int c = lane & 15, g = lane >> 4;
+    PackSlot s{16 * m + c, 32 * t + qn_frag_k(g, j)};
+    if (l == 0 && code_w > 0) {  // the policy code's K order (lay::code_slot_*)
+        const int cpg = lay::code_cpg(code_w), cells = code_w * code_w, sl = 8 * t + j;
+        const int lc = lay::code_slot_cell(cpg, sl), ch = lay::code_slot_ch(cpg, sl);
+        const bool ok = sl < 6 * cpg && lc < cpg && g * cpg + lc < cells;
+        s.k = ok ? (g * cpg + lc) * 6 + ch : in;
+        if (g == 0 && sl == 6 * cpg) s.k = -1;
+    }
+    return s;
+}
+
+// Store weight w (W_l[row][k], or layer 0's bias for k == -1) at element e of
+// layer l's fragments as drl_qnet_pack does: a code net's charge-channel
+// weights carry the input's 1/100; DRL_QNET_F32 writes fp16 hi and lo =
+// fp16((w - hi) * 2^11) (|w| >= 65504 or NaN raises DRL_ERR_QNET_RANGE in the
+// packed net's status word), DRL_QNET_BF16 a bf16.
+__device__ __forceinline__ void qnet_pack_write(const QnetPack& p, int l, int64_t e, int k, float w) {
+    if (l == 0 && p.code_w > 0 && k >= 0 && k < p.in[l] && k % 6 == 4) w /= 100.0f;
+    if (p.precision == DRL_QNET_F32) {
+        if (!(__builtin_fabsf(w) < 65504.0f)) atomicOr(p.status, DRL_ERR_QNET_RANGE);
+        const _Float16 hi = (_Float16)w;
+        reinterpret_cast<_Float16*>(p.packed_w)[(int64_t)p.frag_off[l] * 8 + e] = hi;
+        reinterpret_cast<_Float16*>(p.packed_w)[(int64_t)p.frag_lo_off[l] * 8 + e] = (_Float16)((w - (float)hi) * 2048.0f);
+    } else {
+        reinterpret_cast<__bf16*>(p.packed_w)[(int64_t)p.frag_off[l] * 8 + e] = (__bf16)w;
+    }
+}
+
+// ----------------------------------------------------------- DQN learner ---
+// (dronerl_learn.hip; include/dronerl.h drl_dqn_*.)  Device counters of the
+// agent block: the layout include/dronerl.h documents as drl_dqn_counters.
+struct DqnCounters {
+    int32_t step, count;
+    float epsilon, loss;
+    double beta1_pow, beta2_pow;
+    int32_t arrive, trained, target_due;
+    float bc1, bc2;
+    int32_t pad[3];
+};
+static_assert(sizeof(DqnCounters) == 64, "drl_dqn_counters is 64 bytes");
+
+constexpr int DQN_MAX_BATCH = 64;
+constexpr int DQN_TILE = 16;  // layer-0 units per workgroup of the gradient kernel
+
+struct LearnArgs {
+    int n_layers, batch, code_w, trained, nblk0, tiles0, maxw;
+    int in[QN_MAX_LAYERS], out[QN_MAX_LAYERS];
+    int in4;                          // layer 0's input row stride in LDS / scratch (in[0] rounded up to 4)
+    int64_t woff[QN_MAX_LAYERS], boff[QN_MAX_LAYERS];  // float offsets of W_l / b_l in a parameter set
+    float* online;
+    float* target;
+    float* adam_m;
+    float* adam_v;
+    DqnCounters* ctr;
+    float* sx;                        // scratch: the online net's inputs X [batch][in4]
+    float* sz0;                       // scratch: layer-0 pre-activations [2 nets][batch][out0]
+    float* sh[QN_MAX_LAYERS];         // scratch: online hidden activations h_l [batch][out_l]
+    float* sd[QN_MAX_LAYERS];         // scratch: deltas dL/dz_l [batch][out_l]
+    // replay rows (buffers.py:79-93 sample)
+    const uint32_t* r_obs;
+    const uint32_t* r_next;
+    int64_t row_words;
+    const int32_t* r_act;
+    const float* r_rew;
+    const uint8_t* r_done;
+    int64_t size;
+    uint64_t seed;
+    // hyperparameters, as the f32 constants jax's weak typing makes of the python floats
+    float gamma, b1, b2, c1, c2, adam_eps, neg_lr, tau, one_minus_tau, eps_decay, eps_end, inv_batch;
+    double b1d, b2d;
+    int target_every, eps_every;
+    // the act kernels' packed image of the online net (drl_dqn_update_kernel refreshes it)
+    QnetPack pack;
+};
+
 hipError_t launch_qnet_pack(const QnetPack& p, hipStream_t s);
+hipError_t launch_dqn_train(const LearnArgs& a, size_t lds_grad, hipStream_t s);
+hipError_t launch_dqn_init(void* counters, float epsilon, hipStream_t s);
 hipError_t launch_qnet_act(const QnetArgs& a, int num_cus, hipStream_t s);
 hipError_t launch_qnet_act_code(const QnetArgs& a, int window, int num_cus, hipStream_t s);
 hipError_t launch_replay_add(const ReplayArgs& a, hipStream_t s);

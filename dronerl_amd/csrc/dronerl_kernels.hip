@@ -2474,44 +2474,32 @@ hipError_t launch_code_decode(const void* code, int64_t n, int W, float* obs, hi
 
 // ------------------------------------------------------------ HBM probe ---
 // SURVEY.md §8 D3's "measured copy-kernel" peak beside the 8 TB/s spec
-// (drl_hbm_probe): 16-B non-temporal loads (and stores for the copy), four
-// independent vectors in flight per lane, a grid of 8 workgroups of 256 lanes
-// per CU striding over the buffer.  The read form folds what it loads into
-// one word per lane so that the loads are not dead.
+// (drl_hbm_probe): the plain grid-sized float4 copy of MI355X_MICROARCH.md's
+// 6.29 TB/s figure -- one 16-B element per lane, ordinary loads and stores, a
+// grid covering the buffer.  The read form folds each element into a compare
+// whose (practically never taken) store stays inside dst's first `bytes`.
 template <bool COPY>
 __global__ void __launch_bounds__(256) drl_hbm_probe_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
                                                             int64_t n) {
-    const int64_t stride = (int64_t)gridDim.x * 256;
-    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    uint32_t fold = 0;
-    for (; i + 3 * stride < n; i += 4 * stride) {
-        u32x4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if constexpr (COPY) __builtin_nontemporal_store(v[u], dst + i + u * stride);
-            else fold ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-        }
-    }
-    for (; i < n; i += stride) {
-        const u32x4 v = __builtin_nontemporal_load(src + i);
-        if constexpr (COPY) __builtin_nontemporal_store(v, dst + i);
-        else fold ^= v.x ^ v.y ^ v.z ^ v.w;
-    }
-    if constexpr (!COPY) {
-        if (fold == 0x9e3779b9u) dst[blockIdx.x * 256 + threadIdx.x].x = fold;  // (practically never taken)
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const u32x4 v = src[i];
+    if constexpr (COPY) {
+        dst[i] = v;
+    } else {
+        if ((v.x ^ v.y ^ v.z ^ v.w) == 0x9e3779b9u) dst[i].x = v.x;
     }
 }
 
 hipError_t launch_hbm_probe(const void* src, void* dst, int64_t bytes, int mode, int num_cus, hipStream_t s) {
+    (void)num_cus;
     const int64_t n = bytes / 16;
-    const unsigned blocks = (unsigned)(8 * num_cus);
+    const dim3 grid((unsigned)((n + 255) / 256));
     if (mode == 0)
-        hipLaunchKernelGGL(drl_hbm_probe_kernel<true>, dim3(blocks), dim3(256), 0, s, static_cast<const u32x4*>(src),
+        hipLaunchKernelGGL(drl_hbm_probe_kernel<true>, grid, dim3(256), 0, s, static_cast<const u32x4*>(src),
                            static_cast<u32x4*>(dst), n);
     else
-        hipLaunchKernelGGL(drl_hbm_probe_kernel<false>, dim3(blocks), dim3(256), 0, s, static_cast<const u32x4*>(src),
+        hipLaunchKernelGGL(drl_hbm_probe_kernel<false>, grid, dim3(256), 0, s, static_cast<const u32x4*>(src),
                            static_cast<u32x4*>(dst), n);
     return hipGetLastError();
 }

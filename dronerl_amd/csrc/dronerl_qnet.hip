@@ -37,6 +37,10 @@ __device__ __forceinline__ uint64_t qn_splitmix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
+// The exploration rate: the argument, or the learner's device counter
+// (drl_qnet_act_eps).
+__device__ __forceinline__ float qn_eps(const QnetArgs& a) { return a.eps_ptr ? *a.eps_ptr : a.epsilon; }
+
 // K index within a 32-wide slice of fragment element j for lane group g (see
 // the header comment).
 __device__ __forceinline__ int frag_k(int g, int j) { return j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4); }
@@ -52,35 +56,14 @@ __global__ void drl_qnet_pack_kernel(QnetPack p) {
         int l = 0;
         while (l + 1 < p.n_layers && i >= (int64_t)p.frag_src[l + 1] * 8) ++l;
         const int64_t e = i - (int64_t)p.frag_src[l] * 8;  // element within the layer
-        const int j = (int)(e & 7), lane = (int)((e >> 3) & 63);
-        const int64_t frag = e >> 9;                       // m * kt + t
-        const int kt = p.kt[l];
-        const int m = (int)(frag / kt), t = (int)(frag % kt);
-        const int c = lane & 15, g = lane >> 4;
-        const int row = 16 * m + c;
-        int k = 32 * t + frag_k(g, j);
-        if (l == 0 && p.code_w > 0) {  // the policy code's K order (drl_qnet_act_code_kernel)
-            const int cpg = lay::code_cpg(p.code_w), cells = p.code_w * p.code_w, sl = 8 * t + j;
-            const int lc = lay::code_slot_cell(cpg, sl), ch = lay::code_slot_ch(cpg, sl);
-            const bool ok = sl < 6 * cpg && lc < cpg && g * cpg + lc < cells;
-            k = ok ? (g * cpg + lc) * 6 + ch : p.in[l];  // (in[l]: a zero weight)
-            // the first padding slot of lane group 0 carries the bias (input 1)
-            if (g == 0 && sl == 6 * cpg) k = -1;
-        }
-        float w = (row < p.out[l] && k >= 0 && k < p.in[l]) ? p.w[l][(int64_t)row * p.in[l] + k] : 0.0f;
-        if (k < 0) w = row < p.out[l] ? p.b[l][row] : 0.0f;
-        // the charge channel's 1/100 moves into its weights: the kernel feeds
-        // the integer charge (exact in fp16), so no input needs an x_lo product
-        if (l == 0 && p.code_w > 0 && k >= 0 && k < p.in[l] && k % 6 == 4) w /= 100.0f;
-        if (p.precision == DRL_QNET_F32) {  // hi = fp16(w), lo = fp16((w - hi) * 2^11), lo after the LDS image
-            if (!(__builtin_fabsf(w) < 65504.0f)) atomicOr(p.status, DRL_ERR_QNET_RANGE);  // 
-            const _Float16 hi = (_Float16)w;
-            reinterpret_cast<_Float16*>(p.packed_w)[(int64_t)p.frag_off[l] * 8 + e] = hi;
-            reinterpret_cast<_Float16*>(p.packed_w)[(int64_t)p.frag_lo_off[l] * 8 + e] =
-                (_Float16)((w - (float)hi) * 2048.0f);
-        } else {
-            reinterpret_cast<__bf16*>(p.packed_w)[(int64_t)p.frag_off[l] * 8 + e] = (__bf16)w;
-        }
+        // (a code net: layer 0 in the policy code's K order, its bias in the
+        // first padding slot of lane group 0 -- qnet_pack_slot)
+        const PackSlot s = qnet_pack_slot(l, e, p.kt[l], p.code_w, p.in[l]);
+        float w = (s.row < p.out[l] && s.k >= 0 && s.k < p.in[l]) ? p.w[l][(int64_t)s.row * p.in[l] + s.k] : 0.0f;
+        if (s.k < 0) w = s.row < p.out[l] ? p.b[l][s.row] : 0.0f;
+        // (the charge channel's 1/100 moves into its weights: the kernel feeds
+        // the integer charge, exact in fp16, so no input needs an x_lo product)
+        qnet_pack_write(p, l, e, s.k, w);
     } else if (i < p.n_wfrag_elems + p.n_bias) {
         const int64_t bi = i - p.n_wfrag_elems;
         int l = 0;
@@ -279,7 +262,7 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_kernel(QnetArgs a)
                 const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (ge << 8) ^ 0xa5ull));
                 const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
                 const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
-                a.actions[env * a.action_stride] = (u < a.epsilon) ? rnd : best;
+                a.actions[env * a.action_stride] = (u < qn_eps(a)) ? rnd : best;
                 if (a.q)
                     for (int i = 0; i < a.n_actions; ++i) a.q[env * a.n_actions + i] = q[i];
             }
@@ -529,7 +512,7 @@ __global__ void __launch_bounds__(64 * QN_WAVES) drl_qnet_act_f32_kernel(QnetArg
                 const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (ge << 8) ^ 0xa5ull));
                 const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
                 const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
-                a.actions[env * a.action_stride] = (u < a.epsilon) ? rnd : best;
+                a.actions[env * a.action_stride] = (u < qn_eps(a)) ? rnd : best;
                 if (a.q)
                     for (int i = 0; i < a.n_actions; ++i) a.q[env * a.n_actions + i] = q[i];
             }
@@ -884,7 +867,7 @@ __global__ void __launch_bounds__(64 * QN_CODE_MAXW) drl_qnet_act_code_kernel(Qn
             const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (ge << 8) ^ 0xa5ull));
             const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
             const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
-            a.actions[env * a.action_stride] = (u < a.epsilon) ? rnd : best;
+            a.actions[env * a.action_stride] = (u < qn_eps(a)) ? rnd : best;
 #ifndef DRL_QC_STAMPS
             if (a.q)
                 for (int i = 0; i < a.n_actions; ++i) a.q[env * a.n_actions + i] = q[i];
@@ -1151,7 +1134,7 @@ __global__ void __launch_bounds__(64 * QN_CODE2_WAVES) drl_qnet_act_code2_kernel
                 const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (ge << 8) ^ 0xa5ull));
                 const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
                 const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
-                a.actions[env * a.action_stride] = (u < a.epsilon) ? rnd : best;
+                a.actions[env * a.action_stride] = (u < qn_eps(a)) ? rnd : best;
 #ifndef DRL_QC_STAMPS
                 if (a.q)
                     for (int i = 0; i < a.n_actions; ++i) a.q[env * a.n_actions + i] = q[i];
@@ -1191,37 +1174,12 @@ __global__ void __launch_bounds__(64 * QN_CODE2_WAVES) drl_qnet_act_code2_kernel
     }
 }
 
-// ------------------------------------------------ act from the code, v3 ---
-// drl_qnet_act_code3_kernel: the benchmark nets (layer 0's hi + lo fragments
-// the LDS image, 8 unit tiles, two hidden layers, the second 16 * NT1 wide),
-// two 16-env tiles per wave as drl_qnet_act_code2_kernel, rebuilt around what
-// the ISA and per-phase stamps of that kernel showed (profiles/r04_act/): its
-// layer 0 ran at ~50 % of the MFMA pipe because, at 249 VGPRs, the compiler
-// could keep only two fragments in flight (read 2, wait, 4 MFMAs), and no
-// tile started before the whole 160 KB image had landed (~6k cycles).
-//  * One accumulator per (tile, unit tile): the lo weights are multiplied by
-//    x * 2^-11 (exact in fp16 for every input: 0, 1, a charge <= 100) into the
-//    hi product's accumulator, so layer 0 keeps 64 instead of 128 accumulator
-//    VGPRs.  The products are the same exact f32 values as before (hi * x and
-//    lo * x * 2^-11); only the f32 summation order differs (the Q tolerance of
-//    tests/test_policy_code.py applies unchanged).  Within a slice the 16 hi
-//    MFMAs come before the 16 lo ones, so an accumulator's two MFMAs are 16
-//    apart.
-//  * Fragment reads run QC3_PD steps ahead in a register ring (inline
-//    ds_read_b128 with explicit lgkmcnt waits: the compiler would otherwise
-//    put a vmcnt(0) for the LDS-DMA in front of the first LDS read and drain
-//    the whole staging before any MFMA).
-//  * The staging is issued in slice order (wave w copies unit tile w's hi and
-//    lo fragments of slice 0, 1, ...) and slice t's reads wait only for the
-//    DMAs of slices <= t (vmcnt) and a barrier: layer 0 starts after 16 KB.
-//  * Layer 1's fragments (from L2) are double-buffered per K-slice, the first
-//    slice's issued during layer 0's last slice; the output layer's fragments
-//    and biases during layer 1's last slice.
-#ifndef DRL_QC3_PD
-#define DRL_QC3_PD 8
-#endif
-constexpr int QC3_PD = DRL_QC3_PD;  // fragment reads in flight per wave (ring of QC3_PD + 2)
-
+// ------------------------------------- inline LDS reads of the code act ---
+// Helpers of drl_qnet_act_code4_kernel (round 3's v3 kernel, whose measured
+// lessons v4 builds on, is described in DESIGN.md; removed in round 5): a
+// compile-time loop, fragment reads as inline ds_read_b128 with explicit
+// lgkmcnt waits (the compiler would otherwise put a vmcnt(0) for the LDS-DMA
+// in front of the first LDS read and drain the whole staging before any MFMA).
 typedef uint32_t q3u4 __attribute__((ext_vector_type(4)));
 
 template <int I, int N, class F>
@@ -1246,312 +1204,6 @@ __device__ __forceinline__ f16x8 q3_f16(const q3u4 v) {
     f16x8 f;
     __builtin_memcpy(&f, &v, 16);
     return f;
-}
-
-template <int NT0, int WN, int NT1>
-__global__ void __launch_bounds__(64 * QN_CODE2_WAVES) drl_qnet_act_code3_kernel(QnetArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint4 wl[];
-    constexpr int TP = 2;
-    constexpr int CPG = lay::code_cpg(WN), CPG8 = lay::code_cpg8(WN), CELLS = WN * WN;
-    constexpr int NV = CPG8 / 8;                 // 16-B code vectors per lane group
-    constexpr int KP = lay::code_kt(WN);         // layer 0's K-slices
-    constexpr int KT1 = NT0 / 2, KT2 = NT1 / 2;  // K-slices of layer 1 and of the output layer
-    constexpr int STEPS = KP * 2 * NT0;          // layer-0 fragment reads per group: slice-major, hi then lo
-    constexpr int RS = QC3_PD + 2;               // ring slots (a slot is rewritten 2 steps after its MFMAs)
-    constexpr int FLO = NT0 * KP * 64;           // uint4 offset of the lo fragments (lo0_lds layout)
-    static_assert(8 * KP > 6 * CPG, "no padding slot for layer 0's bias");
-    static_assert(2 * FLO * 16 <= 160 * 1024, "layer 0 must fit the LDS");
-    static_assert(NT0 == QN_CODE2_WAVES, "wave w stages unit tile w's fragments");
-    // (the wave index through readfirstlane: group tests are then scalar branches, not exec-masked blocks)
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
-    const int c = lane & 15, g = lane >> 4;
-    const int64_t ntiles = (a.E + 15) / 16;
-    const int64_t ngroups = (ntiles + TP - 1) / TP;
-    const int64_t gstride = (int64_t)gridDim.x * nw;
-    constexpr float kLo = 1.0f / 2048.0f;
-    const int ncell_g = min(CPG, CELLS - g * CPG);
-    const uint4* const code = reinterpret_cast<const uint4*>(a.obs);
-    auto load_codes = [&](int64_t tile, uint32_t (&dst)[4 * NV]) __attribute__((always_inline)) {
-        const int64_t env = min(tile * 16 + c, a.E - 1);
-        const uint4* src = code + env * (4 * NV) + g * NV;
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            const uint4 q = src[v];
-            dst[4 * v + 0] = q.x;
-            dst[4 * v + 1] = q.y;
-            dst[4 * v + 2] = q.z;
-            dst[4 * v + 3] = q.w;
-        }
-    };
-    const int64_t grp0 = (int64_t)blockIdx.x * nw + wave;
-#ifdef DRL_QC_STAMPS
-    const uint64_t t_entry = __builtin_amdgcn_s_memtime();
-#endif
-    // staging in slice order: instruction 2t + h of wave w copies fragment (w, t) of set h (hi / lo).
-    // An LDS-DMA may land out of order with respect to a register load, so waiting for the codes
-    // costs a vmcnt(0) while any DMA is in flight: slices 0 and 1 go first, then the codes, one
-    // vmcnt(0) for all of them, then the other slices (they land while slices 0-1 compute).
-    auto dma = [&](int t) __attribute__((always_inline)) {
-#ifdef DRL_DIAG_QC3_NOSTAGE  // timing diagnostic (wrong results): no weight staging
-        return;
-#endif
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int v0 = h * FLO + (wave * KP + t) * 64;
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(a.packed + v0 + lane),
-                                             (__attribute__((address_space(3))) void*)(wl + v0), 16, 0, 0);
-        }
-    };
-    constexpr int KE = KP < 2 ? KP : 2;  // slices staged before the codes
-#pragma unroll
-    for (int t = 0; t < KE; ++t) dma(t);
-    __builtin_amdgcn_sched_barrier(0);
-    uint32_t cw[TP][4 * NV];
-#pragma unroll
-    for (int h = 0; h < TP; ++h) load_codes(TP * (grp0 < ngroups ? grp0 : 0) + h, cw[h]);
-#pragma unroll
-    for (int h = 0; h < TP; ++h)
-#pragma unroll
-        for (int i = 0; i < 4 * NV; ++i) asm volatile("s_waitcnt vmcnt(0)" : "+v"(cw[h][i]));
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int t = KE; t < KP; ++t) dma(t);
-    __builtin_amdgcn_sched_barrier(0);
-    // slice t readable: this wave's DMAs of slices <= t have landed (in-order vmcnt) and every wave's (barrier)
-    auto slice_ready = [&](auto t_c) __attribute__((always_inline)) {
-        constexpr int T = decltype(t_c)::value;
-        // (slices < KE landed with the codes' vmcnt(0))
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(T < KE ? 0 : 2 * (KP - 1 - T)) : "memory");
-    };
-    bool bad = false;
-    const auto pbuf = __builtin_amdgcn_make_buffer_rsrc((void*)a.packed, 0, a.total_bytes, 0x00020000);
-    const int lane16 = lane * 16;
-    auto frag_ld = [&](int frag_u4) __attribute__((always_inline)) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(pbuf, lane16, frag_u4 * 16, 0);
-        uint4 r;
-        __builtin_memcpy(&r, &v, 16);
-        return r;
-    };
-    auto bias4 = [&](int off) __attribute__((always_inline)) {
-        f32x4 r;
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(pbuf, 16 * g, a.bias_vec * 16 + off * 4, 0);
-        __builtin_memcpy(&r, &v, 16);
-        return r;
-    };
-    const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
-    const uint32_t base[3] = {(uint32_t)lane16, (uint32_t)lane16 + 65536u, (uint32_t)lane16 + 131072u};
-    // the B operands of slice t from the codes: x and x * 2^-11 (exact in fp16)
-    auto decode = [&](auto t_c, f16x8 (&bh)[TP], f16x8 (&bl)[TP]) __attribute__((always_inline)) {
-        constexpr int t = decltype(t_c)::value;
-#pragma unroll
-        for (int h = 0; h < TP; ++h) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int sl = 8 * t + j;  // compile-time slot
-                const int l = lay::code_slot_cell(CPG, sl), ch = lay::code_slot_ch(CPG, sl);
-                float x = (sl == 6 * CPG && g == 0) ? 1.0f : 0.0f;  // the bias slot (drl_qnet_pack)
-                if (sl < 6 * CPG) {
-                    const uint32_t cd = (cw[h][l >> 1] >> (16 * (l & 1))) & 0xffffu;
-                    x = l < ncell_g ? code_channel(cd, ch) : 0.0f;
-                }
-                bh[h][j] = (_Float16)x;
-            }
-            bl[h] = bh[h] * (_Float16)kLo;
-        }
-    };
-
-    bool first = true;
-    if (grp0 >= ngroups) {  // no group: still take part in the staging barriers
-        qc3_for<0, KP>([&](auto t_c) { slice_ready(t_c); });
-    }
-    for (int64_t grp = grp0; grp < ngroups; grp += gstride) {
-#ifdef DRL_QC_STAMPS
-        __builtin_amdgcn_sched_barrier(0);
-        const uint64_t ts0 = __builtin_amdgcn_s_memtime();
-#endif
-        const int64_t ngrp = grp + gstride;
-        f32x4 acc[TP][NT0];
-        f16x8 bh[2][TP], bl[2][TP];  // [slice parity][tile]
-        q3u4 ring[RS];
-        decode(std::integral_constant<int, 0>{}, bh[0], bl[0]);
-        // ---- layer 0, STEPS fragment reads QC3_PD ahead of their MFMAs
-        auto issue = [&](auto s_c) __attribute__((always_inline)) {
-            constexpr int S = decltype(s_c)::value;
-            if constexpr (S < STEPS) {
-                constexpr int t = S / (2 * NT0), hl = (S / NT0) & 1, m = S % NT0;
-                if constexpr (S % (2 * NT0) == 0) {
-                    if (first) slice_ready(std::integral_constant<int, t>{});
-                }
-#ifdef DRL_DIAG_QC3_HALFLDS  // timing diagnostic (wrong results): odd steps re-read the even step's fragment
-                if constexpr (S % 2 == 1) {
-                    ring[S % RS] = ring[(S - 1) % RS];
-                    asm volatile("ds_read_b32 %0, %1 offset:0" : "=v"(ring[S % RS][0]) : "v"(base[0]));
-                } else
-#endif
-                qc3_read<(hl * FLO + (m * KP + t) * 64) * 16>(ring[S % RS], base);
-            }
-        };
-        qc3_for<0, QC3_PD>([&](auto s_c) { issue(s_c); });
-        qc3_for<0, STEPS>([&](auto s_c) {
-            constexpr int S = decltype(s_c)::value;
-            constexpr int t = S / (2 * NT0), hl = (S / NT0) & 1, m = S % NT0;
-            constexpr int after = (S + QC3_PD - 1 < STEPS ? S + QC3_PD - 1 : STEPS - 1) - S;
-            qc3_wait<after>(ring[S % RS]);
-            const f16x8 w = q3_f16(ring[S % RS]);
-#pragma unroll
-            for (int h = 0; h < TP; ++h)
-#ifdef DRL_DIAG_QC3_NOMFMA  // timing diagnostic (wrong results): a VALU stand-in for each MFMA
-                acc[h][m] = ((t == 0 && hl == 0) ? z4 : acc[h][m]) + (float)w[h] * (float)(hl ? bl[t & 1][h] : bh[t & 1][h])[m];
-#else
-                acc[h][m] = MFMA_F16(w, hl ? bl[t & 1][h] : bh[t & 1][h], (t == 0 && hl == 0) ? z4 : acc[h][m], 0, 0, 0);
-#endif
-            issue(std::integral_constant<int, S + QC3_PD>{});
-            if constexpr (S % (2 * NT0) == 3 && t + 1 < KP) {  // the next slice's inputs, between MFMAs
-                decode(std::integral_constant<int, t + 1>{}, bh[(t + 1) & 1], bl[(t + 1) & 1]);
-                if constexpr (t + 2 == KP) {  // the codes are dead: the next group's in flight
-#pragma unroll
-                    for (int h = 0; h < TP; ++h) load_codes(TP * (ngrp < ngroups ? ngrp : grp) + h, cw[h]);
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        });
-        first = false;
-#ifdef DRL_QC_STAMPS
-        __builtin_amdgcn_sched_barrier(0);
-        const uint64_t ts1 = __builtin_amdgcn_s_memtime();
-#endif
-        // ---- layer 1 (bias folded into layer 0): fragments double-buffered per K-slice
-        uint4 f1[2][2][NT1];  // [buffer][hi / lo][unit tile]
-        auto ld1 = [&](int t, int b) __attribute__((always_inline)) {
-            const int fl = a.frag_off[1], flo = a.frag_lo_off[1];
-#pragma unroll
-            for (int m = 0; m < NT1; ++m) {
-                f1[b][0][m] = frag_ld(fl + (m * KT1 + t) * 64);
-                f1[b][1][m] = frag_ld(flo + (m * KT1 + t) * 64);
-            }
-        };
-        ld1(0, 0);
-        f16x8 ah[TP][KT1], al[TP][KT1];
-#pragma unroll
-        for (int h = 0; h < TP; ++h)
-#pragma unroll
-            for (int s2 = 0; s2 < KT1; ++s2) {
-                float v[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = fmaxf(acc[h][2 * s2 + (j >> 2)][j & 3], 0.0f);
-                split_f16(v, ah[h][s2], al[h][s2], bad);
-            }
-        f32x4 bcc[TP][NT1], bcl[TP][NT1];
-        uint4 f2h[KT2], f2l[KT2];
-        f32x4 b1[KT2][2], bq;
-#pragma unroll
-        for (int t = 0; t < KT1; ++t) {
-            if (t + 1 < KT1) {
-                ld1(t + 1, (t + 1) & 1);
-            } else {  // the output layer's fragments and biases
-                const int fl = a.frag_off[2], flo = a.frag_lo_off[2], bo = a.bias_off[1];
-#pragma unroll
-                for (int u = 0; u < KT2; ++u) {
-                    f2h[u] = frag_ld(fl + u * 64);
-                    f2l[u] = frag_ld(flo + u * 64);
-                    b1[u][0] = bias4(bo + 32 * u);
-                    b1[u][1] = bias4(bo + 32 * u + 16);
-                }
-                bq = bias4(a.bias_off[2]);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int m = 0; m < NT1; ++m) {
-                const f16x8 wh = as_f16x8(f1[t & 1][0][m]), wo = as_f16x8(f1[t & 1][1][m]);
-#pragma unroll
-                for (int h = 0; h < TP; ++h) {
-                    bcc[h][m] = MFMA_F16(wh, ah[h][t], t == 0 ? z4 : bcc[h][m], 0, 0, 0);
-                    bcl[h][m] = MFMA_F16(wh, al[h][t], t == 0 ? z4 : bcl[h][m], 0, 0, 0);
-                    bcl[h][m] = MFMA_F16(wo, ah[h][t], bcl[h][m], 0, 0, 0);
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-#ifdef DRL_QC_STAMPS
-        __builtin_amdgcn_sched_barrier(0);
-        const uint64_t ts2 = __builtin_amdgcn_s_memtime();
-#endif
-        // ---- the output layer and the epsilon-greedy act (drl_qnet_act_code2_kernel)
-#pragma unroll
-        for (int h = 0; h < TP; ++h) {
-            f16x8 ah2[KT2], al2[KT2];
-#pragma unroll
-            for (int s2 = 0; s2 < KT2; ++s2) {
-                float v[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int m = 2 * s2 + (j >> 2), i = j & 3;
-                    v[j] = fmaxf((bcc[h][m][i] + bcl[h][m][i] * kLo) + b1[s2][j >> 2][i], 0.0f);
-                }
-                split_f16(v, ah2[s2], al2[s2], bad);
-            }
-            f32x4 qc, ql;
-#pragma unroll
-            for (int t = 0; t < KT2; ++t) {
-                const f16x8 wh = as_f16x8(f2h[t]), wo = as_f16x8(f2l[t]);
-                qc = MFMA_F16(wh, ah2[t], t == 0 ? z4 : qc, 0, 0, 0);
-                ql = MFMA_F16(wh, al2[t], t == 0 ? z4 : ql, 0, 0, 0);
-                ql = MFMA_F16(wo, ah2[t], ql, 0, 0, 0);
-            }
-            float q[8];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float own = (qc[i] + ql[i] * kLo) + bq[i];
-                const float hi = __shfl(own, c + 16);
-                q[i] = own;
-                q[i + 4] = hi;
-            }
-            const int64_t env = (TP * grp + h) * 16 + c;
-            if (g == 0 && env < a.E) {
-                int best = 0;
-                for (int i = 1; i < a.n_actions; ++i) best = q[i] > q[best] ? i : best;
-                const uint64_t ge = (uint64_t)(a.env_offset + env);
-                const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (ge << 8) ^ 0xa5ull));
-                const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
-                const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
-                a.actions[env * a.action_stride] = (u < a.epsilon) ? rnd : best;
-#ifndef DRL_QC_STAMPS
-                if (a.q)
-                    for (int i = 0; i < a.n_actions; ++i) a.q[env * a.n_actions + i] = q[i];
-#endif
-            }
-        }
-#ifdef DRL_QC_STAMPS
-        __builtin_amdgcn_sched_barrier(0);
-        const uint64_t ts3 = __builtin_amdgcn_s_memtime();
-        if (lane == 0 && a.q) {
-            uint32_t* st = reinterpret_cast<uint32_t*>(a.q) + grp * 5;
-            st[0] = (uint32_t)(ts1 - ts0);
-            st[1] = (uint32_t)(ts2 - ts1);
-            st[2] = (uint32_t)(ts3 - ts2);
-            st[3] = (uint32_t)(ts0 - t_entry);
-            st[4] = (uint32_t)(ts3 - t_entry);
-        }
-#endif
-    }
-    bad |= lane == 0 && reinterpret_cast<const int32_t*>(a.packed + a.status_vec)[0] != 0;  // pack range flag
-    if (__ballot(bad) && lane == 0 && a.err) atomicOr(a.err, DRL_ERR_QNET_RANGE);
-    if (a.synth_n > 1) {  // as in drl_qnet_act_kernel (TP 16-env tiles per group)
-        const uint32_t nd = (uint32_t)a.synth_n - 1u;
-        const uint32_t per = (uint32_t)(TP * 16) * nd;
-        for (int64_t gg = grp0; gg < ngroups; gg += gstride) {
-            for (uint32_t k = (uint32_t)lane; k < per; k += 64u) {
-                const uint32_t el = k / nd;
-                const int64_t env = TP * 16 * gg + el;
-                const uint64_t drone = 1u + (k - el * nd);
-                if (env < a.E) {
-                    const uint64_t ctr = (a.synth_step << 40) ^ ((uint64_t)(a.env_offset + env) << 8) ^ drone;
-                    const uint64_t hh = qn_splitmix64(a.synth_seed ^ qn_splitmix64(ctr));
-                    a.actions[env * a.action_stride + (int64_t)drone] = (int32_t)(((hh >> 32) * 5ull) >> 32);
-                }
-            }
-        }
-    }
 }
 
 // ------------------------------------------------ act from the code, v4 ---
@@ -1900,7 +1552,7 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
             const uint64_t hsh = qn_splitmix64(a.seed ^ qn_splitmix64((a.step << 40) ^ (ge << 8) ^ 0xa5ull));
             const float u = (float)(hsh >> 40) * (1.0f / 16777216.0f);
             const int rnd = (int)(((hsh & 0xffffffffull) * (uint64_t)a.n_actions) >> 32);
-            explore = (u < a.epsilon) ? rnd : -1;
+            explore = (u < qn_eps(a)) ? rnd : -1;
         }
         uint4 f1[2][2][NT1];  // layer 1's fragments: [buffer][hi / lo][unit tile]
         uint4 f2h[KT2], f2l[KT2];  // the output layer's, and the biases
@@ -2275,25 +1927,21 @@ hipError_t launch_qnet_act_code(const QnetArgs& a, int window, int num_cus, hipS
 #define QN_CODE_LAUNCH(NT, W)                                                                                   \
     if (a.lo0_lds) hipLaunchKernelGGL((drl_qnet_act_code_kernel<NT, true, W, 0>), grid, block, lds, s, a);     \
     else hipLaunchKernelGGL((drl_qnet_act_code_kernel<NT, false, W, 0>), grid, block, lds, s, a)
-    static const int ver = [] {  // DRL_QN_CODE=2|3: an earlier kernel (A/B knob; DRL_QN_CODE3=0 = 2)
+    static const bool v2 = [] {  // DRL_QN_CODE=2: the two-tile kernel for the benchmark nets too (A/B knob)
         const char* e = getenv("DRL_QN_CODE");
-        const char* e3 = getenv("DRL_QN_CODE3");
-        if (e && (e[0] == '2' || e[0] == '3')) return e[0] - '0';
-        return (e3 && e3[0] == '0') ? 2 : 4;
+        return e && e[0] == '2';
     }();
-    const bool v3 = ver >= 3;
     const int64_t ng4 = (nt + 3) / 4;  // drl_qnet_act_code4_kernel: four tiles per wave, four waves per workgroup
     int64_t nb4 = (ng4 + QC4_WAVES - 1) / QC4_WAVES;
     if (nb4 > num_cus) nb4 = num_cus;
     const dim3 grid4((unsigned)nb4), block4(64 * QC4_WAVES);
-    // drl_qnet_act_code3_kernel: the lo0_lds layout (layer 0's hi then lo fragments from offset 0) with
-    // 8 waves of 128 units and a window whose layer 0 fits the LDS (5x5, 7x7)
-    const bool c4ok = a.E * (int64_t)lay::code_bytes(window) < (1ll << 31);  // (v4: 32-bit code offsets)
-    const bool c3ok = v3 && a.lo0_lds && a.frag_off[0] == 0 && window <= 7 &&
-                      a.frag_lo_off[0] == 8 * lay::code_kt(window) * 64 && blocks_ok(a);
+    // drl_qnet_act_code4_kernel: the lo0_lds layout (layer 0's hi then lo fragments from offset 0), 128 units,
+    // a window whose layer 0 fits the LDS (5x5, 7x7), 32-bit code offsets; drl_qnet_act_code2_kernel otherwise
+    const bool v4ok = !v2 && a.lo0_lds && a.frag_off[0] == 0 && window <= 7 &&
+                      a.frag_lo_off[0] == 8 * lay::code_kt(window) * 64 && blocks_ok(a) &&
+                      a.E * (int64_t)lay::code_bytes(window) < (1ll << 31);
 #define QN_CODE_SPEC(W)                                                                                         \
-    if (c3ok && W <= 7 && ver == 4 && c4ok) hipLaunchKernelGGL((drl_qnet_act_code4_kernel<8, (W <= 7 ? W : 7), 4>), grid4, block4, lds, s, a); \
-    else if (c3ok && W <= 7) hipLaunchKernelGGL((drl_qnet_act_code3_kernel<8, (W <= 7 ? W : 7), 4>), grid2, block2, lds, s, a); \
+    if (v4ok && W <= 7) hipLaunchKernelGGL((drl_qnet_act_code4_kernel<8, (W <= 7 ? W : 7), 4>), grid4, block4, lds, s, a); \
     else if (a.lo0_lds) hipLaunchKernelGGL((drl_qnet_act_code2_kernel<8, true, W, 4>), grid2, block2, lds, s, a);   \
     else hipLaunchKernelGGL((drl_qnet_act_code2_kernel<8, false, W, 4>), grid2, block2, lds, s, a)
     const bool spec = a.n_hidden == 2 && a.nt[0] == 8 && a.nt[1] == 4;  // 128 -> 64 hidden

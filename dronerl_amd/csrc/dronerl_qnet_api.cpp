@@ -130,6 +130,66 @@ int num_cus() {
     return cache[dev];
 }
 
+
+// The agent block of a learner (include/dronerl.h drl_dqn_layout), the scratch
+// regions of drl::LearnArgs, and the gradient launch's LDS.
+struct DqnPlan {
+    drl_dqn_layout pub;
+    int64_t sx, sz0, sh[drl::QN_MAX_LAYERS], sd[drl::QN_MAX_LAYERS];  // float offsets within the scratch
+    int in4, maxw, tiles0;
+    size_t lds;
+};
+
+static int64_t r4(int64_t v) { return (v + 3) / 4 * 4; }
+
+static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout& L, DqnPlan* P) {
+    if (batch < 1 || batch > drl::DQN_MAX_BATCH) return fail("batch must be in [1, 64]");
+    memset(P, 0, sizeof *P);
+    drl_dqn_layout& o = P->pub;
+    int64_t f = 0;
+    for (int l = 0; l < L.n_layers; ++l) {
+        o.weight_off[l] = f;
+        f += r4((int64_t)L.in[l] * L.out[l]);
+        o.bias_off[l] = f;
+        f += r4(L.out[l]);
+    }
+    o.n_params = f;
+    const int64_t set = f * 4;
+    o.online_off = 0;
+    o.target_off = set;
+    o.m_off = 2 * set;
+    o.v_off = 3 * set;
+    o.counters_off = 4 * set;
+    o.scratch_off = o.counters_off + (int64_t)sizeof(drl::DqnCounters);
+    P->in4 = (int)r4(L.in[0]);
+    int maxw = 0;
+    for (int l = 0; l < L.n_layers; ++l) maxw = L.out[l] > maxw ? L.out[l] : maxw;
+    P->maxw = (int)r4(maxw);
+    int64_t sc = 0;
+    P->sx = sc;
+    sc += r4((int64_t)batch * P->in4);
+    P->sz0 = sc;
+    sc += r4(2ll * batch * L.out[0]);
+    for (int l = 0; l + 1 < L.n_layers; ++l) {
+        P->sh[l] = sc;
+        sc += r4((int64_t)batch * L.out[l]);
+    }
+    for (int l = 0; l < L.n_layers; ++l) {
+        P->sd[l] = sc;
+        sc += r4((int64_t)batch * L.out[l]);
+    }
+    o.bytes = o.scratch_off + sc * 4;
+    P->tiles0 = (L.out[0] + drl::DQN_TILE - 1) / drl::DQN_TILE;
+    o.grad_workgroups = 2 * P->tiles0;
+    // layer 0 (X + the weight tile) and the last workgroup (activations of both nets twice + the ReLU masks)
+    const size_t a0 = (size_t)(batch + drl::DQN_TILE) * P->in4 * 4;
+    const size_t a1 = (size_t)4 * batch * P->maxw * 4 + (size_t)r4((int64_t)(L.n_layers - 1) * batch * P->maxw);
+    P->lds = a0 > a1 ? a0 : a1;
+    o.grad_lds_bytes = (int32_t)P->lds;
+    if (P->lds > 160 * 1024 - 1024) return fail("the learner's batch and widths do not fit the LDS of a CU");
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -142,42 +202,50 @@ int drl_qnet_packed_bytes(const drl_qnet_desc* d, int64_t* bytes) {
     return 0;
 }
 
+// The pack kernel's arguments for net layout L (weights / biases: nullable
+// source pointers; the learner's update kernel writes from its own sets).
+static void fill_pack(const drl::QnetLayout& L, void* d_packed, const float* const* w, const float* const* b,
+                      drl::QnetPack* p) {
+    memset(p, 0, sizeof *p);
+    p->n_layers = L.n_layers;
+    for (int l = 0; l < L.n_layers; ++l) {
+        p->frag_off[l] = L.frag_off[l];
+        p->frag_src[l] = L.frag_src[l];
+        p->kt[l] = L.kt[l];
+        p->in[l] = L.in[l];
+        p->out[l] = L.out[l];
+        p->bias_off[l] = L.bias_off[l];
+        p->w[l] = w ? w[l] : nullptr;
+        p->b[l] = b ? b[l] : nullptr;
+        p->frag_lo_off[l] = L.frag_lo_off[l];
+    }
+    p->precision = L.precision;
+    p->code_w = L.code_w;
+    p->status = reinterpret_cast<int32_t*>(static_cast<uint8_t*>(d_packed) + (size_t)L.status_vec * 16);
+    p->n_wfrag_elems = (int64_t)L.frag_total * 8;
+    p->n_bias = L.n_bias;
+    p->packed_w = static_cast<uint16_t*>(d_packed);
+    p->packed_b = reinterpret_cast<float*>(static_cast<uint8_t*>(d_packed) + (size_t)L.bias_vec * 16);
+}
+
 int drl_qnet_pack(const drl_qnet_desc* d, const float* const* d_weights, const float* const* d_biases, void* d_packed,
                   hipStream_t stream) {
     drl::QnetLayout L;
     if (qnet_layout(d, &L)) return -1;
     if (!d_weights || !d_biases || !d_packed) return fail("weights/biases/packed must be non-NULL");
     if ((uintptr_t)d_packed % 16) return fail("packed buffer must be 16-byte aligned");
-    drl::QnetPack p;
-    memset(&p, 0, sizeof p);
-    p.n_layers = L.n_layers;
-    for (int l = 0; l < L.n_layers; ++l) {
+    for (int l = 0; l < L.n_layers; ++l)
         if (!d_weights[l] || !d_biases[l]) return fail("a weight or bias pointer is NULL");
-        p.frag_off[l] = L.frag_off[l];
-        p.frag_src[l] = L.frag_src[l];
-        p.kt[l] = L.kt[l];
-        p.in[l] = L.in[l];
-        p.out[l] = L.out[l];
-        p.bias_off[l] = L.bias_off[l];
-        p.w[l] = d_weights[l];
-        p.b[l] = d_biases[l];
-    }
-    p.precision = L.precision;
-    p.code_w = L.code_w;
-    p.status = reinterpret_cast<int32_t*>(static_cast<uint8_t*>(d_packed) + (size_t)L.status_vec * 16);
+    drl::QnetPack p;
+    fill_pack(L, d_packed, d_weights, d_biases, &p);
     if (hipError_t e0 = hipMemsetAsync(p.status, 0, 16, stream); e0 != hipSuccess)
         return hip_fail(e0, "drl_qnet_pack status reset");
-    for (int l = 0; l < L.n_layers; ++l) p.frag_lo_off[l] = L.frag_lo_off[l];
-    p.n_wfrag_elems = (int64_t)L.frag_total * 8;
-    p.n_bias = L.n_bias;
-    p.packed_w = static_cast<uint16_t*>(d_packed);
-    p.packed_b = reinterpret_cast<float*>(static_cast<uint8_t*>(d_packed) + (size_t)L.bias_vec * 16);
     hipError_t e = drl::launch_qnet_pack(p, stream);
     return e == hipSuccess ? 0 : hip_fail(e, "drl_qnet_pack launch");
 }
 
 static int qnet_act_impl(const drl_qnet_desc* d, const void* d_packed, const float* d_obs, int64_t num_envs,
-                         int64_t obs_stride, float epsilon, uint64_t seed, uint64_t step, int64_t env_offset,
+                         int64_t obs_stride, float epsilon, const float* eps_ptr, uint64_t seed, uint64_t step, int64_t env_offset,
                          int32_t* d_actions, int64_t action_stride, float* d_q, int synth_n, uint64_t synth_seed,
                          uint64_t synth_step, int32_t* d_err, hipStream_t stream) {
     drl::QnetLayout L;
@@ -215,6 +283,7 @@ static int qnet_act_impl(const drl_qnet_desc* d, const void* d_packed, const flo
     a.obs_stride = obs_stride;
     a.E = num_envs;
     a.epsilon = epsilon;
+    a.eps_ptr = eps_ptr;
     a.seed = seed;
     a.step = step;
     a.env_offset = env_offset;
@@ -232,7 +301,7 @@ static int qnet_act_impl(const drl_qnet_desc* d, const void* d_packed, const flo
 int drl_qnet_act(const drl_qnet_desc* d, const void* d_packed, const float* d_obs, int64_t num_envs,
                  int64_t obs_stride, float epsilon, uint64_t seed, uint64_t step, int64_t env_offset,
                  int32_t* d_actions, int64_t action_stride, float* d_q, int32_t* d_err, hipStream_t stream) {
-    return qnet_act_impl(d, d_packed, d_obs, num_envs, obs_stride, epsilon, seed, step, env_offset, d_actions,
+    return qnet_act_impl(d, d_packed, d_obs, num_envs, obs_stride, epsilon, nullptr, seed, step, env_offset, d_actions,
                          action_stride, d_q, 0, 0, 0, d_err, stream);
 }
 
@@ -241,14 +310,14 @@ int drl_qnet_act_synth(const drl_qnet_desc* d, const void* d_packed, const float
                        int32_t* d_actions, int32_t n_drones, uint64_t synth_seed, uint64_t synth_step, float* d_q,
                        int32_t* d_err, hipStream_t stream) {
     if (n_drones < 1 || n_drones > 255) return fail("n_drones must be in [1, 255]");
-    return qnet_act_impl(d, d_packed, d_obs, num_envs, obs_stride, epsilon, seed, step, env_offset, d_actions,
+    return qnet_act_impl(d, d_packed, d_obs, num_envs, obs_stride, epsilon, nullptr, seed, step, env_offset, d_actions,
                          n_drones, d_q, n_drones, synth_seed, synth_step, d_err, stream);
 }
 
-int drl_qnet_act_code(const drl_qnet_desc* d, const void* d_packed, const void* d_code, int64_t num_envs,
-                      float epsilon, uint64_t seed, uint64_t step, int64_t env_offset, int32_t* d_actions,
-                      int64_t action_stride, int32_t synth_n, uint64_t synth_seed, uint64_t synth_step, float* d_q,
-                      int32_t* d_err, hipStream_t stream) {
+static int qnet_act_code_impl(const drl_qnet_desc* d, const void* d_packed, const void* d_code, int64_t num_envs,
+                              float epsilon, const float* eps_ptr, uint64_t seed, uint64_t step, int64_t env_offset,
+                              int32_t* d_actions, int64_t action_stride, int32_t synth_n, uint64_t synth_seed,
+                              uint64_t synth_step, float* d_q, int32_t* d_err, hipStream_t stream) {
     drl::QnetLayout L;
     if (qnet_layout(d, &L)) return -1;
     if (!L.code_w) return fail("drl_qnet_act_code needs a DRL_QNET_INPUT_CODE net");
@@ -282,6 +351,7 @@ int drl_qnet_act_code(const drl_qnet_desc* d, const void* d_packed, const void* 
     a.obs = static_cast<const float*>(d_code);
     a.E = num_envs;
     a.epsilon = epsilon;
+    a.eps_ptr = eps_ptr;
     a.seed = seed;
     a.step = step;
     a.env_offset = env_offset;
@@ -295,6 +365,33 @@ int drl_qnet_act_code(const drl_qnet_desc* d, const void* d_packed, const void* 
     a.total_bytes = L.total_vec * 16;
     hipError_t e = drl::launch_qnet_act_code(a, L.code_w, num_cus(), stream);
     return e == hipSuccess ? 0 : hip_fail(e, "drl_qnet_act_code launch");
+}
+
+int drl_qnet_act_code(const drl_qnet_desc* d, const void* d_packed, const void* d_code, int64_t num_envs,
+                      float epsilon, uint64_t seed, uint64_t step, int64_t env_offset, int32_t* d_actions,
+                      int64_t action_stride, int32_t synth_n, uint64_t synth_seed, uint64_t synth_step, float* d_q,
+                      int32_t* d_err, hipStream_t stream) {
+    return qnet_act_code_impl(d, d_packed, d_code, num_envs, epsilon, nullptr, seed, step, env_offset, d_actions,
+                              action_stride, synth_n, synth_seed, synth_step, d_q, d_err, stream);
+}
+
+int drl_qnet_act_eps(const drl_qnet_desc* d, const void* d_packed, const void* d_input, int64_t num_envs,
+                     int64_t obs_stride, const float* d_epsilon, uint64_t seed, uint64_t step, int64_t env_offset,
+                     int32_t* d_actions, int64_t action_stride, int32_t synth_n, uint64_t synth_seed,
+                     uint64_t synth_step, float* d_q, int32_t* d_err, hipStream_t stream) {
+    if (!d_epsilon) return fail("d_epsilon is NULL");
+    if ((uintptr_t)d_epsilon % 4) return fail("d_epsilon must be 4-byte aligned");
+    if (!d || d->input != DRL_QNET_INPUT_CODE) {
+        if (synth_n > 1) {
+            if (synth_n > 255) return fail("n_drones must be in [1, 255]");
+            if (action_stride < synth_n) return fail("action_stride must be >= synth_n");
+        }
+        return qnet_act_impl(d, d_packed, static_cast<const float*>(d_input), num_envs, obs_stride, 0.0f, d_epsilon,
+                             seed, step, env_offset, d_actions, action_stride, d_q, synth_n > 1 ? synth_n : 0,
+                             synth_seed, synth_step, d_err, stream);
+    }
+    return qnet_act_code_impl(d, d_packed, d_input, num_envs, 0.0f, d_epsilon, seed, step, env_offset, d_actions,
+                              action_stride, synth_n, synth_seed, synth_step, d_q, d_err, stream);
 }
 
 int drl_replay_add(const drl_replay* r, int64_t cursor, int64_t n, const float* d_obs, int64_t obs_stride,
@@ -338,6 +435,112 @@ int drl_replay_add(const drl_replay* r, int64_t cursor, int64_t n, const float* 
     a.buf_dones = r->dones;
     hipError_t e = drl::launch_replay_add(a, stream);
     return e == hipSuccess ? 0 : hip_fail(e, "drl_replay_add launch");
+}
+
+int drl_dqn_layout_query(const drl_qnet_desc* d, int32_t batch, drl_dqn_layout* layout) {
+    drl::QnetLayout L;
+    if (qnet_layout(d, &L)) return -1;
+    if (!layout) return fail("layout is NULL");
+    DqnPlan P;
+    if (dqn_plan(d, batch, L, &P)) return -1;
+    *layout = P.pub;
+    return 0;
+}
+
+int drl_dqn_init(const drl_qnet_desc* d, int32_t batch, void* d_agent, float epsilon_start, hipStream_t stream) {
+    drl::QnetLayout L;
+    if (qnet_layout(d, &L)) return -1;
+    DqnPlan P;
+    if (dqn_plan(d, batch, L, &P)) return -1;
+    if (!d_agent || (uintptr_t)d_agent % 16) return fail("the agent block must be a 16-byte aligned device pointer");
+    uint8_t* base = static_cast<uint8_t*>(d_agent);
+    const size_t set = (size_t)P.pub.n_params * 4;
+    if (hipError_t e = hipMemsetAsync(base + P.pub.m_off, 0, 2 * set, stream); e != hipSuccess)
+        return hip_fail(e, "drl_dqn_init moments");
+    hipError_t e = drl::launch_dqn_init(base + P.pub.counters_off, epsilon_start, stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_dqn_init launch");
+}
+
+int drl_dqn_train(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agent, void* d_packed, const drl_replay* r,
+                  int64_t size, hipStream_t stream) {
+    drl::QnetLayout L;
+    if (qnet_layout(d, &L)) return -1;
+    if (!h) return fail("hparams is NULL");
+    DqnPlan P;
+    if (dqn_plan(d, h->batch, L, &P)) return -1;
+    if (h->target_update_interval < 1 || h->epsilon_decay_every < 1)
+        return fail("target_update_interval and epsilon_decay_every must be >= 1");
+    if (!(h->beta1 >= 0.0 && h->beta1 < 1.0 && h->beta2 >= 0.0 && h->beta2 < 1.0))
+        return fail("beta1 and beta2 must be in [0, 1)");
+    if (!d_agent || (uintptr_t)d_agent % 16) return fail("the agent block must be a 16-byte aligned device pointer");
+    if (!d_packed || (uintptr_t)d_packed % 16) return fail("packed buffer must be a 16-byte aligned device pointer");
+    if (!r || !r->obs || !r->next_obs || !r->actions || !r->rewards || !r->dones) return fail("replay buffers are NULL");
+    if (r->capacity < 1 || r->capacity >= ((int64_t)1 << 31)) return fail("replay capacity must be in [1, 2^31)");
+    if (size < 0 || size > r->capacity) return fail("size must be in [0, capacity]");
+    if (L.code_w) {
+        if ((int64_t)r->obs_floats * 4 != drl::lay::code_bytes(L.code_w))
+            return fail("a DRL_QNET_INPUT_CODE net's replay rows are policy codes (drl_policy_code_bytes / 4 words)");
+    } else if (r->obs_floats < d->in_features) {
+        return fail("replay obs_floats < in_features");
+    }
+    if ((uintptr_t)r->obs % 4 || (uintptr_t)r->next_obs % 4) return fail("replay rows must be 4-byte aligned");
+    uint8_t* base = static_cast<uint8_t*>(d_agent);
+    drl::LearnArgs a;
+    memset(&a, 0, sizeof a);
+    a.n_layers = L.n_layers;
+    a.batch = h->batch;
+    a.code_w = L.code_w;
+    a.trained = size >= h->batch;  // buffers.py:92-93 can_sample
+    a.tiles0 = P.tiles0;
+    a.nblk0 = 2 * P.tiles0;
+    a.maxw = P.maxw;
+    a.in4 = P.in4;
+    for (int l = 0; l < L.n_layers; ++l) {
+        a.in[l] = L.in[l];
+        a.out[l] = L.out[l];
+        a.woff[l] = P.pub.weight_off[l];
+        a.boff[l] = P.pub.bias_off[l];
+    }
+    a.online = reinterpret_cast<float*>(base + P.pub.online_off);
+    a.target = reinterpret_cast<float*>(base + P.pub.target_off);
+    a.adam_m = reinterpret_cast<float*>(base + P.pub.m_off);
+    a.adam_v = reinterpret_cast<float*>(base + P.pub.v_off);
+    a.ctr = reinterpret_cast<drl::DqnCounters*>(base + P.pub.counters_off);
+    float* sc = reinterpret_cast<float*>(base + P.pub.scratch_off);
+    a.sx = sc + P.sx;
+    a.sz0 = sc + P.sz0;
+    for (int l = 0; l < L.n_layers; ++l) {
+        a.sh[l] = l + 1 < L.n_layers ? sc + P.sh[l] : nullptr;
+        a.sd[l] = sc + P.sd[l];
+    }
+    a.r_obs = reinterpret_cast<const uint32_t*>(r->obs);
+    a.r_next = reinterpret_cast<const uint32_t*>(r->next_obs);
+    a.row_words = r->obs_floats;
+    a.r_act = r->actions;
+    a.r_rew = r->rewards;
+    a.r_done = r->dones;
+    a.size = size;
+    a.seed = h->sample_seed;
+    // the python floats as jax's weak typing rounds them into f32 arithmetic
+    a.gamma = (float)h->gamma;
+    a.b1 = (float)h->beta1;
+    a.b2 = (float)h->beta2;
+    a.c1 = (float)(1.0 - h->beta1);
+    a.c2 = (float)(1.0 - h->beta2);
+    a.adam_eps = (float)h->adam_eps;
+    a.neg_lr = (float)(-h->learning_rate);
+    a.tau = (float)h->tau;
+    a.one_minus_tau = (float)(1.0 - h->tau);
+    a.eps_decay = (float)h->epsilon_decay;
+    a.eps_end = (float)h->epsilon_end;
+    a.inv_batch = 1.0f / (float)h->batch;
+    a.b1d = h->beta1;
+    a.b2d = h->beta2;
+    a.target_every = h->target_update_interval;
+    a.eps_every = h->epsilon_decay_every;
+    fill_pack(L, d_packed, nullptr, nullptr, &a.pack);
+    hipError_t e = drl::launch_dqn_train(a, P.lds, stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_dqn_train launch");
 }
 
 }  // extern "C"

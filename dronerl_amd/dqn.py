@@ -42,6 +42,21 @@ class DrlReplay(ctypes.Structure):
                 ("dones", ctypes.c_void_p)]
 
 
+class DrlDqnHParams(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int32), ("target_update_interval", ctypes.c_int32),
+                ("epsilon_decay_every", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("gamma", ctypes.c_double), ("learning_rate", ctypes.c_double), ("beta1", ctypes.c_double),
+                ("beta2", ctypes.c_double), ("adam_eps", ctypes.c_double), ("tau", ctypes.c_double),
+                ("epsilon_decay", ctypes.c_double), ("epsilon_end", ctypes.c_double), ("sample_seed", ctypes.c_uint64)]
+
+
+class DrlDqnLayout(ctypes.Structure):
+    _fields_ = [("n_params", ctypes.c_int64), ("weight_off", ctypes.c_int64 * 4), ("bias_off", ctypes.c_int64 * 4),
+                ("online_off", ctypes.c_int64), ("target_off", ctypes.c_int64), ("m_off", ctypes.c_int64),
+                ("v_off", ctypes.c_int64), ("counters_off", ctypes.c_int64), ("scratch_off", ctypes.c_int64),
+                ("bytes", ctypes.c_int64), ("grad_workgroups", ctypes.c_int32), ("grad_lds_bytes", ctypes.c_int32)]
+
+
 _vp = ctypes.c_void_p
 
 
@@ -57,6 +72,10 @@ def _bind(L):
         "drl_qnet_act_synth": [D, _vp, _vp, i64, i64, f32, u64, u64, i64, _vp, i32, u64, u64, _vp, _vp, _vp],
         "drl_qnet_act_code": [D, _vp, _vp, i64, f32, u64, u64, i64, _vp, i64, i32, u64, u64, _vp, _vp, _vp],
         "drl_replay_add": [ctypes.POINTER(DrlReplay), i64, i64, _vp, i64, _vp, i64, _vp, i64, _vp, i64, _vp, i64, _vp],
+        "drl_qnet_act_eps": [D, _vp, _vp, i64, i64, _vp, u64, u64, i64, _vp, i64, i32, u64, u64, _vp, _vp, _vp],
+        "drl_dqn_layout_query": [D, i32, ctypes.POINTER(DrlDqnLayout)],
+        "drl_dqn_init": [D, i32, _vp, f32, _vp],
+        "drl_dqn_train": [D, ctypes.POINTER(DrlDqnHParams), _vp, _vp, ctypes.POINTER(DrlReplay), i64, _vp],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -145,11 +164,16 @@ class QNetwork:
         self.pack()
 
     def pack(self):
+        for t in (*self.weights, *self.biases):
+            if not bool(torch.isfinite(t).all()):
+                raise ValueError("weights and biases must be finite")
         if self.precision == "f32":  # fp16 hi/lo split range (include/dronerl.h DRL_QNET_F32)
-            for w, b in zip(self.weights, self.biases):  # (a code net splits layer 0's bias too: ADVICE r3)
-                for t in (w, b):
-                    if not bool(torch.isfinite(t).all()) or float(t.abs().max()) >= 65504.0:
-                        raise ValueError("f32 precision needs finite weights and biases with |w| < 65504")
+            # the weights are split into fp16 pieces, and so is a code net's
+            # layer-0 bias (packed as a weight); every other bias stays f32
+            split = list(self.weights) + ([self.biases[0]] if self.input == "code" else [])
+            for t in split:
+                if float(t.abs().max()) >= 65504.0:
+                    raise ValueError("f32 precision needs |w| < 65504 (and |b| < 65504 for a code net's layer 0)")
         n = len(self.weights)
         wp = (_vp * n)(*[w.data_ptr() for w in self.weights])
         bp = (_vp * n)(*[b.data_ptr() for b in self.biases])
@@ -167,7 +191,7 @@ class QNetwork:
                 x = r(torch.relu(x))
         return x
 
-    def act(self, obs: torch.Tensor, epsilon: float, seed: int = 0, step: int = 0, env_offset: int = 0,
+    def act(self, obs: torch.Tensor, epsilon, seed: int = 0, step: int = 0, env_offset: int = 0,
             actions: Optional[torch.Tensor] = None, q_out: Optional[torch.Tensor] = None,
             synth: Optional[Tuple[int, int]] = None) -> torch.Tensor:
         """Epsilon-greedy action for each row of obs [E, ..., in_features]
@@ -175,7 +199,9 @@ class QNetwork:
         `actions` may be an [E, n_drones] int32 tensor: column 0 is written (the
         other drones keep their actions, train_jax.py:47-49).  synth=(seed,
         step): the other columns get BatchedDeliveryDrones.synth_actions(seed,
-        step)'s values in the same launch (drl_qnet_act_synth)."""
+        step)'s values in the same launch (drl_qnet_act_synth).  epsilon: a
+        float, or a float32 device tensor of one element read by the kernel
+        (DQNLearner.epsilon: the learner's decaying schedule; drl_qnet_act_eps)."""
         E = obs.shape[0]
         if self.input == "code":
             _on(obs, self.device, torch.uint8, "code")
@@ -196,6 +222,18 @@ class QNetwork:
             if tuple(q_out.shape) != (E, self.n_actions) or not q_out.is_contiguous():
                 raise ValueError(f"q_out must be a contiguous float32 [{E}, {self.n_actions}] tensor")
         stride_a = actions.shape[1] if actions.dim() == 2 else 1
+        if isinstance(epsilon, torch.Tensor):
+            _on(epsilon, self.device, torch.float32, "epsilon")
+            if epsilon.numel() != 1:
+                raise ValueError("a device epsilon must be one float32 element")
+            sn, ss, st = (stride_a, synth[0] & (2**64 - 1), synth[1]) if synth is not None else (0, 0, 0)
+            x = obs if self.input == "code" else flat
+            _check(self.L, self.L.drl_qnet_act_eps(
+                ctypes.byref(self.desc), _vp(self.packed.data_ptr()), _vp(x.data_ptr()), E,
+                0 if self.input == "code" else flat.stride(0), _vp(epsilon.data_ptr()), seed & (2**64 - 1), step,
+                env_offset, _vp(actions.data_ptr()), stride_a, sn, ss, st,
+                None if q_out is None else _vp(q_out.data_ptr()), _vp(self.err.data_ptr()), _stream(self.device)))
+            return actions
         if self.input == "code":
             sn, ss, st = (stride_a, synth[0] & (2**64 - 1), synth[1]) if synth is not None else (0, 0, 0)
             _check(self.L, self.L.drl_qnet_act_code(
@@ -330,3 +368,118 @@ class ReplayBuffer:
             next_obs = decode_policy_code(next_obs, self.code_radius)
         return dict(obs=obs, actions=self.actions[idx], rewards=self.rewards[idx],
                     next_obs=next_obs, dones=self.dones[idx])
+
+
+@dataclass
+class DQNHParams:
+    """The learner's hyperparameters: jax_impl/agents/dqn.py DQNAgentParams
+    (:20-33) with train_jax.py's defaults (:349-360) and optax.adam's
+    (b1 0.9, b2 0.999, eps 1e-8).  `epsilon_decay` None: train_jax.py:133-134's
+    value for `num_steps` (half the way to epsilon_end after 20 % of them)."""
+    batch: int = 8
+    gamma: float = 0.9
+    learning_rate: float = 1e-3
+    beta1: float = 0.9
+    beta2: float = 0.999
+    adam_eps: float = 1e-8
+    tau: float = 1.0
+    target_update_interval: int = 10
+    epsilon_start: float = 1.0
+    epsilon_decay: Optional[float] = None
+    epsilon_end: float = 0.01
+    epsilon_decay_every: int = 5
+    num_steps: int = 1000
+    sample_seed: int = 0
+
+    def decay(self) -> float:
+        if self.epsilon_decay is not None:
+            return self.epsilon_decay
+        return (1 - 0.5 * (1 - self.epsilon_end / self.epsilon_start)) ** (1 / (0.2 * self.num_steps))
+
+    def c(self) -> DrlDqnHParams:
+        return DrlDqnHParams(self.batch, self.target_update_interval, self.epsilon_decay_every, 0, self.gamma,
+                             self.learning_rate, self.beta1, self.beta2, self.adam_eps, self.tau, self.decay(),
+                             self.epsilon_end, self.sample_seed & (2**64 - 1))
+
+
+class DQNLearner:
+    """jax_impl/agents/dqn.py DQNAgent's training state on the device: the
+    online net (`net`, whose weights become views of the agent block), a target
+    net, Adam's moments and the counters (step, Adam count, epsilon) -- one
+    agent block (include/dronerl.h drl_dqn_layout).  `train(rb)` is the
+    learner block of one train_jax.py scan step (:68-98): sample + train_step
+    when the buffer can sample, the target update every
+    target_update_interval steps, the epsilon decay every epsilon_decay_every
+    steps, step + 1 -- all on the device (drl_dqn_train), the packed net the
+    act reads refreshed in the same call.  `epsilon` is a device scalar to
+    pass to QNetwork.act.
+
+    target: the target net's initial (weights, biases) (torch layout); the
+    reference initialises it from its own key (dqn.py:119-121), so by default
+    it is a fresh random init from `generator`."""
+
+    def __init__(self, net: QNetwork, hp: Optional[DQNHParams] = None, target=None,
+                 generator: Optional[torch.Generator] = None):
+        self.net, self.hp = net, hp or DQNHParams()
+        self.L = net.L
+        lay = DrlDqnLayout()
+        _check(self.L, self.L.drl_dqn_layout_query(ctypes.byref(net.desc), self.hp.batch, ctypes.byref(lay)))
+        self.layout = lay
+        dev = net.device
+        self.block = torch.zeros(lay.bytes, dtype=torch.uint8, device=dev)
+        n = lay.n_params
+
+        def fset(off):
+            return self.block[off:off + 4 * n].view(torch.float32)
+
+        self.sets = {k: fset(getattr(lay, k + "_off")) for k in ("online", "target", "m", "v")}
+        ctr = self.block[lay.counters_off:lay.counters_off + 64]
+        self._ctr_f = ctr.view(torch.float32)
+        self._ctr_i = ctr.view(torch.int32)
+        self.epsilon = self._ctr_f[2:3]  # drl_dqn_counters.epsilon
+        shapes = [(w.shape, b.shape) for w, b in zip(net.weights, net.biases)]
+        if target is None:
+            g = generator if generator is not None else torch.Generator().manual_seed(1)
+            tw = []
+            for ws, _ in shapes:
+                std = (2.0 / ws[1]) ** 0.5 if len(tw) < len(shapes) - 1 else (1.0 / ws[1]) ** 0.5
+                tw.append(torch.randn(ws, generator=g) * std)
+            target = (tw, [torch.zeros(bs) for _, bs in shapes])
+        for l, (ws, bs) in enumerate(shapes):
+            self.params("online")[l][0].copy_(net.weights[l])
+            self.params("online")[l][1].copy_(net.biases[l])
+            self.params("target")[l][0].copy_(target[0][l].to(dev, torch.float32))
+            self.params("target")[l][1].copy_(target[1][l].to(dev, torch.float32))
+        online = self.params("online")
+        net.weights = [w for w, _ in online]  # the net now reads the live parameters
+        net.biases = [b for _, b in online]
+        net.pack()
+        _check(self.L, self.L.drl_dqn_init(ctypes.byref(net.desc), self.hp.batch, _vp(self.block.data_ptr()),
+                                           float(self.hp.epsilon_start), _stream(dev)))
+        self._hp = self.hp.c()
+
+    def params(self, which: str):
+        """[(W [out][in], b [out])] views of one parameter set ("online",
+        "target", "m", "v")."""
+        s, lay = self.sets[which], self.layout
+        out = []
+        for l, (w, b) in enumerate(zip(self.net.weights, self.net.biases)):
+            wo, bo = lay.weight_off[l], lay.bias_off[l]
+            out.append((s[wo:wo + w.numel()].view(w.shape), s[bo:bo + b.numel()]))
+        return out
+
+    def train(self, rb: "ReplayBuffer"):
+        """One learner block (train_jax.py:68-98) on the replay's current
+        contents (rb.size transitions)."""
+        if rb.obs.device != self.block.device:
+            raise ValueError("the replay buffer must be on the learner's device")
+        _check(self.L, self.L.drl_dqn_train(ctypes.byref(self.net.desc), ctypes.byref(self._hp),
+                                            _vp(self.block.data_ptr()), _vp(self.net.packed.data_ptr()),
+                                            ctypes.byref(rb._c), rb.size, _stream(self.block.device)))
+
+    def counters(self) -> dict:
+        """Host copy of the device counters (synchronises)."""
+        f, i = self._ctr_f.cpu(), self._ctr_i.cpu()
+        d = self.block[self.layout.counters_off + 16:self.layout.counters_off + 32].view(torch.float64).cpu()
+        return {"step": int(i[0]), "count": int(i[1]), "epsilon": float(f[2]), "loss": float(f[3]),
+                "beta1_pow": float(d[0]), "beta2_pow": float(d[1])}

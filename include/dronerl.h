@@ -15,6 +15,11 @@
  *   jax_impl/env/env.py:274-309    DeliveryDrones.get_obs drl_obs
  *   jax_impl/env/env.py:11-35      DroneEnvParams/State   drl_params / drl_state + drl_decode
  *   torch_impl/helpers/rl_helpers.py:12-18 set_seed       drl_reset(reseed=1)
+ *   jax_impl/agents/dqn.py:132-146 DQNAgent.act          drl_qnet_act* (drl_qnet_act_eps: epsilon on device)
+ *   jax_impl/agents/dqn.py:147-200 train_step / update_target / update_epsilon,
+ *   jax_impl/buffers.py:79-93      sample / can_sample,
+ *   train_jax.py:68-98             the scan body's learner block   drl_dqn_train
+ *   jax_impl/buffers.py:57-77      ReplayBuffer.add_many  drl_replay_add
  *
  * Two layers: stateless calls on caller-owned buffers (drl_reset, drl_step,
  * ...) and library-owned env handles (drl_env_*) that
@@ -46,7 +51,7 @@ extern "C" {
 
 typedef struct ihipStream_t* hipStream_t;
 
-#define DRL_ABI_VERSION 8
+#define DRL_ABI_VERSION 9
 /* Per-env RNG row of `mt` (u32 words, 7104 B):
  *   [0, 624)     MT19937 block 0     the env's CPython stream lives in block
  *   [624, 1248)  MT19937 block 1     mt_index.par; the other block holds the
@@ -239,8 +244,8 @@ int drl_step_code(const drl_params* p, const drl_state* s, const int32_t* d_acti
 int drl_code_decode(int32_t window_radius, const void* d_code, int64_t n, float* d_obs, hipStream_t stream);
 /* Measurement helper (the measured copy-kernel peak beside
  * the spec): mode 0 copies `bytes` from d_src to d_dst, mode 1 only reads
- * d_src (d_dst: a scratch buffer of >= 4 KiB per workgroup it may write).
- * 16-B non-temporal accesses, 8 workgroups of 256 lanes per CU.  Time it with
+ * d_src (d_dst, at least `bytes` long, may be written).  A plain float4
+ * copy: one 16-B element per lane, a grid over the buffer.  Time it with
  * events on `stream`. */
 int drl_hbm_probe(const void* d_src, void* d_dst, int64_t bytes, int32_t mode, hipStream_t stream);
 /* drl_obs that also writes the policy code (d_code nullable); d_obs NULL:
@@ -429,6 +434,91 @@ int drl_replay_add(const drl_replay* r, int64_t cursor, int64_t n, const float* 
                    const float* d_next_obs, int64_t next_obs_stride, const int32_t* d_actions, int64_t action_stride,
                    const float* d_rewards, int64_t reward_stride, const uint8_t* d_dones, int64_t done_stride,
                    hipStream_t stream);
+
+
+/* drl_qnet_act / drl_qnet_act_code with epsilon read from device memory
+ * (d_epsilon: e.g. the learner's drl_dqn_counters.epsilon, which drl_dqn_train
+ * decays on the device), so a captured graph of the train loop acts with the
+ * current schedule.  d_input: the f32 observation rows (obs_stride floats) of
+ * a DRL_QNET_INPUT_OBS net, or the policy code of a DRL_QNET_INPUT_CODE net
+ * (obs_stride ignored).  synth_n > 1: drl_qnet_act_synth's columns. */
+int drl_qnet_act_eps(const drl_qnet_desc* d, const void* d_packed, const void* d_input, int64_t num_envs,
+                     int64_t obs_stride, const float* d_epsilon, uint64_t seed, uint64_t step, int64_t env_offset,
+                     int32_t* d_actions, int64_t action_stride, int32_t synth_n, uint64_t synth_seed,
+                     uint64_t synth_step, float* d_q, int32_t* d_err, hipStream_t stream);
+
+/* ------------------------------------------------------------------------
+ * DQN learner (the train half): one drl_dqn_train call is the
+ * learner block of one train_jax.py scan step (:68-98):
+ *   if current_size >= batch (buffers.py:92-93 can_sample):
+ *       batch = sample(replay) (buffers.py:79-90: uniform rows in [0, size));
+ *       train_step (jax_impl/agents/dqn.py:147-183): q = Q(obs)[action],
+ *       td = reward + gamma * max_a Q_target(next_obs) * (1 - done),
+ *       loss = mean((q - td)^2), gradient, optax.adam(learning_rate, beta1,
+ *       beta2, adam_eps) update;
+ *   if step % target_update_interval == 0: target = tau * online + (1 - tau)
+ *       * target (dqn.py:185-190, optax.incremental_update);
+ *   if step % epsilon_decay_every == 0: epsilon = max(epsilon * decay, end)
+ *       (dqn.py:192-200);
+ *   step += 1.
+ * The step counter, Adam count, epsilon and bias-correction powers live in the
+ * agent block on the device (drl_dqn_counters), so the call is graph-capturable
+ * and a replayed graph continues the schedule.  The online net's packed image
+ * (drl_qnet_pack's layout, d_packed) is refreshed by the same call, ready for
+ * the next act.  Row sampling: a counter hash of (sample_seed, step, row) --
+ * the reference's jax.random stream is jax-only.  Numerics: f32 throughout,
+ * each product and sum rounded in a fixed order (oracle/dqn_learner.py).
+ * Dense nets of drl_qnet_desc (1-3 hidden layers, <= 128 wide, <= 8 actions).
+ * ------------------------------------------------------------------------ */
+typedef struct drl_dqn_hparams {
+    int32_t batch;                  /* sample batch, 1..64 (train_jax.py --batch_size, 8) */
+    int32_t target_update_interval; /* >= 1 (--target_update_interval, 10) */
+    int32_t epsilon_decay_every;    /* >= 1 (--epsilon_decay_every, 5) */
+    int32_t reserved;               /* 0 */
+    double gamma;                   /* 0.9 (--gamma) */
+    double learning_rate;           /* 1e-3 (--learning_rate) */
+    double beta1, beta2, adam_eps;  /* optax.adam defaults 0.9, 0.999, 1e-8 */
+    double tau;                     /* 1.0 (--tau) */
+    double epsilon_decay, epsilon_end;  /* train_jax.py:133-136; --epsilon_end 0.01 */
+    uint64_t sample_seed;
+} drl_dqn_hparams;
+
+/* Device counters at counters_off of the agent block. */
+typedef struct drl_dqn_counters {
+    int32_t step;        /* the scan step (train_jax.py carry `step`) */
+    int32_t count;       /* Adam steps taken (optax ScaleByAdamState.count) */
+    float epsilon;       /* the act's exploration rate */
+    float loss;          /* the last train_step's loss (0 without a sample) */
+    double beta1_pow, beta2_pow;  /* beta^count */
+    int32_t internal[8]; /* the learner's own: arrival ticket, the step's plan */
+} drl_dqn_counters;
+
+/* The agent block (device, caller-owned, one allocation of `bytes`, 16-B
+ * aligned): four parameter sets (online, target, Adam mu, Adam nu) of n_params
+ * floats each -- layer l's weight [out][in] row-major (torch nn.Linear) at
+ * weight_off[l], its bias at bias_off[l] (floats from the set's start) --, the
+ * counters, and the learner's scratch. */
+typedef struct drl_dqn_layout {
+    int64_t n_params;
+    int64_t weight_off[4], bias_off[4];
+    int64_t online_off, target_off, m_off, v_off;  /* bytes */
+    int64_t counters_off, scratch_off, bytes;       /* bytes */
+    int32_t grad_workgroups, grad_lds_bytes;        /* the gradient launch (informative) */
+} drl_dqn_layout;
+
+int drl_dqn_layout_query(const drl_qnet_desc* d, int32_t batch, drl_dqn_layout* layout);
+/* Zero the Adam moments and the counters, epsilon = epsilon_start
+ * (dqn.py:116-130: optax.adam's init, epsilon_start).  The caller writes the
+ * online and target parameters (the reference initialises them from
+ * different keys, dqn.py:114-121). */
+int drl_dqn_init(const drl_qnet_desc* d, int32_t batch, void* d_agent, float epsilon_start, hipStream_t stream);
+/* One learner step on replay `r` holding `size` transitions (current_size,
+ * 0 <= size <= capacity).  The replay's rows: f32 observations (obs_floats >=
+ * in_features) for a DRL_QNET_INPUT_OBS net, policy code rows
+ * (drl_policy_code_bytes / 4 words) for a DRL_QNET_INPUT_CODE one.  d_packed:
+ * the online net's packed image (drl_qnet_pack of the online set). */
+int drl_dqn_train(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agent, void* d_packed,
+                  const struct drl_replay* r, int64_t size, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol():
     exported = set(re.findall(r"\s(drl_\w+)$", out, re.M))
     missing = [f for f in fns if f not in exported]
     assert not missing, missing
-    assert lib().drl_abi_version() == 8
+    assert lib().drl_abi_version() == 9
 
 
 def test_library_is_gfx950_code_object():

@@ -146,25 +146,63 @@ def test_refill_traffic_from_either_refill_form(kern):
     assert set(bench.PMC_KERNELS) >= {"drl_step_kernel", "drl_refill_list_kernel", "drl_refill_kernel"}
 
 
-@pytest.mark.parametrize("cfg,launch_us", [("c3", 19.83), ("c3", 14.0), ("c4", 28.0), ("c5", 143.6), ("c5", 110.0)])
+@pytest.mark.parametrize("cfg,launch_us", [("c3", 19.83), ("c3", 14.0), ("c4", 28.0), ("c5", 143.6), ("c5", 110.0),
+                                            ("c5", 70.0)])
 def test_no_ceiling_below_its_frac(cfg, launch_us):
-    """every `*ceiling*` field bounds its frac (the r3
-    `frac_ceiling_read_only` was exceeded at C5: its W counted a G^2 ground
-    write-back no step does).  frac_ceiling = R / (R + W - G^2) holds for any
-    launch that moves at least the obligatory bytes at or below the spec peak."""
+    """VERDICT r3 item 8 / ADVICE r4: every `*ceiling*` field bounds its frac.
+    frac_ceiling = R / ((R - G^2/2) + (W - G^2)): the obligatory bytes are
+    the ground as stored (two cells per byte) and the outputs; a launch that
+    moves them at or below the spec peak takes at least t_min, and then frac
+    <= frac_ceiling (at C5 the ceiling exceeds 1: R counts G^2 ground bytes,
+    the kernel reads G^2/2)."""
     G, N, E, K = bench.CONFIGS[cfg]
     R, Wb = bench.algorithmic_bytes(G, N, K)
     refill = {"every": 32, "per_step_us": 2.0}
     peak = {"copy_GBs": 6290.0, "read_GBs": 5900.0, "note": "test"}
     rl = bench.roofline(E, R, Wb, launch_us * 1e-6, refill, None, G, peak)
-    assert rl["frac"] <= rl["frac_ceiling"] <= 1.0
-    # the bound itself: obligatory bytes E * (R + W - G^2) at the spec peak take at least this long
-    t_min = E * (R + Wb - G * G) / (bench.PEAK_HBM_GBS * 1e9)
+    obligatory = (R - G * G // 2) + (Wb - G * G)
+    assert rl["frac_ceiling"] == pytest.approx(R / obligatory)
+    t_min = E * obligatory / (bench.PEAK_HBM_GBS * 1e9)
     if launch_us * 1e-6 >= t_min:
         assert rl["frac"] <= rl["frac_ceiling"]
+        ceilings = {k: v for k, v in rl.items() if "ceiling" in k}
+        assert ceilings and all(v >= rl["frac"] for v in ceilings.values())
     assert rl["frac_vs_measured_peak"] == pytest.approx(rl["achieved"] / 6290.0)
-    ceilings = {k: v for k, v in rl.items() if "ceiling" in k}
-    assert ceilings and all(v >= rl["frac"] for v in ceilings.values())
+
+
+@pytest.mark.parametrize("probe,kernel_GBs", [(6290.0, 5760.0), (4800.0, 5760.0), (6300.0, None)])
+def test_measured_peak_fractions_at_most_one(probe, kernel_GBs):
+    """the measured peak is a peak -- the best of the
+    probe's copy / read rates and the kernel's own measured traffic rate -- so
+    every *_vs_measured_peak field is <= 1 (round 4's 4.80 TB/s probe gave
+    1.21 against a 5.76 TB/s step)."""
+    E, R, Wb, G = 65536, 296, 1504, 16
+    launch_s = 19.0e-6
+    traffic = None
+    if kernel_GBs:
+        b = kernel_GBs * 1e9 * launch_s
+        traffic = {"drl_step_kernel": {"bytes_per_launch": b, "read_bytes_per_launch": 0.3 * b,
+                                       "write_bytes_per_launch": 0.7 * b}, "source": "test", "envs": E}
+    peak = {"copy_GBs": probe, "read_GBs": probe * 0.95, "note": "test"}
+    rl = bench.roofline(E, R, Wb, launch_s, {"every": 32, "per_step_us": 1.2}, traffic, G, peak)
+    vs = {k: v for k, v in rl.items() if k.endswith("vs_measured_peak")}
+    assert vs and all(0.0 < v <= 1.0 for v in vs.values()), vs
+    assert rl["peak_measured"] == max(probe, kernel_GBs or 0.0)
+    assert rl["peak_measured_source"] == ("drl_hbm_probe copy" if probe >= (kernel_GBs or 0) else
+                                          "drl_step_kernel traffic")
+
+
+def test_visible_gpus_counts_without_hip(monkeypatch):
+    """the launcher counts GPUs from the KFD topology (no HIP call),
+    narrowed by the *_VISIBLE_DEVICES variables."""
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: (_ for _ in ()).throw(AssertionError("HIP")))
+    n = bench.visible_gpus()
+    assert n is None or n >= 0
+    if n:
+        monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
+        assert bench.visible_gpus() == 1
 
 
 def test_act_code_flops_count():
@@ -204,6 +242,6 @@ def test_launcher_refuses_more_nccl_ranks_than_gpus(monkeypatch, capsys):
     """No GPU here: nccl (RCCL) needs one device per rank, so the launcher
     refuses before starting anything (exit 2); gloo may share devices."""
     monkeypatch.setattr(bench, "DIST_BACKEND", "nccl")
-    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 0)
+    monkeypatch.setattr(bench, "visible_gpus", lambda: 0)
     assert bench.launch_ranks(["--gpus", "2"], 2) == 2
     assert "one GPU per rank" in capsys.readouterr().err

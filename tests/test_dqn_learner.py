@@ -1,0 +1,355 @@
+"""DQN learner (SURVEY.md §8 F1's train half): drl_dqn_train.
+
+Reference: jax_impl/agents/dqn.py:147-200 (train_step, update_target,
+update_epsilon), train_jax.py:68-98 (the scan body's learner block),
+jax_impl/buffers.py:79-93 (sample, can_sample), optax.adam.
+
+Oracle: oracle/dqn_learner.py, a numpy f32 restatement in the kernel's fixed
+arithmetic order -- the GPU learner must equal it BIT FOR BIT (parameters,
+target, Adam moments, loss, counters) over many steps.  The restatement
+itself is pinned here on the CPU against an independent fp32 PyTorch
+restatement (autograd for the gradient, optax's Adam formula written out):
+within REL_TOL per step.  jax/optax are not importable, so
+agreement with optax's own code stays parity unpinned; the row draw is the
+build's counter hash (the reference's jax.random stream is jax-only).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import dqn_learner as O
+
+gpu = pytest.mark.gpu
+REL_TOL = 2e-5  # oracle vs the torch restatement: different summation orders, f32
+
+
+def _rand_net(sizes, seed):
+    g = np.random.default_rng(seed)
+    out = []
+    for i in range(len(sizes) - 1):
+        std = (2.0 / sizes[i]) ** 0.5
+        out.append((g.normal(0, std, (sizes[i + 1], sizes[i])).astype(np.float32),
+                    g.normal(0, 0.05, sizes[i + 1]).astype(np.float32)))
+    return out
+
+
+def _rand_replay(cap, n_in, seed, code_window=0):
+    g = np.random.default_rng(seed)
+    if code_window:
+        W = code_window
+        cells = W * W
+        cpg = -(-cells // 4)
+        cpg8 = -(-cpg // 8) * 8
+        codes = np.zeros((2, cap, 4, cpg8), np.uint16)
+        for t in range(2):
+            for grp in range(4):
+                k = min(cpg, cells - grp * cpg)
+                obj = g.choice([0, 0, 0, 2, 3, 4, 5], size=(cap, k))
+                air = np.where(g.random((cap, k)) < 0.2, g.integers(1, 102, (cap, k)) | (g.integers(0, 2, (cap, k)) << 7), 0)
+                codes[t, :, grp, :k] = (obj | (air << 3)).astype(np.uint16)
+        obs = codes[0].reshape(cap, -1).view(np.uint8).reshape(cap, -1)
+        nxt = codes[1].reshape(cap, -1).view(np.uint8).reshape(cap, -1)
+    else:
+        obs = (g.random((cap, n_in)) < 0.15).astype(np.float32)
+        nxt = (g.random((cap, n_in)) < 0.15).astype(np.float32)
+        obs[:, 4::6] *= g.integers(0, 101, (cap, n_in // 6)).astype(np.float32) / np.float32(100)
+        nxt[:, 4::6] *= g.integers(0, 101, (cap, n_in // 6)).astype(np.float32) / np.float32(100)
+    return {"obs": obs, "next_obs": nxt, "actions": g.integers(0, 5, cap).astype(np.int32),
+            "rewards": g.choice(np.array([0.0, 1.0, -1.0, -0.1], np.float32), cap),
+            "dones": (g.random(cap) < 0.1).astype(np.uint8)}
+
+
+def _torch_forward(ps, X):
+    a = X
+    for i in range(0, len(ps), 2):
+        a = a @ ps[i].t() + ps[i + 1]
+        if i < len(ps) - 2:
+            a = torch.relu(a)
+    return a
+
+
+def _torch_step(st, hp, X, Xn, act, rew, done):
+    """fp32 PyTorch restatement of train_step + optax.adam (independent of the
+    oracle's order): autograd gradient, the optax formula written out."""
+    ps = [torch.tensor(t).requires_grad_() for wb in st["online"] for t in wb]
+    tg = [torch.tensor(t) for wb in st["target"] for t in wb]
+    q = _torch_forward(ps, torch.tensor(X))
+    qa = q.gather(1, torch.tensor(act, dtype=torch.long)[:, None])[:, 0]
+    with torch.no_grad():
+        mx = _torch_forward(tg, torch.tensor(Xn)).max(dim=1).values
+        td = torch.tensor(rew) + hp.gamma * mx * (1 - torch.tensor(done, dtype=torch.float32))
+    loss = ((qa - td) ** 2).mean()
+    loss.backward()
+    st["t"] += 1
+    t = st["t"]
+    new_p, new_m, new_v = [], [], []
+    for p, m, v in zip(ps, [x for wb in st["m"] for x in wb], [x for wb in st["v"] for x in wb]):
+        g = p.grad
+        m = (1 - hp.beta1) * g + hp.beta1 * torch.tensor(m)
+        v = (1 - hp.beta2) * g * g + hp.beta2 * torch.tensor(v)
+        u = (m / (1 - hp.beta1 ** t)) / (torch.sqrt(v / (1 - hp.beta2 ** t)) + hp.adam_eps)
+        new_p.append((p.detach() - hp.learning_rate * u).numpy())
+        new_m.append(m.numpy())
+        new_v.append(v.numpy())
+    pair = lambda xs: [(xs[i], xs[i + 1]) for i in range(0, len(xs), 2)]  # noqa: E731
+    st["online"], st["m"], st["v"] = pair(new_p), pair(new_m), pair(new_v)
+    return float(loss.detach())
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(a - b)) / (1e-3 + np.max(np.abs(b))))
+
+
+@pytest.mark.parametrize("sizes,batch,code_window", [((294, 128, 64, 5), 8, 7), ((150, 64, 5), 4, 0),
+                                                     ((96, 32, 32, 32, 5), 16, 0)])
+def test_oracle_learner_matches_torch_restatement(sizes, batch, code_window):
+    """The oracle's learner step == autograd + optax's Adam formula (fp32
+    PyTorch) within REL_TOL: loss, parameters and moments, step by step, with
+    the target update (tau 0.7 every 3 steps) and the epsilon schedule."""
+    hp = O.HParams(batch=batch, tau=0.7, target_update_interval=3, epsilon_decay=0.97, epsilon_decay_every=2,
+                   sample_seed=11)
+    cap = 300
+    rep = _rand_replay(cap, sizes[0], seed=len(sizes) + batch, code_window=code_window)
+    online, target = _rand_net(sizes, 1), _rand_net(sizes, 2)
+    st = O.LearnerState.start(online, target, epsilon_start=1.0)
+    ts = {"online": [(w.copy(), b.copy()) for w, b in online], "target": [(w.copy(), b.copy()) for w, b in target],
+          "m": [(np.zeros_like(w), np.zeros_like(b)) for w, b in online],
+          "v": [(np.zeros_like(w), np.zeros_like(b)) for w, b in online], "t": 0}
+    eps = np.float32(1.0)
+    for step in range(12):
+        info = O.learner_step(st, hp, rep["obs"], rep["next_obs"], rep["actions"], rep["rewards"], rep["dones"],
+                              cap, code_window)
+        idx = info["rows"]
+        if code_window:
+            X, Xn = O.decode_code_rows(rep["obs"][idx], code_window), O.decode_code_rows(rep["next_obs"][idx],
+                                                                                        code_window)
+        else:
+            X, Xn = rep["obs"][idx], rep["next_obs"][idx]
+        loss = _torch_step(ts, hp, X, Xn, rep["actions"][idx], rep["rewards"][idx], rep["dones"][idx])
+        assert abs(float(info["loss"]) - loss) <= REL_TOL * (1e-3 + abs(loss)), step
+        if step % hp.target_update_interval == 0:
+            ts["target"] = [(hp.tau * w + (1 - hp.tau) * tw, hp.tau * b + (1 - hp.tau) * tb)
+                            for (w, b), (tw, tb) in zip(ts["online"], ts["target"])]
+        for k in ("online", "target", "m", "v"):
+            for (a, b), (c, d) in zip(getattr(st, k), ts[k]):
+                assert _rel(a, c) <= REL_TOL and _rel(b, d) <= REL_TOL, (step, k)
+        if step % hp.epsilon_decay_every == 0:
+            eps = max(np.float32(eps * np.float32(hp.epsilon_decay)), np.float32(hp.epsilon_end))
+        assert st.epsilon == eps and st.step == step + 1 and st.count == step + 1
+        # resynchronise the torch side on the oracle (the comparison is per step)
+        for k in ("online", "target", "m", "v"):
+            ts[k] = [(w.copy(), b.copy()) for w, b in getattr(st, k)]
+
+
+def test_oracle_learner_without_sample_only_schedules():
+    """size < batch: no train_step (loss 0, parameters unchanged, Adam count
+    unchanged) but the target update and the epsilon decay still run."""
+    hp = O.HParams(batch=8, tau=0.5, target_update_interval=1)
+    online, target = _rand_net((30, 32, 5), 3), _rand_net((30, 32, 5), 4)
+    st = O.LearnerState.start(online, target, 1.0)
+    rep = _rand_replay(16, 30, 5)
+    info = O.learner_step(st, hp, rep["obs"], rep["next_obs"], rep["actions"], rep["rewards"], rep["dones"], 7)
+    assert not info["trained"] and info["loss"] == 0 and st.count == 0 and st.step == 1
+    for (w, b), (w0, b0) in zip(st.online, online):
+        assert np.array_equal(w, w0) and np.array_equal(b, b0)
+    for (tw, _), (w0, _), (t0, _) in zip(st.target, online, target):
+        assert np.array_equal(tw, np.float32(0.5) * w0 + np.float32(0.5) * t0)
+    assert st.epsilon == np.float32(np.float32(1.0) * np.float32(hp.epsilon_decay))
+
+
+def test_train_jax_epsilon_decay_formula():
+    """train_jax.py:133-134: half-way to epsilon_end after 20 % of the steps
+    (per decay call, as the reference computes it)."""
+    d = O.train_jax_epsilon_decay(1000)
+    assert abs(d ** 200 - 0.505) < 1e-9
+
+
+def test_sample_indices_in_range_and_uniform():
+    rows = np.array([O.sample_indices(7, s, 64, 1000) for s in range(200)]).ravel()
+    assert rows.min() >= 0 and rows.max() < 1000
+    hist = np.bincount(rows // 100, minlength=10)
+    assert hist.min() > 0.8 * rows.size / 10
+
+
+# ------------------------------------------------------------ C ABI (CPU) ---
+def _desc(in_features, hidden, inp=0, precision=1):
+    from dronerl_amd.dqn import DrlQnetDesc
+    h = list(hidden) + [0] * (3 - len(hidden))
+    return DrlQnetDesc(in_features, len(hidden), (ctypes.c_int32 * 3)(*h), 5, precision, inp)
+
+
+def test_dqn_layout_query():
+    """The agent block: four parameter sets in torch state_dict order, 16-B
+    aligned sections, the counters, the scratch; batch bounds; LDS fit."""
+    from dronerl_amd._native import lib
+    from dronerl_amd.dqn import DrlDqnLayout, _bind
+    L = _bind(lib())
+    lay = DrlDqnLayout()
+    assert L.drl_dqn_layout_query(ctypes.byref(_desc(294, (128, 64), 1)), 8, ctypes.byref(lay)) == 0
+    n = 294 * 128 + 128 + 128 * 64 + 64 + 64 * 8  # (the 5-row output layer padded to 4 floats: 320 -> 320, bias 5 -> 8)
+    assert lay.weight_off[0] == 0 and lay.bias_off[0] == 294 * 128
+    assert lay.weight_off[1] == 294 * 128 + 128 and lay.weight_off[2] == 294 * 128 + 128 + 128 * 64 + 64
+    assert lay.n_params == 294 * 128 + 128 + 128 * 64 + 64 + 320 + 8 and n > 0
+    assert (lay.online_off, lay.target_off, lay.m_off, lay.v_off) == tuple(i * 4 * lay.n_params for i in range(4))
+    assert lay.counters_off == 16 * lay.n_params and lay.scratch_off == lay.counters_off + 64
+    assert lay.bytes % 16 == 0 and lay.grad_workgroups == 16 and lay.grad_lds_bytes <= 159 * 1024
+    for b, ok in ((0, False), (1, True), (64, True), (65, False)):
+        assert (L.drl_dqn_layout_query(ctypes.byref(_desc(294, (128, 64), 1)), b, ctypes.byref(lay)) == 0) == ok
+    # a batch of 64 rows of 510 inputs does not fit a CU's LDS; 32 does
+    assert L.drl_dqn_layout_query(ctypes.byref(_desc(510, (64,), 0, 0)), 64, ctypes.byref(lay)) != 0
+    assert b"LDS" in L.drl_last_error()
+    assert L.drl_dqn_layout_query(ctypes.byref(_desc(510, (64,), 0, 0)), 32, ctypes.byref(lay)) == 0
+
+
+def test_dqn_train_argument_checks():
+    """drl_dqn_train validates before it launches (no GPU work reached)."""
+    from dronerl_amd._native import lib
+    from dronerl_amd.dqn import DrlDqnHParams, DrlReplay, _bind
+    L = _bind(lib())
+    d = _desc(294, (128, 64), 1)
+    hp = DrlDqnHParams(8, 10, 5, 0, 0.9, 1e-3, 0.9, 0.999, 1e-8, 1.0, 0.999, 0.01, 0)
+    fake = ctypes.c_void_p(1 << 20)
+    rep = DrlReplay(1000, 32, 1 << 20, 1 << 20, 1 << 20, 1 << 20, 1 << 20)
+
+    def call(h=hp, agent=fake, packed=fake, r=rep, size=100):
+        return L.drl_dqn_train(ctypes.byref(d), ctypes.byref(h), agent, packed, ctypes.byref(r), size, None)
+    assert call(size=1001) != 0 and b"size" in L.drl_last_error()
+    assert call(size=-1) != 0
+    assert call(agent=None) != 0 and b"agent" in L.drl_last_error()
+    assert call(packed=ctypes.c_void_p((1 << 20) + 4)) != 0 and b"packed" in L.drl_last_error()
+    bad = DrlDqnHParams(8, 0, 5, 0, 0.9, 1e-3, 0.9, 0.999, 1e-8, 1.0, 0.999, 0.01, 0)
+    assert call(h=bad) != 0 and b"interval" in L.drl_last_error()
+    bad = DrlDqnHParams(8, 10, 5, 0, 0.9, 1e-3, 1.0, 0.999, 1e-8, 1.0, 0.999, 0.01, 0)
+    assert call(h=bad) != 0 and b"beta" in L.drl_last_error()
+    wrong_rows = DrlReplay(1000, 294, 1 << 20, 1 << 20, 1 << 20, 1 << 20, 1 << 20)  # f32 rows for a code net
+    assert call(r=wrong_rows) != 0 and b"policy code" in L.drl_last_error()
+
+
+# ------------------------------------------------------------------- GPU ---
+def _learner_setup(sizes, inp, hp_kw, E=64, cap=300, seed=0):
+    from dronerl_amd import BatchedDeliveryDrones, EnvParams
+    from dronerl_amd.dqn import DQNHParams, DQNLearner, QNetwork, ReplayBuffer
+    radius = 3
+    env = BatchedDeliveryDrones(EnvParams(n_drones=8, grid_size=16, window_radius=radius), E)
+    env.reset(seed=seed)
+    g = torch.Generator().manual_seed(seed + 5)
+    net = QNetwork(sizes[0], sizes[1:-1], generator=g, precision="f32", input=inp)
+    gb = torch.Generator(device="cuda").manual_seed(seed + 6)
+    for b in net.biases:
+        b.normal_(0, 0.05, generator=gb)
+    net.pack()
+    hp = DQNHParams(**hp_kw)
+    target = ([torch.randn(w.shape, generator=g) * 0.1 for w in net.weights],
+              [torch.randn(b.shape, generator=g) * 0.05 for b in net.biases])
+    learner = DQNLearner(net, hp, target=target)
+    rb = ReplayBuffer(cap, sizes[0], torch.device("cuda"), code_radius=radius if inp == "code" else 0)
+    return env, net, learner, rb, hp
+
+
+def _host(t):
+    return t.detach().cpu().numpy().copy()
+
+
+def _state_from_learner(learner):
+    st = O.LearnerState.start([(_host(w), _host(b)) for w, b in learner.params("online")],
+                              [(_host(w), _host(b)) for w, b in learner.params("target")], 1.0)
+    st.m = [(_host(w), _host(b)) for w, b in learner.params("m")]
+    st.v = [(_host(w), _host(b)) for w, b in learner.params("v")]
+    c = learner.counters()
+    st.step, st.count, st.epsilon = c["step"], c["count"], np.float32(c["epsilon"])
+    st.beta1_pow, st.beta2_pow = c["beta1_pow"], c["beta2_pow"]
+    return st
+
+
+def _assert_same(learner, st, where):
+    for k in ("online", "target", "m", "v"):
+        for l, ((w, b), (ow, ob)) in enumerate(zip(learner.params(k), getattr(st, k))):
+            assert np.array_equal(_host(w).view(np.uint32), ow.view(np.uint32)), (where, k, l, "W")
+            assert np.array_equal(_host(b).view(np.uint32), ob.view(np.uint32)), (where, k, l, "b")
+    c = learner.counters()
+    assert c["step"] == st.step and c["count"] == st.count, where
+    assert np.float32(c["epsilon"]) == st.epsilon and np.float32(c["loss"]) == st.loss, where
+    assert c["beta1_pow"] == st.beta1_pow and c["beta2_pow"] == st.beta2_pow, where
+
+
+@gpu
+@pytest.mark.parametrize("sizes,inp,hp_kw,E,cap", [
+    ((294, 128, 64, 5), "code", dict(batch=8, num_steps=1000), 64, 300),                      # train_jax defaults
+    ((294, 128, 64, 5), "obs", dict(batch=8, tau=0.6, target_update_interval=3), 50, 257),
+    ((294, 64, 5), "code", dict(batch=1, epsilon_decay=0.9, epsilon_decay_every=1), 16, 100),
+    ((294, 96, 32, 32, 5), "code", dict(batch=32, learning_rate=3e-3, gamma=0.95), 40, 500),
+    ((294, 128, 64, 5), "code", dict(batch=64, target_update_interval=7, sample_seed=99), 24, 96),
+])
+def test_learner_matches_oracle_bit_exact(sizes, inp, hp_kw, E, cap):
+    """The train_jax.py loop shape with the learner on: act (device epsilon)
+    -> step -> replay add_many -> drl_dqn_train, 40 steps.  Before each train
+    the ring is copied to the host and the oracle takes the same learner step:
+    parameters, target, moments, loss and counters equal bit for bit after
+    every step (including the first steps, where a batch larger than the
+    ring's size skips train_step: buffers.py can_sample)."""
+    env, net, learner, rb, hp = _learner_setup(sizes, inp, hp_kw, E=E, cap=cap)
+    st = _state_from_learner(learner)
+    ohp = O.HParams(batch=hp.batch, gamma=hp.gamma, learning_rate=hp.learning_rate, tau=hp.tau,
+                    target_update_interval=hp.target_update_interval, epsilon_decay=hp.decay(),
+                    epsilon_end=hp.epsilon_end, epsilon_decay_every=hp.epsilon_decay_every,
+                    sample_seed=hp.sample_seed)
+    W = 7
+    cur = env.new_code() if inp == "code" else torch.empty((E, 1, W, W, 6), device="cuda")
+    nxt = env.new_code() if inp == "code" else torch.empty((E, 1, W, W, 6), device="cuda")
+    if inp == "code":
+        env.get_code(out=cur)
+    else:
+        env.get_obs(1, out=cur)
+    acts = torch.empty((E, 8), dtype=torch.int32, device="cuda")
+    trained = 0
+    for t in range(40):
+        x = cur if inp == "code" else cur.reshape(E, -1)
+        eps_before = float(learner.epsilon.item())
+        assert np.float32(eps_before) == st.epsilon
+        net.act(x, learner.epsilon, seed=3, step=t, actions=acts, synth=(5, t))
+        if inp == "code":
+            r, d = env.step(acts, code=nxt)
+        else:
+            r, d, _ = env.step(acts, obs_k=1, obs=nxt)
+        rb.add_many(cur, acts, r, nxt, d)
+        rep = {"obs": _host(rb.obs), "next_obs": _host(rb.next_obs), "actions": _host(rb.actions),
+               "rewards": _host(rb.rewards), "dones": _host(rb.dones)}
+        info = O.learner_step(st, ohp, rep["obs"], rep["next_obs"], rep["actions"], rep["rewards"], rep["dones"],
+                              rb.size, W if inp == "code" else 0)
+        trained += info["trained"]
+        learner.train(rb)
+        torch.cuda.synchronize()
+        _assert_same(learner, st, t)
+        cur, nxt = nxt, cur
+    net.check_errors()
+    env.check_errors()
+    assert trained >= 30
+    # the act's packed image is the online net's: a fresh drl_qnet_pack of the same parameters is byte-identical
+    after = net.packed.clone()
+    net.pack()
+    assert torch.equal(after, net.packed)
+
+
+@gpu
+def test_learner_act_reads_device_epsilon():
+    """drl_qnet_act_eps == drl_qnet_act with the same epsilon value (both
+    inputs, with and without the synthetic columns)."""
+    from dronerl_amd.dqn import QNetwork
+    env, net, learner, rb, hp = _learner_setup((294, 128, 64, 5), "code", dict(epsilon_start=0.37), E=777)
+    code = env.new_code()
+    _, _, obs = env.step(env.synth_actions(seed=1, step=0), obs_k=1, code=code)
+    a1 = torch.full((777, 8), -1, dtype=torch.int32, device="cuda")
+    a2 = a1.clone()
+    net.act(code, learner.epsilon, seed=5, step=2, actions=a1, synth=(9, 4))
+    net.act(code, float(learner.epsilon.item()), seed=5, step=2, actions=a2, synth=(9, 4))
+    assert torch.equal(a1, a2)
+    onet = QNetwork(294, (128, 64), precision="f32")
+    onet.load(net.weights, net.biases)
+    x = obs.reshape(777, -1)
+    b1 = torch.empty((777, 1), dtype=torch.int32, device="cuda")
+    b2 = b1.clone()
+    onet.act(x, learner.epsilon, seed=5, step=2, actions=b1)
+    onet.act(x, 0.37, seed=5, step=2, actions=b2)
+    assert torch.equal(b1, b2)
