@@ -158,6 +158,15 @@ def launch_ranks(argv, n: int) -> int:
     return rc
 
 
+def strong_split(total: int, world: int) -> int:
+    """Envs per rank of the strong-scaling sub-record: `total` envs over the
+    job, contiguous shards (train_jax.py:196-212), num_envs % devices == 0 as
+    train_jax.py:401-402 requires."""
+    if total <= 0 or world <= 0 or total % world:
+        raise ValueError(f"the number of envs (={total}) needs to be divisible by the number of devices (={world})")
+    return total // world
+
+
 def barrier(world):
     if world > 1:
         import torch.distributed as dist
@@ -1065,6 +1074,9 @@ def main():
                     help="envs per GPU of the north-star sub-record (C5: 64x64 grid, 32 drones; 131072 per GPU = "
                          "2^20 over 8 GPUs; 0 = skip)")
     ap.add_argument("--c5-steps", type=int, default=200, help="timed steps of the north-star sub-record (>= 200)")
+    ap.add_argument("--strong-envs", type=int, default=65536,
+                    help="whole-job envs of the strong-scaling sub-record at N > 1 ranks (BASELINE.json: "
+                         "num_envs=65536 over 1/2/4/8 GPUs; 0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-reset-bench", action="store_true")
@@ -1150,6 +1162,27 @@ def main():
                  "note": "the other observation store mode, same steps and results, refill share charged the same "
                          "way; `value` uses env.step()'s default (cached stores at 8 lanes per env, streaming at "
                          ">= 16: the faster one in the train loop, profiles/r02_store_mode/)"}
+
+    # ---- strong scaling (BASELINE.json's metric as written: num_envs = 65536
+    # over the job): the same config, strong_envs / world envs per rank
+    strong = None
+    if args.strong_envs > 0:
+        if world == 1:
+            strong = {"value": main_res["value"], "num_envs_total": E, "n_gpus": 1, "scaling": "strong",
+                      "note": "one rank: the headline itself" + ("" if E == args.strong_envs else
+                                                                 f" ({E} envs, not {args.strong_envs})")}
+        else:
+            Es = strong_split(args.strong_envs, world)
+            env_s, _, _, _, _ = make_env(args.config, Es, rank, dev)
+            run_s = StepRunner(env_s, K, args.warmup + args.steps + 2 * env_s.refill_every, args.obs_stream)
+            rs = run_s.run(args.steps, args.warmup, world, pre=PRE_ROLL_CYCLES * env_s.refill_every)
+            strong = {"value": rs["value"], "unit": "env-steps/s", "scaling": "strong", "n_gpus": world,
+                      "num_envs_total": args.strong_envs, "num_envs_per_gpu": Es, "steps": args.steps,
+                      "ms_per_step": rs["ms_per_step"], "avg_launch_us": rs["launch_s"] * 1e6,
+                      "note": "BASELINE.json's num_envs=65536 split over the ranks (env_offset = rank * E / N); "
+                              "same timing rule as the headline (max over ranks, refill share charged)"}
+            del run_s, env_s
+            torch.cuda.synchronize()
 
     copy_peak = measure_copy_peak(dev)
 
@@ -1261,6 +1294,7 @@ def main():
             "roofline": roofline(E, R, Wb, main_res["launch_s"], main_res["refill"], traffic_of(args.config), G,
                                  copy_peak),
             "refill": main_res["refill"],
+            "strong": strong,
             ("cached_obs" if args.obs_stream else "streaming_obs"): other,
             "c5": c5,
             "cpu_baseline": cpu,

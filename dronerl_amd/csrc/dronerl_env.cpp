@@ -199,7 +199,7 @@ int drl_env_set_state(drl_env* env, const drl_state_view* v, hipStream_t stream)
             return drl_internal_fail("set_state needs every view field");
         const size_t E = (size_t)env->num_envs, cells = (size_t)env->L.cells;
         if (hip_check(drl::launch_ground_pack(v->ground, (int)cells, env->s.ground, env->L.ground_stride, (int64_t)E,
-                                              stream),
+                                              env->err, stream),
                       "ground pack"))
             return -1;
         if (drl_encode(&env->p, &env->s, v->order, v->y, v->x, v->charge, v->carry, stream)) return -1;

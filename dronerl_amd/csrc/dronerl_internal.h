@@ -283,6 +283,7 @@ struct QnetArgs {
 
 struct ReplayArgs {
     int64_t first, n, cursor, capacity;
+    int64_t base;  // slot of the first landing row: (cursor + first) % capacity
     int obs_floats;
     const float* obs;
     int64_t obs_stride;
@@ -359,12 +360,15 @@ struct DqnCounters {
 static_assert(sizeof(DqnCounters) == 64, "drl_dqn_counters is 64 bytes");
 
 constexpr int DQN_MAX_BATCH = 64;
-constexpr int DQN_TILE = 16;  // layer-0 units per workgroup of the gradient kernel
+constexpr int DQN_TILE = 16;      // layer-0 units per workgroup of the gradient kernel
+constexpr int DQN_THREADS = 512;  // the gradient kernel's workgroup
+constexpr int DQN_STAGE = 8;      // loads each thread keeps in flight when the learner stages data
 
 struct LearnArgs {
     int n_layers, batch, code_w, trained, nblk0, tiles0, maxw;
     int in[QN_MAX_LAYERS], out[QN_MAX_LAYERS];
     int in4;                          // layer 0's input row stride in LDS / scratch (in[0] rounded up to 4)
+    int ws_floats;                    // the last workgroup's weight staging: max over l >= 1 of out_l * (in_l + 4)
     int64_t woff[QN_MAX_LAYERS], boff[QN_MAX_LAYERS];  // float offsets of W_l / b_l in a parameter set
     float* online;
     float* target;
@@ -407,7 +411,8 @@ hipError_t launch_decode(const uint32_t* drones, int64_t E, int N, int32_t* orde
 hipError_t launch_code_decode(const void* code, int64_t n, int W, float* obs, hipStream_t s);
 hipError_t launch_hbm_probe(const void* src, void* dst, int64_t bytes, int mode, int num_cus, hipStream_t s);
 hipError_t launch_ground_unpack(const uint8_t* packed, int pstride, uint8_t* out, int cells, int64_t E, hipStream_t s);
-hipError_t launch_ground_pack(const uint8_t* in, int cells, uint8_t* packed, int pstride, int64_t E, hipStream_t s);
+hipError_t launch_ground_pack(const uint8_t* in, int cells, uint8_t* packed, int pstride, int64_t E, int32_t* err,
+                              hipStream_t s);
 hipError_t launch_grid_obs(const uint8_t* ground, const uint32_t* drones, int64_t E, int side, int N, int gstride,
                            float* out, hipStream_t s);
 hipError_t launch_encode(uint32_t* drones, int64_t E, int N, const int32_t* order, const int32_t* y,

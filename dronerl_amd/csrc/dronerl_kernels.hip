@@ -2415,15 +2415,18 @@ __global__ void drl_ground_unpack_kernel(const uint8_t* __restrict__ packed, int
     const int c = (int)(i - e * cells);
     out[i] = (uint8_t)nib_get(packed + e * pstride, c);
 }
+// (a code outside the ground objects {0, 2, 3, 4, 5} raises DRL_ERR_BAD_STATE: ADVICE r4)
 __global__ void drl_ground_pack_kernel(const uint8_t* __restrict__ in, int cells, uint8_t* __restrict__ packed,
-                                       int pstride, int64_t total) {
+                                       int pstride, int64_t total, int32_t* __restrict__ err) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one packed byte
     if (i >= total) return;
     const int64_t e = i / pstride;
     const int b = (int)(i - e * pstride), c0 = 2 * b;
     const uint8_t* row = in + e * cells;
-    const uint32_t lo = c0 < cells ? (row[c0] & 15u) : 0u, hi = c0 + 1 < cells ? (row[c0 + 1] & 15u) : 0u;
-    packed[i] = (uint8_t)(lo | (hi << 4));
+    const uint32_t vlo = c0 < cells ? row[c0] : 0u, vhi = c0 + 1 < cells ? row[c0 + 1] : 0u;
+    const auto bad = [](uint32_t v) { return v == 1u || v > 5u; };
+    if (err && (bad(vlo) || bad(vhi))) atomicOr(err, DRL_ERR_BAD_STATE);
+    packed[i] = (uint8_t)((vlo & 15u) | ((vhi & 15u) << 4));
 }
 hipError_t launch_ground_unpack(const uint8_t* packed, int pstride, uint8_t* out, int cells, int64_t E, hipStream_t s) {
     const int64_t total = E * cells;
@@ -2432,11 +2435,12 @@ hipError_t launch_ground_unpack(const uint8_t* packed, int pstride, uint8_t* out
                        out, cells, total);
     return hipGetLastError();
 }
-hipError_t launch_ground_pack(const uint8_t* in, int cells, uint8_t* packed, int pstride, int64_t E, hipStream_t s) {
+hipError_t launch_ground_pack(const uint8_t* in, int cells, uint8_t* packed, int pstride, int64_t E, int32_t* err,
+                              hipStream_t s) {
     const int64_t total = E * pstride;
     if (total <= 0) return hipSuccess;
     hipLaunchKernelGGL(drl_ground_pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, in, cells, packed,
-                       pstride, total);
+                       pstride, total, err);
     return hipGetLastError();
 }
 

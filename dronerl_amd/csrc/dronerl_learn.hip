@@ -143,13 +143,42 @@ __device__ void dq_finish(const LearnArgs& a, int32_t step, int trained, float l
     }
 }
 
+// Copy n words src(i) -> dst(i) with every thread holding DQN_STAGE loads in
+// flight before its first store (a loop with one dependent load per
+// iteration would serialise them: one L2/HBM round trip each).
+template <class Src, class Dst>
+__device__ __forceinline__ void dq_stage(int n, Src src, Dst dst) {
+    const int nt = blockDim.x;
+    for (int base = threadIdx.x; base < n; base += DQN_STAGE * nt) {
+        float v[DQN_STAGE];
+#pragma unroll
+        for (int q = 0; q < DQN_STAGE; ++q) {
+            const int i = base + q * nt;
+            v[q] = i < n ? src(i) : 0.0f;
+        }
+#pragma unroll
+        for (int q = 0; q < DQN_STAGE; ++q) {
+            const int i = base + q * nt;
+            if (i < n) dst(i, v[q]);
+        }
+    }
+}
+
+// Layer l's weights of one net -> LDS, rows padded to in + 4 floats (float4
+// rows whose starts fall on different banks).
+__device__ __forceinline__ void dq_stage_w(const LearnArgs& a, const float* P, int l, float* Ws) {
+    const int li = a.in[l], lo = a.out[l], ls = li + 4;
+    const float* src = P + a.woff[l];
+    dq_stage(li * lo, [&](int i) { return src[i]; }, [&](int i, float v) { Ws[(i / li) * ls + (i % li)] = v; });
+}
+
 }  // namespace
 
-__global__ void __launch_bounds__(256) drl_dqn_grad_kernel(LearnArgs a) {
+__global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) {
     extern __shared__ float4 dq_lds4[];
     float* lds = reinterpret_cast<float*>(dq_lds4);
     __shared__ int64_t s_idx[DQN_MAX_BATCH];
-    __shared__ float s_d[DQN_MAX_BATCH];
+    __shared__ float s_d[DQN_MAX_BATCH], s_mx[DQN_MAX_BATCH], s_q[DQN_MAX_BATCH * 8];
     __shared__ int s_act[DQN_MAX_BATCH];
     __shared__ int s_last;
     const int tid = threadIdx.x, nt = blockDim.x;
@@ -163,26 +192,39 @@ __global__ void __launch_bounds__(256) drl_dqn_grad_kernel(LearnArgs a) {
     // ---- layer 0 of one net for DQN_TILE units (all workgroups)
     const int net = blockIdx.x / a.tiles0, u0 = (blockIdx.x % a.tiles0) * DQN_TILE;
     const int in = a.in[0], in4 = a.in4, out0 = a.out[0];
+    const int nu = min(DQN_TILE, out0 - u0);
     if (tid < B) s_idx[tid] = dq_sample(a.seed, step, tid, a.size);
     __syncthreads();
     float* X = lds;                // [B][in4] the sampled rows (obs for the online net, next_obs for the target)
     float* Wt = lds + B * in4;     // [DQN_TILE][in4] this tile's layer-0 weight rows
     const uint32_t* rows = net ? a.r_next : a.r_obs;
-    for (int e = tid; e < B * in4; e += nt) {
-        const int b = e / in4, k = e - b * in4;
-        X[e] = k < in ? dq_input(a, rows, s_idx[b], k) : 0.0f;
-    }
+    const int rw = (int)a.row_words;
     const float* P = net ? a.target : a.online;
-    for (int e = tid; e < DQN_TILE * in4; e += nt) {
-        const int u = e / in4, k = e - u * in4;
-        Wt[e] = (u0 + u < out0 && k < in) ? P[a.woff[0] + (int64_t)(u0 + u) * in + k] : 0.0f;
+    // this tile's weight rows are contiguous in the set: one flat copy
+    const float* wsrc = P + a.woff[0] + (int64_t)u0 * in;
+    dq_stage(nu * in, [&](int i) { return wsrc[i]; }, [&](int i, float v) { Wt[(i / in) * in4 + (i % in)] = v; });
+    if (a.code_w) {  // the B code rows -> LDS, then decoded from there
+        uint32_t* R = reinterpret_cast<uint32_t*>(Wt + DQN_TILE * in4);  // [B][rw]
+        dq_stage(B * rw, [&](int i) { return __uint_as_float(rows[s_idx[i / rw] * a.row_words + (i % rw)]); },
+                 [&](int i, float v) { R[i] = __float_as_uint(v); });
+        __syncthreads();
+        for (int e = tid; e < B * in4; e += nt) {
+            const int b = e / in4, k = e - b * in4;
+            X[e] = k < in ? dq_input(a, R + b * rw, 0, k) : 0.0f;
+        }
+    } else {
+        dq_stage(B * in4, [&](int i) {
+            const int b = i / in4, k = i - b * in4;
+            return k < in ? __uint_as_float(rows[s_idx[b] * a.row_words + k]) : 0.0f;
+        }, [&](int i, float v) { X[i] = v; });
     }
+    for (int e = tid; e < (DQN_TILE - nu) * in4; e += nt) Wt[nu * in4 + e] = 0.0f;  // (a partial last tile)
     __syncthreads();
     if (net == 0 && u0 == 0)  // the update kernel's layer-0 inputs
         for (int e = tid; e < B * in4; e += nt) a.sx[e] = X[e];
     for (int o = tid; o < DQN_TILE * B; o += nt) {
         const int u = o % DQN_TILE, b = o / DQN_TILE;
-        if (u0 + u < out0) {
+        if (u < nu) {
             const float z = dq_dot(X + b * in4, Wt + u * in4, in4 / 4) + P[a.boff[0] + u0 + u];
             a.sz0[((int64_t)net * B + b) * out0 + u0 + u] = z;
         }
@@ -206,79 +248,88 @@ __global__ void __launch_bounds__(256) drl_dqn_grad_kernel(LearnArgs a) {
     }
     __syncthreads();
 
-    // ---- the last workgroup: later layers, TD error, backward, biases
+    // ---- the last workgroup: later layers (one net at a time, each layer's
+    // weights staged in LDS), TD error, backward, biases
     const int mw = a.maxw;
-    float* Pa = lds;                       // [2][B][mw] activations of the current layer (both nets)
-    float* Qa = lds + 2 * B * mw;          // [2][B][mw] the next layer's
-    uint8_t* M = reinterpret_cast<uint8_t*>(lds + 4 * B * mw);  // [L-1][B][mw] online ReLU masks (z > 0)
-    for (int o = tid; o < 2 * B * out0; o += nt) {
-        const int n = o / (B * out0), r = o - n * B * out0, b = r / out0, j = r - b * out0;
-        const float z = a.sz0[o];
-        const float h = z > 0.0f ? z : 0.0f;
-        Pa[(n * B + b) * mw + j] = h;
-        if (n == 0) {
-            a.sh[0][r] = h;
-            M[b * mw + j] = z > 0.0f;
-        }
-    }
-    __syncthreads();
-    for (int l = 1; l < L; ++l) {
-        const int li = a.out[l - 1], lo = a.out[l];
-        const bool hidden = l < L - 1;
-        for (int o = tid; o < 2 * B * lo; o += nt) {
-            const int n = o / (B * lo), r = o - n * B * lo, b = r / lo, j = r - b * lo;
-            const float* Pn = n ? a.target : a.online;
-            const float z = dq_dot(Pa + (n * B + b) * mw, Pn + a.woff[l] + (int64_t)j * li, li / 4) + Pn[a.boff[l] + j];
-            if (hidden) {
-                const float h = z > 0.0f ? z : 0.0f;
-                Qa[(n * B + b) * mw + j] = h;
-                if (n == 0) {
-                    a.sh[l][r] = h;
-                    M[(l * B + b) * mw + j] = z > 0.0f;
+    float* Pa = lds;                   // [B][mw] activations of the current layer
+    float* Qa = lds + B * mw;          // [B][mw] the next layer's
+    float* Ws = lds + 2 * B * mw;      // one layer's weights, rows of in + 4 floats
+    uint8_t* M = reinterpret_cast<uint8_t*>(Ws + a.ws_floats);  // [L-1][B][mw] online ReLU masks (z > 0)
+    const int A = a.out[L - 1];
+    for (int n = 1; n >= 0; --n) {  // the target net on next_obs, then the online net on obs
+        const float* Pn = n ? a.target : a.online;
+        dq_stage(B * out0, [&](int i) { return a.sz0[(int64_t)n * B * out0 + i]; }, [&](int i, float z) {
+            const int b = i / out0, j = i - b * out0;
+            const float h = z > 0.0f ? z : 0.0f;
+            Pa[b * mw + j] = h;
+            if (n == 0) {
+                a.sh[0][i] = h;
+                M[b * mw + j] = z > 0.0f;
+            }
+        });
+        for (int l = 1; l < L; ++l) {
+            const int li = a.out[l - 1], lo = a.out[l], ls = li + 4;
+            const bool hidden = l < L - 1;
+            dq_stage_w(a, Pn, l, Ws);
+            __syncthreads();
+            for (int o = tid; o < B * lo; o += nt) {
+                const int b = o / lo, j = o - b * lo;
+                const float z = dq_dot(Pa + b * mw, Ws + j * ls, li / 4) + Pn[a.boff[l] + j];
+                if (hidden) {
+                    const float h = z > 0.0f ? z : 0.0f;
+                    Qa[b * mw + j] = h;
+                    if (n == 0) {
+                        a.sh[l][o] = h;
+                        M[(l * B + b) * mw + j] = z > 0.0f;
+                    }
+                } else {
+                    Qa[b * mw + j] = z;
                 }
+            }
+            __syncthreads();
+            float* t = Pa;
+            Pa = Qa;
+            Qa = t;
+        }
+        // Pa: the net's Q [B][A]
+        for (int b = tid; b < B; b += nt) {
+            if (n == 1) {
+                float mx = Pa[b * mw];
+                for (int j = 1; j < A; ++j) mx = Pa[b * mw + j] > mx ? Pa[b * mw + j] : mx;  // jnp.max
+                s_mx[b] = mx;
             } else {
-                Qa[(n * B + b) * mw + j] = z;
+                for (int j = 0; j < A; ++j) s_q[b * 8 + j] = Pa[b * mw + j];
             }
         }
         __syncthreads();
-        float* t = Pa;
-        Pa = Qa;
-        Qa = t;
     }
-    // Pa: Q of the online net on obs (rows 0..B-1) and of the target net on next_obs (B..2B-1)
-    const int A = a.out[L - 1];
-    if (tid < B) {
-        const int64_t s = s_idx[tid];
+    // Ws still holds the online net's output layer (the first backward step's weights)
+    for (int b = tid; b < B; b += nt) {
+        const int64_t s = s_idx[b];
         const int act = a.r_act[s];
-        const float* qt = Pa + (B + tid) * mw;
-        float mx = qt[0];
-        for (int j = 1; j < A; ++j) mx = qt[j] > mx ? qt[j] : mx;  // jnp.max
         const float notdone = a.r_done[s] ? 0.0f : 1.0f;
-        const float td = a.r_rew[s] + (a.gamma * mx) * notdone;
+        const float td = a.r_rew[s] + (a.gamma * s_mx[b]) * notdone;
         const bool ok = act >= 0 && act < A;
-        const float d = (ok ? Pa[tid * mw + act] : td) - td;  // (an action outside [0, A) adds nothing)
-        s_d[tid] = d;
-        s_act[tid] = ok ? act : -1;
+        s_d[b] = (ok ? s_q[b * 8 + act] : td) - td;  // (an action outside [0, A) adds nothing)
+        s_act[b] = ok ? act : -1;
     }
     __syncthreads();
     float loss = 0.0f;
-    {
-        for (int b = 0; b < B; ++b) loss = loss + s_d[b] * s_d[b];
-        loss = loss / (float)B;  // jnp.mean(jnp.square(q - td))
-    }
+    for (int b = 0; b < B; ++b) loss = loss + s_d[b] * s_d[b];
+    loss = loss / (float)B;  // jnp.mean(jnp.square(q - td))
     // d loss / d q[b][a_b] = 2 (q - td) / B: the output layer's deltas
+    float* D = Pa;   // [B][mw] deltas of layer l
+    float* D2 = Qa;  // [B][mw] deltas of layer l - 1
     for (int o = tid; o < B * A; o += nt) {
         const int b = o / A, j = o - b * A;
         const float dq = (s_act[b] == j) ? (s_d[b] + s_d[b]) / (float)B : 0.0f;
-        Qa[b * mw + j] = dq;
+        D[b * mw + j] = dq;
         a.sd[L - 1][o] = dq;
     }
     __syncthreads();
     // Adam's bias corrections for this step (count + 1): 1 - beta^count in double, rounded once
     const double p1 = a.ctr->beta1_pow * a.b1d, p2 = a.ctr->beta2_pow * a.b2d;
     const float bc1 = (float)(1.0 - p1), bc2 = (float)(1.0 - p2);
-    float* D = Qa;   // [B][mw] deltas of layer l
-    float* D2 = Pa;  // [B][mw] deltas of layer l - 1
     for (int l = L - 1; l >= 0; --l) {
         const int lo = a.out[l];
         for (int j = tid; j < lo; j += nt) {  // the bias: sum of the deltas over the batch, Adam
@@ -288,13 +339,17 @@ __global__ void __launch_bounds__(256) drl_dqn_grad_kernel(LearnArgs a) {
             a.online[bi] = dq_adam(a, a.online[bi], g, a.adam_m + bi, a.adam_v + bi, bc1, bc2);
         }
         if (l == 0) break;
-        const int li = a.out[l - 1];
-        const float* W = a.online + a.woff[l];  // (this step's weights: the update kernel writes them next)
+        const int li = a.out[l - 1], ls = li + 4;
+        if (l < L - 1) {  // (W_{L-1} is still staged from the forward pass)
+            __syncthreads();
+            dq_stage_w(a, a.online, l, Ws);  // (this step's weights: the update kernel writes them next)
+            __syncthreads();
+        }
         for (int o = tid; o < B * li; o += nt) {
             const int b = o / li, i = o - b * li;
-            float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            for (int j = 0; j < lo; ++j) s[j & 3] = s[j & 3] + D[b * mw + j] * W[(int64_t)j * li + i];
-            const float dz = M[((l - 1) * B + b) * mw + i] ? (s[0] + s[1]) + (s[2] + s[3]) : 0.0f;
+            float s4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            for (int j = 0; j < lo; ++j) s4[j & 3] = s4[j & 3] + D[b * mw + j] * Ws[j * ls + i];
+            const float dz = M[((l - 1) * B + b) * mw + i] ? (s4[0] + s4[1]) + (s4[2] + s4[3]) : 0.0f;
             D2[b * mw + i] = dz;
             a.sd[l - 1][o] = dz;
         }
@@ -327,12 +382,28 @@ __global__ void __launch_bounds__(256) drl_dqn_update_kernel(LearnArgs a) {
         const int64_t wi = a.woff[l] + (int64_t)s.row * p.in[l] + s.k;
         float w = a.online[wi];
         if (trained) {
-            const float* D = a.sd[l];
-            const float* X = l ? a.sh[l - 1] : a.sx;
+            const float* D = a.sd[l] + s.row;
+            const float* X = (l ? a.sh[l - 1] : a.sx) + s.k;
             const int xs = l ? p.in[l] : a.in4, ds = p.out[l];
+            const float m0 = a.adam_m[wi], v0 = a.adam_v[wi];
+            // the batch sum in row order, DQN_STAGE rows' operands loaded ahead
             float g = 0.0f;
-            for (int b = 0; b < a.batch; ++b) g = g + D[b * ds + s.row] * X[b * xs + s.k];
-            w = dq_adam(a, w, g, a.adam_m + wi, a.adam_v + wi, a.ctr->bc1, a.ctr->bc2);
+            for (int b0 = 0; b0 < a.batch; b0 += DQN_STAGE) {
+                float dv[DQN_STAGE], xv[DQN_STAGE];
+#pragma unroll
+                for (int q = 0; q < DQN_STAGE; ++q) {
+                    const int b = b0 + q < a.batch ? b0 + q : a.batch - 1;
+                    dv[q] = D[b * ds];
+                    xv[q] = X[b * xs];
+                }
+#pragma unroll
+                for (int q = 0; q < DQN_STAGE; ++q)
+                    if (b0 + q < a.batch) g = g + dv[q] * xv[q];
+            }
+            float m = m0, v = v0;
+            w = dq_adam(a, w, g, &m, &v, a.ctr->bc1, a.ctr->bc2);
+            a.adam_m[wi] = m;
+            a.adam_v[wi] = v;
             a.online[wi] = w;
             qnet_pack_write(p, l, e, s.k, w);
         }
@@ -366,9 +437,9 @@ __global__ void drl_dqn_init_kernel(DqnCounters* c, float epsilon) {
 
 hipError_t launch_dqn_train(const LearnArgs& a, size_t lds_grad, hipStream_t s) {
     if (a.trained)
-        hipLaunchKernelGGL(drl_dqn_grad_kernel, dim3((unsigned)a.nblk0), dim3(256), lds_grad, s, a);
+        hipLaunchKernelGGL(drl_dqn_grad_kernel, dim3((unsigned)a.nblk0), dim3(DQN_THREADS), lds_grad, s, a);
     else
-        hipLaunchKernelGGL(drl_dqn_grad_kernel, dim3(1), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(drl_dqn_grad_kernel, dim3(1), dim3(DQN_THREADS), 0, s, a);
     const int64_t n = a.pack.n_wfrag_elems + a.pack.n_bias;
     hipLaunchKernelGGL(drl_dqn_update_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
     return hipGetLastError();

@@ -1804,6 +1804,13 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
 // transitions than slots only the last `capacity` are written (what a
 // sequential add() loop leaves; XLA's duplicate-index scatter in add_many
 // leaves the order unspecified).
+// Slot of the r-th landing row: (cursor + first + r) % capacity without a
+// 64-bit division (r < capacity; base = (cursor + first) % capacity, host).
+__device__ __forceinline__ int64_t ring_slot(const ReplayArgs& a, uint32_t r) {
+    const int64_t s = a.base + (int64_t)r;
+    return s >= a.capacity ? s - a.capacity : s;
+}
+
 // One thread per float2 of the rows that land (flattened [rows][obs_floats/2]:
 // coalesced over rows, ring-buffer slots contiguous except at the wrap); the
 // thread of column 0 also copies the row's action / reward / done.
@@ -1813,7 +1820,7 @@ __global__ void __launch_bounds__(256) drl_replay_add_kernel(ReplayArgs a, FastD
     const uint32_t D2 = (uint32_t)a.obs_floats / 2u;
     const uint32_t r = __umulhi(k, dcols.m), col = k - r * D2;  // D2 >= 1; dcols.one handled by the host
     const int64_t i = a.first + r;
-    const int64_t slot = (a.cursor + i) % a.capacity;
+    const int64_t slot = ring_slot(a, r);
     const float2 o = reinterpret_cast<const float2*>(a.obs + i * a.obs_stride)[col];
     const float2 nx = reinterpret_cast<const float2*>(a.next_obs + i * a.next_obs_stride)[col];
     reinterpret_cast<float2*>(a.buf_obs + slot * a.obs_floats)[col] = o;
@@ -1834,7 +1841,7 @@ __global__ void __launch_bounds__(256) drl_replay_add16_kernel(ReplayArgs a, Fas
     const uint32_t D4 = (uint32_t)a.obs_floats / 4u;
     const uint32_t r = __umulhi(k, dcols.m), col = k - r * D4;  // D4 >= 2
     const int64_t i = a.first + r;
-    const int64_t slot = (a.cursor + i) % a.capacity;
+    const int64_t slot = ring_slot(a, r);
     const uint4 o = reinterpret_cast<const uint4*>(a.obs + i * a.obs_stride)[col];
     const uint4 nx = reinterpret_cast<const uint4*>(a.next_obs + i * a.next_obs_stride)[col];
     reinterpret_cast<uint4*>(a.buf_obs + slot * a.obs_floats)[col] = o;
@@ -1849,7 +1856,7 @@ __global__ void __launch_bounds__(256) drl_replay_add16_kernel(ReplayArgs a, Fas
 __global__ void drl_replay_add_rows_kernel(ReplayArgs a) {  // fallback for huge batches: block per row
     const int64_t i = a.first + blockIdx.x;
     if (i >= a.n) return;
-    const int64_t slot = (a.cursor + i) % a.capacity;
+    const int64_t slot = ring_slot(a, blockIdx.x);
     const int D2 = a.obs_floats / 2;
     const float2* so = reinterpret_cast<const float2*>(a.obs + i * a.obs_stride);
     const float2* sn = reinterpret_cast<const float2*>(a.next_obs + i * a.next_obs_stride);

@@ -5,6 +5,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -136,7 +137,7 @@ int num_cus() {
 struct DqnPlan {
     drl_dqn_layout pub;
     int64_t sx, sz0, sh[drl::QN_MAX_LAYERS], sd[drl::QN_MAX_LAYERS];  // float offsets within the scratch
-    int in4, maxw, tiles0;
+    int in4, maxw, tiles0, ws_floats;
     size_t lds;
 };
 
@@ -181,12 +182,17 @@ static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout
     o.bytes = o.scratch_off + sc * 4;
     P->tiles0 = (L.out[0] + drl::DQN_TILE - 1) / drl::DQN_TILE;
     o.grad_workgroups = 2 * P->tiles0;
-    // layer 0 (X + the weight tile) and the last workgroup (activations of both nets twice + the ReLU masks)
-    const size_t a0 = (size_t)(batch + drl::DQN_TILE) * P->in4 * 4;
-    const size_t a1 = (size_t)4 * batch * P->maxw * 4 + (size_t)r4((int64_t)(L.n_layers - 1) * batch * P->maxw);
+    // layer 0 (X, the weight tile, a code net's sampled rows) and the last workgroup (two activation buffers
+    // of one net, one layer's weights with rows of in + 4 floats, the online net's ReLU masks)
+    int ws = 0;
+    for (int l = 1; l < L.n_layers; ++l) ws = std::max(ws, L.out[l] * (L.in[l] + 4));
+    P->ws_floats = ws;
+    const int rw = L.code_w ? drl::lay::code_bytes(L.code_w) / 4 : 0;
+    const size_t a0 = ((size_t)(batch + drl::DQN_TILE) * P->in4 + (size_t)batch * rw) * 4;
+    const size_t a1 = ((size_t)2 * batch * P->maxw + ws) * 4 + (size_t)r4((int64_t)(L.n_layers - 1) * batch * P->maxw);
     P->lds = a0 > a1 ? a0 : a1;
     o.grad_lds_bytes = (int32_t)P->lds;
-    if (P->lds > 160 * 1024 - 1024) return fail("the learner's batch and widths do not fit the LDS of a CU");
+    if (P->lds > 156 * 1024) return fail("the learner's batch and widths do not fit the LDS of a CU");
     return 0;
 }
 
@@ -417,6 +423,7 @@ int drl_replay_add(const drl_replay* r, int64_t cursor, int64_t n, const float* 
     a.first = n > r->capacity ? n - r->capacity : 0;  // earlier ones would be overwritten in the same call
     a.cursor = cursor % r->capacity;
     a.capacity = r->capacity;
+    a.base = (a.cursor + a.first % r->capacity) % r->capacity;
     a.obs_floats = r->obs_floats;
     a.obs = d_obs;
     a.obs_stride = obs_stride;
@@ -495,6 +502,7 @@ int drl_dqn_train(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agen
     a.nblk0 = 2 * P.tiles0;
     a.maxw = P.maxw;
     a.in4 = P.in4;
+    a.ws_floats = P.ws_floats;
     for (int l = 0; l < L.n_layers; ++l) {
         a.in[l] = L.in[l];
         a.out[l] = L.out[l];

@@ -153,27 +153,36 @@ class QNetwork:
         self.pack()
 
     def load(self, weights: Sequence[torch.Tensor], biases: Sequence[torch.Tensor]):
-        """Set parameters (torch layout [out][in]) and re-pack."""
+        """Set parameters (torch layout [out][in]) and re-pack.  Nothing
+        changes if they are refused."""
         if len(weights) != len(self.weights) or len(biases) != len(self.biases):
             raise ValueError("layer count mismatch")
         for i, (w, b) in enumerate(zip(weights, biases)):
             if tuple(w.shape) != tuple(self.weights[i].shape) or tuple(b.shape) != tuple(self.biases[i].shape):
                 raise ValueError(f"layer {i}: shape {tuple(w.shape)} != {tuple(self.weights[i].shape)}")
-            self.weights[i] = w.detach().to(self.device, torch.float32).contiguous()
-            self.biases[i] = b.detach().to(self.device, torch.float32).contiguous()
+        ws = [w.detach().to(self.device, torch.float32) for w in weights]
+        bs = [b.detach().to(self.device, torch.float32) for b in biases]
+        self._validate(ws, bs)
+        for i, (w, b) in enumerate(zip(ws, bs)):
+            # (in place: a DQNLearner's net holds views of its agent block)
+            self.weights[i].copy_(w)
+            self.biases[i].copy_(b)
         self.pack()
 
-    def pack(self):
-        for t in (*self.weights, *self.biases):
+    def _validate(self, weights, biases):
+        for t in (*weights, *biases):
             if not bool(torch.isfinite(t).all()):
                 raise ValueError("weights and biases must be finite")
         if self.precision == "f32":  # fp16 hi/lo split range (include/dronerl.h DRL_QNET_F32)
             # the weights are split into fp16 pieces, and so is a code net's
             # layer-0 bias (packed as a weight); every other bias stays f32
-            split = list(self.weights) + ([self.biases[0]] if self.input == "code" else [])
+            split = list(weights) + ([biases[0]] if self.input == "code" else [])
             for t in split:
                 if float(t.abs().max()) >= 65504.0:
                     raise ValueError("f32 precision needs |w| < 65504 (and |b| < 65504 for a code net's layer 0)")
+
+    def pack(self):
+        self._validate(self.weights, self.biases)
         n = len(self.weights)
         wp = (_vp * n)(*[w.data_ptr() for w in self.weights])
         bp = (_vp * n)(*[b.data_ptr() for b in self.biases])

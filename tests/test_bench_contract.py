@@ -245,3 +245,12 @@ def test_launcher_refuses_more_nccl_ranks_than_gpus(monkeypatch, capsys):
     monkeypatch.setattr(bench, "visible_gpus", lambda: 0)
     assert bench.launch_ranks(["--gpus", "2"], 2) == 2
     assert "one GPU per rank" in capsys.readouterr().err
+
+
+def test_strong_split():
+    """BASELINE.json's num_envs=65536 over 1/2/4/8 ranks."""
+    assert [bench.strong_split(65536, n) for n in (1, 2, 4, 8)] == [65536, 32768, 16384, 8192]
+    with pytest.raises(ValueError, match="divisible"):
+        bench.strong_split(65536, 3)
+    with pytest.raises(ValueError):
+        bench.strong_split(0, 2)

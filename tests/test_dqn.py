@@ -180,8 +180,19 @@ def test_qnet_f32_weight_range_checked():
         net.load(w, net.biases)
     b = [t.clone() for t in net.biases]
     b[0][3] = float("inf")
-    with pytest.raises(ValueError, match="65504"):
+    with pytest.raises(ValueError, match="finite"):
         net.load(net.weights, b)
+    # only a code net's layer-0 bias is split into fp16 pieces; the
+    # obs net's biases stay f32, so a large finite bias is a valid net
+    b = [t.clone() for t in net.biases]
+    b[0][3], b[1][2] = 1e6, -2e5
+    net.load(net.weights, b)
+    cnet = QNetwork(294, (32,), precision="f32", input="code")
+    with pytest.raises(ValueError, match="65504"):
+        cnet.load(cnet.weights, b)
+    b = [t.clone() for t in cnet.biases]
+    b[1][2] = 1e6
+    cnet.load(cnet.weights, b)
 
 
 @gpu

@@ -252,7 +252,7 @@ def _host(t):
     return t.detach().cpu().numpy().copy()
 
 
-def _state_from_learner(learner):
+def state_from_learner(learner):
     st = O.LearnerState.start([(_host(w), _host(b)) for w, b in learner.params("online")],
                               [(_host(w), _host(b)) for w, b in learner.params("target")], 1.0)
     st.m = [(_host(w), _host(b)) for w, b in learner.params("m")]
@@ -263,7 +263,36 @@ def _state_from_learner(learner):
     return st
 
 
-def _assert_same(learner, st, where):
+class DevRows:
+    """A device tensor read on demand by the oracle (rows it indexes only):
+    the learner oracle gathers its 8 sampled rows of a 100,000-slot ring
+    without copying the ring."""
+
+    def __init__(self, t):
+        self.t = t
+
+    def __getitem__(self, idx):
+        if isinstance(idx, tuple):
+            return self[idx[0]][(slice(None),) + idx[1:]]
+        if isinstance(idx, (int, np.integer)):
+            return self.t[int(idx)].item()
+        return self.t[torch.as_tensor(np.asarray(idx), device=self.t.device)].cpu().numpy()
+
+
+def oracle_hparams(hp):
+    return O.HParams(batch=hp.batch, gamma=hp.gamma, learning_rate=hp.learning_rate, beta1=hp.beta1, beta2=hp.beta2,
+                     adam_eps=hp.adam_eps, tau=hp.tau, target_update_interval=hp.target_update_interval,
+                     epsilon_decay=hp.decay(), epsilon_end=hp.epsilon_end,
+                     epsilon_decay_every=hp.epsilon_decay_every, sample_seed=hp.sample_seed)
+
+
+def oracle_step_on_ring(st, ohp, rb, code_window):
+    """The oracle's learner step on the device ring's current contents."""
+    return O.learner_step(st, ohp, DevRows(rb.obs), DevRows(rb.next_obs), DevRows(rb.actions), DevRows(rb.rewards),
+                          DevRows(rb.dones), rb.size, code_window)
+
+
+def assert_same(learner, st, where):
     for k in ("online", "target", "m", "v"):
         for l, ((w, b), (ow, ob)) in enumerate(zip(learner.params(k), getattr(st, k))):
             assert np.array_equal(_host(w).view(np.uint32), ow.view(np.uint32)), (where, k, l, "W")
@@ -290,11 +319,8 @@ def test_learner_matches_oracle_bit_exact(sizes, inp, hp_kw, E, cap):
     every step (including the first steps, where a batch larger than the
     ring's size skips train_step: buffers.py can_sample)."""
     env, net, learner, rb, hp = _learner_setup(sizes, inp, hp_kw, E=E, cap=cap)
-    st = _state_from_learner(learner)
-    ohp = O.HParams(batch=hp.batch, gamma=hp.gamma, learning_rate=hp.learning_rate, tau=hp.tau,
-                    target_update_interval=hp.target_update_interval, epsilon_decay=hp.decay(),
-                    epsilon_end=hp.epsilon_end, epsilon_decay_every=hp.epsilon_decay_every,
-                    sample_seed=hp.sample_seed)
+    st = state_from_learner(learner)
+    ohp = oracle_hparams(hp)
     W = 7
     cur = env.new_code() if inp == "code" else torch.empty((E, 1, W, W, 6), device="cuda")
     nxt = env.new_code() if inp == "code" else torch.empty((E, 1, W, W, 6), device="cuda")
@@ -321,7 +347,7 @@ def test_learner_matches_oracle_bit_exact(sizes, inp, hp_kw, E, cap):
         trained += info["trained"]
         learner.train(rb)
         torch.cuda.synchronize()
-        _assert_same(learner, st, t)
+        assert_same(learner, st, t)
         cur, nxt = nxt, cur
     net.check_errors()
     env.check_errors()

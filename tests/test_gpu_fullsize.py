@@ -157,7 +157,13 @@ def test_c5_train_loop_segment_matches_oracle(E, seg):
 
 
 def test_c3_code_train_loop_matches_oracle():
+    """bench.TrainSegment's own calls at C3 (65,536 envs x 100 steps): the
+    env against the env oracle every step, the act against an f32 forward of
+    the live (learning) net, the learner (drl_dqn_train on the reference's
+    100,000-slot ring, train_jax.py:173) against oracle/dqn_learner.py bit for
+    bit every step, the code ring, sample() and the reset."""
     import bench
+    from tests.test_dqn_learner import assert_same, oracle_hparams, oracle_step_on_ring, state_from_learner
     from tests.test_policy_code import decode_code
     E, seg, N = 65536, 100, 8
     p = EnvParams(n_drones=N, grid_size=16)
@@ -167,6 +173,8 @@ def test_c3_code_train_loop_matches_oracle():
     o.reset(5 + np.arange(E))
     loop = bench.TrainSegment(env, seg, precision="f32", input="code")  # the bench's own loop (one stream, fused)
     assert loop.input == "code" and loop.net.precision == "f32" and loop.rb.code_radius == 3
+    assert loop.rb.capacity == 100_000 and loop.learner is not None
+    lst, ohp = state_from_learner(loop.learner), oracle_hparams(loop.learner.hp)
     W = env.layout.obs_window
     want0 = o.obs(3, 1)[:, 0]
     assert np.array_equal(decode_code(loop.code[0].cpu().numpy(), W), want0), "first code"
@@ -175,8 +183,13 @@ def test_c3_code_train_loop_matches_oracle():
     hist, prev = {}, want0
     for t in range(seg):
         b, nb = t % loop.NB, (t + 1) % loop.NB
+        assert np.float32(loop.learner.epsilon.item()) == lst.epsilon
         loop._act_step(t)
         loop._replay(t)
+        info = oracle_step_on_ring(lst, ohp, loop.rb, W)
+        assert info["trained"]  # 65,536 transitions from the first step on: can_sample
+        loop._learn()
+        assert_same(loop.learner, lst, f"C3 learner step {t}")
         a = loop.acts[b].cpu().numpy()
         np.testing.assert_array_equal(a[:, 1:], env.synth_actions(seed=2024, step=t).cpu().numpy()[:, 1:])
         assert ((a[:, 0] >= 0) & (a[:, 0] < 5)).all()

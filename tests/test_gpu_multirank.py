@@ -114,7 +114,7 @@ def test_bench_two_ranks_gloo_whole_job_json():
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
            "--gpus", "2", "--steps", "20", "--warmup", "5", "--envs", "4096", "--no-cpu-baseline", "--no-dqn",
            "--no-reset-bench", "--rollout-chunk", "0", "--loop-segments", "0", "--cached-steps", "10",
-           "--c5-envs", "1024"]
+           "--c5-envs", "1024", "--strong-envs", "4096"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -130,6 +130,10 @@ def test_bench_two_ranks_gloo_whole_job_json():
     c5 = d["c5"]
     assert c5["config"]["num_envs_total"] == 2 * 1024 and c5["steps"] >= 200 and c5["n_gpus"] == 2
     assert c5["value"] == pytest.approx(2 * 1024 * c5["steps"] / (c5["ms_per_step"] * c5["steps"] / 1e3), rel=1e-6)
+    # the strong-scaling sub-record: 4096 envs over the job, 2048 per rank
+    st = d["strong"]
+    assert st["scaling"] == "strong" and st["num_envs_total"] == 4096 and st["num_envs_per_gpu"] == 2048
+    assert st["value"] == pytest.approx(4096 * 20 / (st["ms_per_step"] * 20 / 1e3), rel=1e-6)
 
 
 def test_bench_gpus2_launches_its_own_ranks():

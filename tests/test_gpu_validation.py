@@ -82,6 +82,24 @@ def test_handle_set_state_clamps_and_flags_bad_mt_index():
     h.close()
 
 
+def test_handle_set_state_flags_bad_ground_code():
+    """a ground code outside the objects {0, 2, 3, 4, 5} is flagged
+    (DRL_ERR_BAD_STATE) instead of silently truncated to a nibble."""
+    from dronerl_amd.handle import DrlEnvHandle
+    h = DrlEnvHandle(P, 4, device=0)
+    h.reset()
+    d = h.get_state()
+    h.set_state(d)
+    assert h.errors() == 0
+    for bad in (1, 6, 7, 16, 200):
+        g = d["ground"].clone()
+        g[2, 5, 3] = bad
+        h.set_state(dict(d, ground=g))
+        assert h.errors() & DRL_ERR_BAD_STATE, bad
+        assert h.errors() == 0
+    h.close()
+
+
 def test_qnet_act_and_replay_checks():
     from dronerl_amd.dqn import QNetwork, ReplayBuffer
     net = QNetwork(294, (32, 32), device="cuda:0")
@@ -146,8 +164,12 @@ def test_hbm_probe_copies_and_reads():
         dst = torch.zeros_like(src)
         assert L.drl_hbm_probe(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), n, 0, st) == 0
         assert torch.equal(src, dst), n
-    scratch = torch.zeros(8 << 20, dtype=torch.uint8, device="cuda:0")
-    assert L.drl_hbm_probe(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(scratch.data_ptr()), n, 1, st) == 0
+    # the read form writes (if ever) only inside dst's first `bytes`: a dst of exactly n bytes,
+    # with a source whose every element hits the fold sentinel, is written in place and nowhere else
+    hit = torch.tensor([0x9E3779B9, 0, 0, 0], dtype=torch.int64).to(torch.int32).repeat(n // 16).to("cuda:0")
+    guard = torch.zeros(n // 4 + 64, dtype=torch.int32, device="cuda:0")
+    assert L.drl_hbm_probe(ctypes.c_void_p(hit.data_ptr()), ctypes.c_void_p(guard.data_ptr()), n, 1, st) == 0
     torch.cuda.synchronize()
+    assert torch.equal(guard[:n // 4], hit) and not guard[n // 4:].any()
     assert L.drl_hbm_probe(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), 15, 0, st) != 0
     assert L.drl_hbm_probe(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), 16, 2, st) != 0

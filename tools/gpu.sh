@@ -19,6 +19,8 @@
 #   reset     tools/reset_rate.py              RR_CFGS, RR_VARIANTS, RR_ARGS
 #   act       tools/time_act.py                ACT_ARGS
 #   ab        tools/ab.py per variant library  VARS="name:cfg ...", AB_ROUNDS, AB_STEPS, AB_VARIANTS
+#   loopprof  rocprofv3 kernel trace + stats of the graph-captured train loop (tools/loop_only.py) per config
+#             of LCFGS (c3 c5)                 -> gpurun_out/loopprof_<cfg>$TAG/
 #   run       any python command               CMD="tools/x.py ...", T_RUN (s), TAG
 set -u
 cd "$(dirname "$0")/.."
@@ -94,6 +96,12 @@ for task in "$@"; do
         v=${vc%%:*}; c=${vc##*:}
         step "ab-$v" 300 gpurun_out/ab_$v$TAG.log python tools/ab.py --lib tools/var_$v.so --config $c \
           --rounds ${AB_ROUNDS:-5} --steps ${AB_STEPS:-100} --variants ${AB_VARIANTS:-spec1,spec1_noobs}
+      done ;;
+    loopprof)
+      for c in ${LCFGS:-c3 c5}; do
+        OUT=gpurun_out/loopprof_$c$TAG; mkdir -p $OUT
+        step "loopprof-$c" 300 $OUT/trace.log rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv \
+          -- python3 tools/loop_only.py --config $c --segments ${LSEG:-3} ${LARGS:-}
       done ;;
     run)
       step run "${T_RUN:-300}" gpurun_out/run$TAG.log python ${CMD:?CMD=\"tools/x.py ...\"} ;;
