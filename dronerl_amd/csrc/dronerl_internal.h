@@ -329,6 +329,33 @@ __host__ __device__ inline PackSlot qnet_pack_slot(int l, int64_t e, int kt, int
     return s;
 }
 
+// The inverse: W_l[row][k] (k == -1: a code net's layer-0 bias) -> its
+// element in layer l's fragments.
+__host__ __device__ inline int64_t qnet_pack_elem(int l, int row, int k, int kt, int code_w) {
+    int t, j, g;
+    if (l == 0 && code_w > 0) {
+        const int cpg = lay::code_cpg(code_w);
+        int sl;
+        if (k < 0) {  // the bias: lane group 0's first padding slot
+            g = 0;
+            sl = 6 * cpg;
+        } else {
+            const int cell = k / 6, ch = k - 6 * cell, lc = cell % cpg;
+            g = cell / cpg;
+            sl = lc < (cpg & ~1) ? 12 * (lc / 2) + 2 * ch + (lc & 1) : 6 * (cpg - 1) + ch;
+        }
+        t = sl / 8;
+        j = sl % 8;
+    } else {
+        t = k / 32;
+        const int kk = k % 32;
+        g = kk < 16 ? kk / 4 : (kk - 16) / 4;
+        j = kk < 16 ? kk % 4 : 4 + (kk - 16) % 4;
+    }
+    const int m = row / 16, c = row % 16;
+    return (((int64_t)m * kt + t) * 64 + (g * 16 + c)) * 8 + j;
+}
+
 // Store weight w (W_l[row][k], or layer 0's bias for k == -1) at element e of
 // layer l's fragments as drl_qnet_pack does: a code net's charge-channel
 // weights carry the input's 1/100; DRL_QNET_F32 writes fp16 hi and lo =
@@ -363,12 +390,38 @@ constexpr int DQN_MAX_BATCH = 64;
 constexpr int DQN_TILE = 16;      // layer-0 units per workgroup of the gradient kernel
 constexpr int DQN_THREADS = 512;  // the gradient kernel's workgroup
 constexpr int DQN_STAGE = 8;      // loads each thread keeps in flight when the learner stages data
+constexpr int DQN_MAX_SEGS = 28;  // copy segments of the gradient kernel's prefetch
+
+// One segment of the gradient kernel's one-round staging into LDS: element
+// i < n of `src` lands at LDS float dst + (pad ? (i / row) * (row + pad) +
+// i % row : i) (kind 4: in float4 units, dst still in floats).  kind 0: f32
+// (or raw 32-bit) at src[i]; 1: 32-bit at src[sample[i]]; 2: u8 at
+// src[sample[i]], as 0.0f / 1.0f; 3: replay rows, element (b, k) =
+// src[sample[b] * row_words + k], k < row; 4: float4 at src[i].  rm: the
+// multiply-shift reciprocal of row (i / row == umulhi(i, rm); 0 when row == 1).
+struct DqSeg {
+    const void* src;
+    int n, dst, row, pad, kind;
+    uint32_t rm;
+};
 
 struct LearnArgs {
     int n_layers, batch, code_w, trained, nblk0, tiles0, maxw;
     int in[QN_MAX_LAYERS], out[QN_MAX_LAYERS];
     int in4;                          // layer 0's input row stride in LDS / scratch (in[0] rounded up to 4)
-    int ws_floats;                    // the last workgroup's weight staging: max over l >= 1 of out_l * (in_l + 4)
+    int xs0;                          // layer 0's weight row stride in LDS (>= in[0], = 2 mod 32: micro-tile banks)
+    uint32_t rm_in, rm_rw;            // DqSeg::rm of in[0] and of row_words
+    int ws_floats;                    // per-layer weight staging (no prefetch): max over l >= 1 of out_l * (in_l + 4)
+    int region_a;                     // the tail workgroup's LDS floats before its prefetched tail (activations, masks)
+    // prefetch != 0: every workgroup loads the last workgroup's data (later layers' weights of both nets,
+    // every bias, the online biases' moments, the sampled rows' action / reward / done) into LDS after
+    // region A in its first load round (tail[]); otherwise the last workgroup stages layer by layer
+    int prefetch, ntail;
+    int ntail_of[2];                  // the online tail's segments, then the target tail's (tail[ntail_of[0]..])
+    DqSeg tail[DQN_MAX_SEGS];
+    int tail_start[DQN_MAX_SEGS + 1];
+    float* smx;                       // scratch: max_a Q_target [batch] (the target tail's hand-off)
+    int tw[2][QN_MAX_LAYERS], tb[2][QN_MAX_LAYERS], tm[QN_MAX_LAYERS], tv[QN_MAX_LAYERS], tr;  // LDS float offsets
     int64_t woff[QN_MAX_LAYERS], boff[QN_MAX_LAYERS];  // float offsets of W_l / b_l in a parameter set
     float* online;
     float* target;
@@ -394,6 +447,8 @@ struct LearnArgs {
     int target_every, eps_every;
     // the act kernels' packed image of the online net (drl_dqn_update_kernel refreshes it)
     QnetPack pack;
+    int64_t wstart[QN_MAX_LAYERS + 1];  // update kernel: thread index of layer l's first weight; [L] = weights total
+    uint64_t* stamps;                   // DRL_DQN_STAMPS builds: [8 per workgroup (<= 64)][512 + last workgroup's]
 };
 
 hipError_t launch_qnet_pack(const QnetPack& p, hipStream_t s);

@@ -14,11 +14,13 @@
 // continuing schedule.
 //
 // Two launches:
-//   drl_dqn_grad_kernel: the workgroups split layer 0 of both nets (online on
-//     the sampled obs, target on next_obs) in 16-unit tiles; the last one to
-//     arrive (agent-scope release / acquire around a ticket counter) runs the
-//     later layers of both nets, the TD error, the loss, the backward pass to
-//     layer 0's deltas, and the bias updates; it writes the step's plan.
+//   drl_dqn_grad_kernel: workgroups split layer 0 of both nets (online on
+//     the sampled obs, target on next_obs) in 16-unit tiles and hand their
+//     pre-activations over with write-through stores and a ticket counter;
+//     one more workgroup prefetches everything else into LDS meanwhile, waits
+//     for the tickets, and runs the later layers of both nets, the TD error,
+//     the loss, the backward pass to layer 0's deltas and the bias updates;
+//     it writes the step's plan.
 //   drl_dqn_update_kernel: one thread per element of the act kernels' packed
 //     net (qnet_pack_slot: each weight has exactly one): the weight's gradient
 //     (sum over the batch of delta x input), the Adam update, the packed
@@ -27,8 +29,9 @@
 // Arithmetic order is fixed and contraction-free (each product rounded, then
 // each sum), so oracle/dqn_learner.py reproduces the result bit for bit:
 // a dot product of length n keeps four partial sums over k mod 4, each in k
-// order, combined (s0 + s1) + (s2 + s3), then + bias; a batch sum runs over
-// rows in order; Adam is optax's formula term by term.  The f32 constants are
+// order, combined (s0 + s1) + (s2 + s3), then + bias (dq_mm: one lane per
+// partial sum); a batch sum runs over rows in order; Adam is optax's formula
+// term by term.  The f32 constants are
 // what jax's weak typing makes of the python floats (1 - b1 rounded once).
 // The learner is latency-bound (a batch of 8 rows): VALU, no MFMA.
 #include <hip/hip_runtime.h>
@@ -40,6 +43,16 @@
 #pragma clang fp contract(off)
 
 namespace drl {
+
+// DRL_DQN_STAMPS (diagnostic builds, tools/learn_stamps.py): thread 0 of each
+// workgroup stores wall_clock64() (100 MHz) at phase boundaries into the 8 KB
+// the layout appends to the agent block's scratch.
+#ifdef DRL_DQN_STAMPS
+#define DQ_STAMP(i) \
+    do { if (threadIdx.x == 0) a.stamps[(i)] = wall_clock64(); } while (0)
+#else
+#define DQ_STAMP(i) do { } while (0)
+#endif
 
 namespace {
 
@@ -76,21 +89,6 @@ __device__ __forceinline__ float dq_input(const LearnArgs& a, const uint32_t* __
     }
 }
 
-// The learner's dot product (see the header): n4 float4s of x and w.
-__device__ __forceinline__ float dq_dot(const float* __restrict__ x, const float* __restrict__ w, int n4) {
-    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
-    const float4* xv = reinterpret_cast<const float4*>(x);
-    const float4* wv = reinterpret_cast<const float4*>(w);
-    for (int q = 0; q < n4; ++q) {
-        const float4 xa = xv[q], wa = wv[q];
-        s0 = s0 + xa.x * wa.x;
-        s1 = s1 + xa.y * wa.y;
-        s2 = s2 + xa.z * wa.z;
-        s3 = s3 + xa.w * wa.w;
-    }
-    return (s0 + s1) + (s2 + s3);
-}
-
 // optax.adam (scale_by_adam + scale(-lr)) + apply_updates, term by term:
 // mu = (1-b1) g + b1 mu; nu = (1-b2) g^2 + b2 nu; u = (mu / bc1) / (sqrt(nu / bc2)
 // + eps); p + u * (-lr).
@@ -109,38 +107,31 @@ __device__ __forceinline__ float dq_blend(const LearnArgs& a, float nw, float ol
     return a.tau * nw + a.one_minus_tau * old;
 }
 
-// The end of a learner step (the last workgroup, or the one workgroup of a
-// step without a sample): the bias half of the target blend, then thread 0
-// writes the counters and the plan drl_dqn_update_kernel reads.
-__device__ void dq_finish(const LearnArgs& a, int32_t step, int trained, float loss, float bc1, float bc2) {
-    const bool due = step % a.target_every == 0;
-    if (due) {
-        for (int l = 0; l < a.n_layers; ++l)
-            for (int j = threadIdx.x; j < a.out[l]; j += blockDim.x) {
-                const int64_t bi = a.boff[l] + j;
-                a.target[bi] = dq_blend(a, a.online[bi], a.target[bi]);
-            }
+// The counters at the end of a learner step (thread 0 of the last workgroup,
+// or of the one workgroup of a step without a sample): Adam's count and
+// powers, the loss, the epsilon decay, the plan drl_dqn_update_kernel reads,
+// step + 1.  ctr: the values the kernel read at its start.
+__device__ void dq_finish(const LearnArgs& a, const DqnCounters& ctr, int trained, float loss, float bc1, float bc2) {
+    if (threadIdx.x != 0) return;
+    DqnCounters* c = a.ctr;
+    const int32_t step = ctr.step;
+    if (trained) {
+        c->count = ctr.count + 1;
+        c->beta1_pow = ctr.beta1_pow * a.b1d;
+        c->beta2_pow = ctr.beta2_pow * a.b2d;
     }
-    if (threadIdx.x == 0) {
-        DqnCounters* c = a.ctr;
-        if (trained) {
-            c->count = c->count + 1;
-            c->beta1_pow = c->beta1_pow * a.b1d;
-            c->beta2_pow = c->beta2_pow * a.b2d;
-        }
-        c->loss = trained ? loss : 0.0f;
-        float eps = c->epsilon;
-        if (step % a.eps_every == 0) {
-            const float d = eps * a.eps_decay;
-            eps = d > a.eps_end ? d : a.eps_end;  // jnp.maximum
-        }
-        c->epsilon = eps;
-        c->trained = trained;
-        c->target_due = due ? 1 : 0;
-        c->bc1 = bc1;
-        c->bc2 = bc2;
-        c->step = step + 1;
+    c->loss = trained ? loss : 0.0f;
+    float eps = ctr.epsilon;
+    if (step % a.eps_every == 0) {
+        const float d = eps * a.eps_decay;
+        eps = d > a.eps_end ? d : a.eps_end;  // jnp.maximum
     }
+    c->epsilon = eps;
+    c->trained = trained;
+    c->target_due = step % a.target_every == 0 ? 1 : 0;
+    c->bc1 = bc1;
+    c->bc2 = bc2;
+    c->step = step + 1;
 }
 
 // Copy n words src(i) -> dst(i) with every thread holding DQN_STAGE loads in
@@ -164,159 +155,363 @@ __device__ __forceinline__ void dq_stage(int n, Src src, Dst dst) {
     }
 }
 
-// Layer l's weights of one net -> LDS, rows padded to in + 4 floats (float4
-// rows whose starts fall on different banks).
+// Layer l's weights of one net -> LDS, rows padded to in + 4 floats (in is a
+// multiple of 32: consecutive rows of a micro-tile start 4 banks apart).
 __device__ __forceinline__ void dq_stage_w(const LearnArgs& a, const float* P, int l, float* Ws) {
     const int li = a.in[l], lo = a.out[l], ls = li + 4;
     const float* src = P + a.woff[l];
     dq_stage(li * lo, [&](int i) { return src[i]; }, [&](int i, float v) { Ws[(i / li) * ls + (i % li)] = v; });
 }
 
+typedef const __attribute__((address_space(1))) float gcf32;
+typedef float dq_f4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) dq_f4 gcf4;
+typedef const __attribute__((address_space(1))) uint8_t gcu8;
+
+__device__ __forceinline__ uint32_t dq_div(uint32_t i, const DqSeg& g) { return g.rm ? __umulhi(i, g.rm) : i; }
+
+// (global-address-space loads: a flat load would also count against the LDS counter)
+__device__ __forceinline__ dq_f4 dq_seg_load(const DqSeg& g, int i, const int64_t* sidx, int64_t row_words) {
+    switch (g.kind) {
+        case 0: return dq_f4{((gcf32*)g.src)[i], 0.0f, 0.0f, 0.0f};
+        case 1: return dq_f4{((gcf32*)g.src)[sidx[i]], 0.0f, 0.0f, 0.0f};
+        case 2: return dq_f4{((gcu8*)g.src)[sidx[i]] ? 1.0f : 0.0f, 0.0f, 0.0f, 0.0f};
+        case 3: {
+            const int b = (int)dq_div((uint32_t)i, g);
+            return dq_f4{((gcf32*)g.src)[sidx[b] * row_words + (i - b * g.row)], 0.0f, 0.0f, 0.0f};
+        }
+        default: return ((gcf4*)g.src)[i];
+    }
+}
+__device__ __forceinline__ int dq_seg_dst(const DqSeg& g, int i) {
+    if (!g.pad) return g.dst + (g.kind == 4 ? 4 * i : i);
+    const int r = (int)dq_div((uint32_t)i, g), c = i - r * g.row;
+    return g.dst + (g.kind == 4 ? 4 * (r * (g.row + g.pad) + c) : r * (g.row + g.pad) + c);
+}
+
+// The segments seg[0..ns) (start: their prefix sums, start[ns] = total) in
+// one pass: DQN_STAGE loads per thread in flight, then their LDS stores.  A
+// thread's elements only move forward, so its segment is carried in
+// registers and re-read from LDS only when it crosses into the next one.
+__device__ __forceinline__ void dq_stage_segs(float* lds, const DqSeg* seg, const int* start, int ns,
+                                              const int64_t* sidx, int64_t row_words) {
+    const int n = start[ns], nt = blockDim.x;
+    int g = 0, ge = start[1], gs = 0;
+    DqSeg cur = seg[0];
+    for (int base = threadIdx.x; base < n; base += DQN_STAGE * nt) {
+        dq_f4 v[DQN_STAGE];
+        int d[DQN_STAGE];
+        bool w4[DQN_STAGE];
+#pragma unroll
+        for (int q = 0; q < DQN_STAGE; ++q) {
+            const int i = base + q * nt;
+            d[q] = -1;
+            w4[q] = false;
+            if (i < n) {
+                while (i >= ge) {
+                    ++g;
+                    cur = seg[g];
+                    gs = ge;
+                    ge = start[g + 1];
+                }
+                v[q] = dq_seg_load(cur, i - gs, sidx, row_words);
+                d[q] = dq_seg_dst(cur, i - gs);
+                w4[q] = cur.kind == 4;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < DQN_STAGE; ++q) {
+            if (d[q] < 0) continue;
+            if (w4[q]) *reinterpret_cast<dq_f4*>(lds + d[q]) = v[q];
+            else lds[d[q]] = v[q].x;
+        }
+    }
+}
+
+// Write-through (sc1) store / load of a handed-off word (MI355X_MICROARCH.md
+// § visibility, Valid forms, table row 1: every store and every load of the
+// bytes sc1; the consumer polls the one agent-scope counter with sc1 loads).
+typedef __attribute__((address_space(1))) uint32_t gu32;
+__device__ __forceinline__ void dq_store_sc1(float* p, float v) {
+    __hip_atomic_store((gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float dq_load_sc1(const float* p) {
+    return __uint_as_float(__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// The learner's dot products as micro-tiles: z[b][j] = sum over k < n of
+// X[b * xs + k * xk] * W[j * wr + k * wk] for b < B, j < J.  A group of four
+// lanes takes two rows b by two outputs j; lane c of the group accumulates
+// the partial sums of k = c (mod 4) in k order -- exactly the canonical four
+// partial sums -- and the group combines them as (s0 + s1) + (s2 + s3) by
+// lane swaps (float addition commutes, so every lane holds the same value).
+// out(b, j, z) runs once per output, on lane c == 0.  Every lane of a wave
+// runs every iteration (the swaps need the whole wave).
+template <class Out>
+__device__ __forceinline__ void dq_mm(const float* X, int xs, int xk, const float* W, int wr, int wk, int n, int B,
+                                      int J, Out out) {
+    const int nbp = (B + 1) / 2, njp = (J + 1) / 2, items = nbp * njp * 4;
+    for (int base = 0; base < items; base += blockDim.x) {
+        const int it = base + threadIdx.x;
+        const bool live = it < items;
+        const int c = it & 3, pr = it >> 2;
+        const int jp = pr % njp, bp = pr / njp;
+        const int b0 = 2 * bp, b1 = min(b0 + 1, B - 1), j0 = 2 * jp, j1 = min(j0 + 1, J - 1);
+        float s00 = 0.0f, s01 = 0.0f, s10 = 0.0f, s11 = 0.0f;
+        if (live) {
+            const float *x0 = X + b0 * xs, *x1 = X + b1 * xs, *w0 = W + j0 * wr, *w1 = W + j1 * wr;
+#pragma unroll 4
+            for (int k = c; k < n; k += 4) {
+                const float a0 = x0[k * xk], a1 = x1[k * xk], c0 = w0[k * wk], c1 = w1[k * wk];
+                s00 = s00 + a0 * c0;
+                s01 = s01 + a0 * c1;
+                s10 = s10 + a1 * c0;
+                s11 = s11 + a1 * c1;
+            }
+        }
+        s00 = s00 + __shfl_xor(s00, 1);
+        s01 = s01 + __shfl_xor(s01, 1);
+        s10 = s10 + __shfl_xor(s10, 1);
+        s11 = s11 + __shfl_xor(s11, 1);
+        s00 = s00 + __shfl_xor(s00, 2);
+        s01 = s01 + __shfl_xor(s01, 2);
+        s10 = s10 + __shfl_xor(s10, 2);
+        s11 = s11 + __shfl_xor(s11, 2);
+        if (live && c == 0) {
+            out(b0, j0, s00);
+            if (j1 != j0) out(b0, j1, s01);
+            if (b1 != b0) {
+                out(b1, j0, s10);
+                if (j1 != j0) out(b1, j1, s11);
+            }
+        }
+    }
+}
+
+// The later layers of net n (1 = target, 0 = online) for the B sampled rows,
+// from its layer-0 pre-activations (handed over write-through) and its
+// prefetched (or staged) weights; Pa ends holding Q [B][A].  The online net
+// also stores its hidden activations (the update kernel's inputs) and ReLU
+// masks.  Returns the buffer holding Q.
+__device__ float* dq_forward(const LearnArgs& a, int n, float* Pa, float* Qa, float* Ws, uint8_t* M, const float* T) {
+    const int B = a.batch, L = a.n_layers, mw = a.maxw, out0 = a.out[0];
+    const float* Pn = n ? a.target : a.online;
+    dq_stage(B * out0, [&](int i) { return dq_load_sc1(a.sz0 + (int64_t)n * B * out0 + i); }, [&](int i, float z) {
+        const int b = i / out0, j = i - b * out0;
+        const float h = z > 0.0f ? z : 0.0f;
+        Pa[b * mw + j] = h;
+        if (n == 0) {
+            a.sh[0][i] = h;
+            M[b * mw + j] = z > 0.0f;
+        }
+    });
+    for (int l = 1; l < L; ++l) {
+        const int li = a.out[l - 1], lo = a.out[l], ls = li + 4;
+        const bool hidden = l < L - 1;
+        const float* W = a.prefetch ? T + a.tw[n][l] : Ws;
+        const float* bias = T + a.tb[n][l];
+        if (!a.prefetch) dq_stage_w(a, Pn, l, Ws);
+        __syncthreads();
+        dq_mm(Pa, mw, 1, W, ls, 1, li, B, lo, [&](int b, int j, float d) {
+            const float z = d + bias[j];
+            if (hidden) {
+                const float h = z > 0.0f ? z : 0.0f;
+                Qa[b * mw + j] = h;
+                if (n == 0) {
+                    a.sh[l][b * lo + j] = h;
+                    M[(l * B + b) * mw + j] = z > 0.0f;
+                }
+            } else {
+                Qa[b * mw + j] = z;
+            }
+        });
+        __syncthreads();
+        float* t = Pa;
+        Pa = Qa;
+        Qa = t;
+    }
+    return Pa;
+}
+
+// Poll an agent-scope counter (sc1 loads, one lane) until it reaches `want`;
+// false after a bounded wait (DqnCounters::pad[0] = 1).
+__device__ __forceinline__ bool dq_wait(const LearnArgs& a, int32_t* word, uint32_t want) {
+    uint32_t spins = 0;
+    while (__hip_atomic_load((gu32*)word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 24)) {
+            a.ctr->pad[0] = 1;
+            return false;
+        }
+    }
+    return true;
+}
+
 }  // namespace
 
+// Workgroups 0 .. nblk0-1: layer 0 of one net for DQN_TILE units each;
+// workgroup nblk0 (target tail) and nblk0 + 1 (online tail): each prefetches
+// its net's later layers (the online tail also the biases, their moments and
+// the sampled rows' action / reward / done) while the layer-0 workgroups
+// compute, waits for their tickets, and runs its net's later layers; the
+// target tail hands max_a Q_target over (write-through, a second counter), the
+// online tail then runs the TD error, the loss, the backward pass and the bias
+// updates.
 __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) {
     extern __shared__ float4 dq_lds4[];
     float* lds = reinterpret_cast<float*>(dq_lds4);
     __shared__ int64_t s_idx[DQN_MAX_BATCH];
     __shared__ float s_d[DQN_MAX_BATCH], s_mx[DQN_MAX_BATCH], s_q[DQN_MAX_BATCH * 8];
     __shared__ int s_act[DQN_MAX_BATCH];
-    __shared__ int s_last;
+    __shared__ DqSeg s_seg[DQN_MAX_SEGS];
+    __shared__ int s_start[DQN_MAX_SEGS + 1];
+    __shared__ int s_flag;
     const int tid = threadIdx.x, nt = blockDim.x;
     const int B = a.batch, L = a.n_layers;
-    // every workgroup reads the step before it arrives; the last one writes it
-    const int32_t step = a.ctr->step;
-    if (!a.trained) {  // buffer.can_sample is false: no train_step this step (loss 0)
-        dq_finish(a, step, 0, 0.0f, 0.0f, 0.0f);
+    // the counters as this step starts (the online tail writes them after
+    // every other workgroup has arrived)
+    DqnCounters ctr;
+    ctr.step = a.ctr->step;
+    ctr.count = a.ctr->count;
+    ctr.epsilon = a.ctr->epsilon;
+    ctr.beta1_pow = a.ctr->beta1_pow;
+    ctr.beta2_pow = a.ctr->beta2_pow;
+    DQ_STAMP(8 * blockIdx.x + 0);
+    if (!a.trained) {  // buffer.can_sample is false: no train_step this step (loss 0); the bias half of the target blend
+        if (ctr.step % a.target_every == 0)
+            for (int l = 0; l < L; ++l)
+                for (int j = tid; j < a.out[l]; j += nt) {
+                    const int64_t bi = a.boff[l] + j;
+                    a.target[bi] = dq_blend(a, a.online[bi], a.target[bi]);
+                }
+        dq_finish(a, ctr, 0, 0.0f, 0.0f, 0.0f);
         return;
     }
-    // ---- layer 0 of one net for DQN_TILE units (all workgroups)
-    const int net = blockIdx.x / a.tiles0, u0 = (blockIdx.x % a.tiles0) * DQN_TILE;
-    const int in = a.in[0], in4 = a.in4, out0 = a.out[0];
-    const int nu = min(DQN_TILE, out0 - u0);
-    if (tid < B) s_idx[tid] = dq_sample(a.seed, step, tid, a.size);
-    __syncthreads();
-    float* X = lds;                // [B][in4] the sampled rows (obs for the online net, next_obs for the target)
-    float* Wt = lds + B * in4;     // [DQN_TILE][in4] this tile's layer-0 weight rows
-    const uint32_t* rows = net ? a.r_next : a.r_obs;
-    const int rw = (int)a.row_words;
-    const float* P = net ? a.target : a.online;
-    // this tile's weight rows are contiguous in the set: one flat copy
-    const float* wsrc = P + a.woff[0] + (int64_t)u0 * in;
-    dq_stage(nu * in, [&](int i) { return wsrc[i]; }, [&](int i, float v) { Wt[(i / in) * in4 + (i % in)] = v; });
-    if (a.code_w) {  // the B code rows -> LDS, then decoded from there
-        uint32_t* R = reinterpret_cast<uint32_t*>(Wt + DQN_TILE * in4);  // [B][rw]
-        dq_stage(B * rw, [&](int i) { return __uint_as_float(rows[s_idx[i / rw] * a.row_words + (i % rw)]); },
-                 [&](int i, float v) { R[i] = __float_as_uint(v); });
+    if (tid < B) s_idx[tid] = dq_sample(a.seed, ctr.step, tid, a.size);
+    const int in = a.in[0], in4 = a.in4, xs0 = a.xs0, out0 = a.out[0];
+    if (blockIdx.x < (unsigned)a.nblk0) {
+        // ---- layer 0 of one net for DQN_TILE units
+        const int net = blockIdx.x / a.tiles0, u0 = (blockIdx.x % a.tiles0) * DQN_TILE;
+        const int nu = min(DQN_TILE, out0 - u0);
+        float* X = lds;                   // [B][in4] the sampled rows (obs: online net, next_obs: target)
+        float* Wt = lds + B * in4;        // [DQN_TILE][xs0] this tile's layer-0 weight rows, then its biases
+        float* Bt = Wt + DQN_TILE * xs0;
+        const int rw = (int)a.row_words;
+        const float* P = net ? a.target : a.online;
+        if (tid == 0) {
+            const uint32_t* rows = net ? a.r_next : a.r_obs;
+            // the tile's weight rows are contiguous in the set: one flat copy into rows of xs0
+            s_seg[0] = DqSeg{P + a.woff[0] + (int64_t)u0 * in, nu * in, B * in4, in, xs0 - in, 0, a.rm_in};
+            s_seg[1] = DqSeg{P + a.boff[0] + u0, nu, B * in4 + DQN_TILE * xs0, 1, 0, 0, 0u};
+            if (a.code_w)  // the code rows, decoded from LDS below
+                s_seg[2] = DqSeg{rows, B * rw, B * in4 + DQN_TILE * xs0 + DQN_TILE, rw, 0, 3, a.rm_rw};
+            else
+                s_seg[2] = DqSeg{rows, B * in, 0, in, in4 - in, 3, a.rm_in};
+            s_start[0] = 0;
+            s_start[1] = nu * in;
+            s_start[2] = nu * in + nu;
+            s_start[3] = nu * in + nu + s_seg[2].n;
+        }
+        if (!a.code_w)  // the f32 rows' padding columns
+            for (int e = tid; e < B * (in4 - in); e += nt) X[(e / (in4 - in)) * in4 + in + e % (in4 - in)] = 0.0f;
         __syncthreads();
-        for (int e = tid; e < B * in4; e += nt) {
-            const int b = e / in4, k = e - b * in4;
-            X[e] = k < in ? dq_input(a, R + b * rw, 0, k) : 0.0f;
+        DQ_STAMP(8 * blockIdx.x + 1);
+        dq_stage_segs(lds, s_seg, s_start, 3, s_idx, a.row_words);
+        __syncthreads();
+        DQ_STAMP(8 * blockIdx.x + 2);
+        if (a.code_w) {  // one thread per (row, cell): its six channels
+            const uint16_t* R = reinterpret_cast<const uint16_t*>(Bt + DQN_TILE);  // [B][rw] words
+            const int W = a.code_w, cells = W * W, cpg = lay::code_cpg(W), cpg8 = lay::code_cpg8(W);
+            for (int e = tid; e < B * cells; e += nt) {
+                const int b = e / cells, cl = e - b * cells;
+                const int grp = (cl >= cpg) + (cl >= 2 * cpg) + (cl >= 3 * cpg);
+                const uint32_t h = R[2 * b * rw + grp * cpg8 + (cl - grp * cpg)];
+                const uint32_t obj = h & 7u, air = h >> 3;
+                float* x = X + b * in4 + 6 * cl;
+                x[0] = air ? 1.0f : 0.0f;
+                x[1] = (obj == OBJ_PACKET || (air & 0x80u)) ? 1.0f : 0.0f;
+                x[2] = obj == OBJ_DROPZONE ? 1.0f : 0.0f;
+                x[3] = obj == OBJ_STATION ? 1.0f : 0.0f;
+                x[4] = air ? (float)((int)(air & 0x7fu) - 1) / 100.0f : 0.0f;
+                x[5] = obj == OBJ_SKYSCRAPER ? 1.0f : 0.0f;
+            }
+            for (int e = tid; e < B * (in4 - in); e += nt) X[(e / (in4 - in)) * in4 + in + e % (in4 - in)] = 0.0f;
+            __syncthreads();
         }
-    } else {
-        dq_stage(B * in4, [&](int i) {
-            const int b = i / in4, k = i - b * in4;
-            return k < in ? __uint_as_float(rows[s_idx[b] * a.row_words + k]) : 0.0f;
-        }, [&](int i, float v) { X[i] = v; });
-    }
-    for (int e = tid; e < (DQN_TILE - nu) * in4; e += nt) Wt[nu * in4 + e] = 0.0f;  // (a partial last tile)
-    __syncthreads();
-    if (net == 0 && u0 == 0)  // the update kernel's layer-0 inputs
-        for (int e = tid; e < B * in4; e += nt) a.sx[e] = X[e];
-    for (int o = tid; o < DQN_TILE * B; o += nt) {
-        const int u = o % DQN_TILE, b = o / DQN_TILE;
-        if (u < nu) {
-            const float z = dq_dot(X + b * in4, Wt + u * in4, in4 / 4) + P[a.boff[0] + u0 + u];
-            a.sz0[((int64_t)net * B + b) * out0 + u0 + u] = z;
-        }
-    }
-    // publish: stores drained, one agent-scope release, the ticket; the last
-    // arriver acquires (cdna_hip_programming.md §5 split-K recipe)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (net == 0 && u0 == 0)  // the update kernel's layer-0 inputs
+            for (int e = tid; e < B * in4; e += nt) a.sx[e] = X[e];
+        float* z0 = a.sz0 + (int64_t)net * B * out0 + u0;
+        dq_mm(X, in4, 1, Wt, xs0, 1, in, B, nu, [&](int b, int u, float z) { dq_store_sc1(z0 + b * out0 + u, z + Bt[u]); });
+        // hand-off: every wave drains its write-through stores, the workgroup
+        // barrier, one agent-scope ticket
+        DQ_STAMP(8 * blockIdx.x + 3);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int t = __hip_atomic_fetch_add(&a.ctr->arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (t == a.nblk0 - 1);
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(&a.ctr->arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        DQ_STAMP(8 * blockIdx.x + 4);
+        return;
     }
-    __syncthreads();
-    if (!s_last) return;
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&a.ctr->arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
 
-    // ---- the last workgroup: later layers (one net at a time, each layer's
-    // weights staged in LDS), TD error, backward, biases
+    // ---- the tails: n = 1 (target, workgroup nblk0), n = 0 (online, nblk0 + 1)
+    const int n = blockIdx.x == (unsigned)a.nblk0 ? 1 : 0;
     const int mw = a.maxw;
     float* Pa = lds;                   // [B][mw] activations of the current layer
     float* Qa = lds + B * mw;          // [B][mw] the next layer's
-    float* Ws = lds + 2 * B * mw;      // one layer's weights, rows of in + 4 floats
-    uint8_t* M = reinterpret_cast<uint8_t*>(Ws + a.ws_floats);  // [L-1][B][mw] online ReLU masks (z > 0)
+    float* Ws = lds + 2 * B * mw;      // (no prefetch) one layer's weights, rows of in + 4 floats
+    uint8_t* M = reinterpret_cast<uint8_t*>(Ws + (a.prefetch ? 0 : a.ws_floats));  // [L-1][B][mw] online ReLU masks
+    const float* T = lds + a.region_a;  // the prefetched tail
+    const int ns = a.ntail_of[n], g0 = n ? a.ntail_of[0] : 0;
+    if (tid < ns) s_seg[tid] = a.tail[g0 + tid];
+    if (tid <= ns) s_start[tid] = a.tail_start[g0 + tid] - a.tail_start[g0];
+    __syncthreads();
+    DQ_STAMP(8 * blockIdx.x + 1);
+    dq_stage_segs(lds, s_seg, s_start, ns, s_idx, a.row_words);
+    DQ_STAMP(8 * blockIdx.x + 2);
+    if (tid == 0) s_flag = dq_wait(a, &a.ctr->arrive, (uint32_t)a.nblk0);  // every layer-0 workgroup's ticket
+    __syncthreads();
+    DQ_STAMP(512 + 8 * n + 0);
+    if (!s_flag) return;
+    Pa = dq_forward(a, n, Pa, Qa, Ws, M, T);
+    Qa = Pa == lds ? lds + B * mw : lds;
+    DQ_STAMP(512 + 8 * n + 1);
     const int A = a.out[L - 1];
-    for (int n = 1; n >= 0; --n) {  // the target net on next_obs, then the online net on obs
-        const float* Pn = n ? a.target : a.online;
-        dq_stage(B * out0, [&](int i) { return a.sz0[(int64_t)n * B * out0 + i]; }, [&](int i, float z) {
-            const int b = i / out0, j = i - b * out0;
-            const float h = z > 0.0f ? z : 0.0f;
-            Pa[b * mw + j] = h;
-            if (n == 0) {
-                a.sh[0][i] = h;
-                M[b * mw + j] = z > 0.0f;
-            }
-        });
-        for (int l = 1; l < L; ++l) {
-            const int li = a.out[l - 1], lo = a.out[l], ls = li + 4;
-            const bool hidden = l < L - 1;
-            dq_stage_w(a, Pn, l, Ws);
-            __syncthreads();
-            for (int o = tid; o < B * lo; o += nt) {
-                const int b = o / lo, j = o - b * lo;
-                const float z = dq_dot(Pa + b * mw, Ws + j * ls, li / 4) + Pn[a.boff[l] + j];
-                if (hidden) {
-                    const float h = z > 0.0f ? z : 0.0f;
-                    Qa[b * mw + j] = h;
-                    if (n == 0) {
-                        a.sh[l][o] = h;
-                        M[(l * B + b) * mw + j] = z > 0.0f;
-                    }
-                } else {
-                    Qa[b * mw + j] = z;
-                }
-            }
-            __syncthreads();
-            float* t = Pa;
-            Pa = Qa;
-            Qa = t;
-        }
-        // Pa: the net's Q [B][A]
+    if (n == 1) {  // max_a Q_target, handed over write-through behind the second ticket
         for (int b = tid; b < B; b += nt) {
-            if (n == 1) {
-                float mx = Pa[b * mw];
-                for (int j = 1; j < A; ++j) mx = Pa[b * mw + j] > mx ? Pa[b * mw + j] : mx;  // jnp.max
-                s_mx[b] = mx;
-            } else {
-                for (int j = 0; j < A; ++j) s_q[b * 8 + j] = Pa[b * mw + j];
-            }
+            float mx = Pa[b * mw];
+            for (int j = 1; j < A; ++j) mx = Pa[b * mw + j] > mx ? Pa[b * mw + j] : mx;  // jnp.max
+            dq_store_sc1(a.smx + b, mx);
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(&a.ctr->pad[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
     }
-    // Ws still holds the online net's output layer (the first backward step's weights)
+    for (int b = tid; b < B; b += nt)
+        for (int j = 0; j < A; ++j) s_q[b * 8 + j] = Pa[b * mw + j];
+    if (tid == 0) {  // the target tail's ticket; then both counters are free for the next step
+        s_flag = dq_wait(a, &a.ctr->pad[1], 1u);
+        __hip_atomic_store((gu32*)&a.ctr->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gu32*)&a.ctr->pad[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_flag) return;
+    for (int b = tid; b < B; b += nt) s_mx[b] = dq_load_sc1(a.smx + b);
+    __syncthreads();
+    DQ_STAMP(512 + 2);
+    float loss = 0.0f;
     for (int b = tid; b < B; b += nt) {
-        const int64_t s = s_idx[b];
-        const int act = a.r_act[s];
-        const float notdone = a.r_done[s] ? 0.0f : 1.0f;
-        const float td = a.r_rew[s] + (a.gamma * s_mx[b]) * notdone;
+        const int act = __float_as_int(T[a.tr + b]);
+        const float rew = T[a.tr + B + b];
+        const float notdone = T[a.tr + 2 * B + b] != 0.0f ? 0.0f : 1.0f;
+        const float td = rew + (a.gamma * s_mx[b]) * notdone;
         const bool ok = act >= 0 && act < A;
         s_d[b] = (ok ? s_q[b * 8 + act] : td) - td;  // (an action outside [0, A) adds nothing)
         s_act[b] = ok ? act : -1;
     }
     __syncthreads();
-    float loss = 0.0f;
     for (int b = 0; b < B; ++b) loss = loss + s_d[b] * s_d[b];
     loss = loss / (float)B;  // jnp.mean(jnp.square(q - td))
+    DQ_STAMP(512 + 3);
     // d loss / d q[b][a_b] = 2 (q - td) / B: the output layer's deltas
     float* D = Pa;   // [B][mw] deltas of layer l
     float* D2 = Qa;  // [B][mw] deltas of layer l - 1
@@ -328,63 +523,70 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) 
     }
     __syncthreads();
     // Adam's bias corrections for this step (count + 1): 1 - beta^count in double, rounded once
-    const double p1 = a.ctr->beta1_pow * a.b1d, p2 = a.ctr->beta2_pow * a.b2d;
+    const double p1 = ctr.beta1_pow * a.b1d, p2 = ctr.beta2_pow * a.b2d;
     const float bc1 = (float)(1.0 - p1), bc2 = (float)(1.0 - p2);
+    const bool due = ctr.step % a.target_every == 0;
     for (int l = L - 1; l >= 0; --l) {
         const int lo = a.out[l];
-        for (int j = tid; j < lo; j += nt) {  // the bias: sum of the deltas over the batch, Adam
+        for (int j = tid; j < lo; j += nt) {  // the bias: sum of the deltas over the batch, Adam, target blend
             float g = 0.0f;
             for (int b = 0; b < B; ++b) g = g + D[b * mw + j];
             const int64_t bi = a.boff[l] + j;
-            a.online[bi] = dq_adam(a, a.online[bi], g, a.adam_m + bi, a.adam_v + bi, bc1, bc2);
+            float m = T[a.tm[l] + j], v = T[a.tv[l] + j];
+            const float b0 = T[a.tb[0][l] + j], tb = T[a.tb[1][l] + j];
+            const float nb = dq_adam(a, b0, g, &m, &v, bc1, bc2);
+            a.online[bi] = nb;
+            a.adam_m[bi] = m;
+            a.adam_v[bi] = v;
+            if (due) a.target[bi] = dq_blend(a, nb, tb);
         }
         if (l == 0) break;
         const int li = a.out[l - 1], ls = li + 4;
-        if (l < L - 1) {  // (W_{L-1} is still staged from the forward pass)
+        const float* W = a.prefetch ? T + a.tw[0][l] : Ws;
+        if (!a.prefetch && l < L - 1) {  // (W_{L-1} is still staged from the forward pass)
             __syncthreads();
             dq_stage_w(a, a.online, l, Ws);  // (this step's weights: the update kernel writes them next)
             __syncthreads();
         }
-        for (int o = tid; o < B * li; o += nt) {
-            const int b = o / li, i = o - b * li;
-            float s4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            for (int j = 0; j < lo; ++j) s4[j & 3] = s4[j & 3] + D[b * mw + j] * Ws[j * ls + i];
-            const float dz = M[((l - 1) * B + b) * mw + i] ? (s4[0] + s4[1]) + (s4[2] + s4[3]) : 0.0f;
+        // delta_{l-1}[b][i] = relu'(z) * sum_j D[b][j] W[j][i]: the same micro-tiles over the out index j
+        dq_mm(D, mw, 1, W, 1, ls, lo, B, li, [&](int b, int i, float s) {
+            const float dz = M[((l - 1) * B + b) * mw + i] ? s : 0.0f;
             D2[b * mw + i] = dz;
-            a.sd[l - 1][o] = dz;
-        }
+            a.sd[l - 1][b * li + i] = dz;
+        });
         __syncthreads();
         float* t = D;
         D = D2;
         D2 = t;
     }
-    __syncthreads();  // (the bias updates are read by the target blend)
-    dq_finish(a, step, 1, loss, bc1, bc2);
+    DQ_STAMP(512 + 4);
+    dq_finish(a, ctr, 1, loss, bc1, bc2);
+    DQ_STAMP(512 + 5);
 }
 
-// One thread per element of the packed net (hi fragments, then biases).
+// One thread per parameter in the set's order (each layer's W row-major, then
+// the biases): the weight's gradient (the batch sum of delta x input, in row
+// order), Adam, the target blend, and its element of the act kernels' packed
+// image (qnet_pack_elem); the bias threads write the packed biases (the
+// gradient kernel updated them).  Coalesced loads and stores of the sets.
 __global__ void __launch_bounds__(256) drl_dqn_update_kernel(LearnArgs a) {
     const int trained = a.ctr->trained, due = a.ctr->target_due;
     if (!trained && !due) return;
     const QnetPack& p = a.pack;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < p.n_wfrag_elems) {
+    const int L = a.n_layers;
+    if (i < a.wstart[L]) {
         int l = 0;
-        while (l + 1 < p.n_layers && i >= (int64_t)p.frag_src[l + 1] * 8) ++l;
-        const int64_t e = i - (int64_t)p.frag_src[l] * 8;
-        const PackSlot s = qnet_pack_slot(l, e, p.kt[l], p.code_w, p.in[l]);
-        if (s.row >= p.out[l]) return;
-        if (s.k < 0) {  // a code net's layer-0 bias slot: the bias the gradient kernel updated
-            if (trained) qnet_pack_write(p, l, e, -1, a.online[a.boff[0] + s.row]);
-            return;
-        }
-        if (s.k >= p.in[l]) return;
-        const int64_t wi = a.woff[l] + (int64_t)s.row * p.in[l] + s.k;
+        while (l + 1 < L && i >= a.wstart[l + 1]) ++l;
+        const int li = a.in[l], lo = a.out[l];
+        const int64_t r = i - a.wstart[l];
+        const int row = (int)(r / li), k = (int)(r - (int64_t)row * li);
+        const int64_t wi = a.woff[l] + r;
         float w = a.online[wi];
         if (trained) {
-            const float* D = a.sd[l] + s.row;
-            const float* X = (l ? a.sh[l - 1] : a.sx) + s.k;
-            const int xs = l ? p.in[l] : a.in4, ds = p.out[l];
+            const float* D = a.sd[l] + row;
+            const float* X = (l ? a.sh[l - 1] : a.sx) + k;
+            const int xs = l ? li : a.in4;
             const float m0 = a.adam_m[wi], v0 = a.adam_v[wi];
             // the batch sum in row order, DQN_STAGE rows' operands loaded ahead
             float g = 0.0f;
@@ -393,7 +595,7 @@ __global__ void __launch_bounds__(256) drl_dqn_update_kernel(LearnArgs a) {
 #pragma unroll
                 for (int q = 0; q < DQN_STAGE; ++q) {
                     const int b = b0 + q < a.batch ? b0 + q : a.batch - 1;
-                    dv[q] = D[b * ds];
+                    dv[q] = D[b * lo];
                     xv[q] = X[b * xs];
                 }
 #pragma unroll
@@ -405,16 +607,19 @@ __global__ void __launch_bounds__(256) drl_dqn_update_kernel(LearnArgs a) {
             a.adam_m[wi] = m;
             a.adam_v[wi] = v;
             a.online[wi] = w;
-            qnet_pack_write(p, l, e, s.k, w);
+            qnet_pack_write(p, l, qnet_pack_elem(l, row, k, p.kt[l], p.code_w), k, w);
         }
         if (due) a.target[wi] = dq_blend(a, w, a.target[wi]);
-    } else if (i < p.n_wfrag_elems + p.n_bias) {
+    } else if (i < a.wstart[L] + p.n_bias) {  // the packed biases (padded to 16 per unit tile)
         if (!trained) return;
-        const int64_t bi = i - p.n_wfrag_elems;
+        const int64_t bi = i - a.wstart[L];
         int l = 0;
-        while (l + 1 < p.n_layers && bi >= p.bias_off[l + 1]) ++l;
+        while (l + 1 < L && bi >= p.bias_off[l + 1]) ++l;
         const int u = (int)(bi - p.bias_off[l]);
-        if (u < p.out[l]) p.packed_b[bi] = a.online[a.boff[l] + u];
+        if (u >= p.out[l]) return;
+        const float b = a.online[a.boff[l] + u];
+        p.packed_b[bi] = b;
+        if (l == 0 && p.code_w > 0) qnet_pack_write(p, 0, qnet_pack_elem(0, u, -1, p.kt[0], p.code_w), -1, b);
     }
 }
 
@@ -437,10 +642,10 @@ __global__ void drl_dqn_init_kernel(DqnCounters* c, float epsilon) {
 
 hipError_t launch_dqn_train(const LearnArgs& a, size_t lds_grad, hipStream_t s) {
     if (a.trained)
-        hipLaunchKernelGGL(drl_dqn_grad_kernel, dim3((unsigned)a.nblk0), dim3(DQN_THREADS), lds_grad, s, a);
+        hipLaunchKernelGGL(drl_dqn_grad_kernel, dim3((unsigned)a.nblk0 + 2), dim3(DQN_THREADS), lds_grad, s, a);
     else
         hipLaunchKernelGGL(drl_dqn_grad_kernel, dim3(1), dim3(DQN_THREADS), 0, s, a);
-    const int64_t n = a.pack.n_wfrag_elems + a.pack.n_bias;
+    const int64_t n = a.wstart[a.n_layers] + a.pack.n_bias;
     hipLaunchKernelGGL(drl_dqn_update_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
     return hipGetLastError();
 }

@@ -136,12 +136,16 @@ int num_cus() {
 // regions of drl::LearnArgs, and the gradient launch's LDS.
 struct DqnPlan {
     drl_dqn_layout pub;
-    int64_t sx, sz0, sh[drl::QN_MAX_LAYERS], sd[drl::QN_MAX_LAYERS];  // float offsets within the scratch
-    int in4, maxw, tiles0, ws_floats;
+    int64_t sx, sz0, smx, sh[drl::QN_MAX_LAYERS], sd[drl::QN_MAX_LAYERS];  // float offsets within the scratch
+    int in4, xs0, maxw, tiles0, ws_floats, region_a, prefetch;
+    int tw[2][drl::QN_MAX_LAYERS], tb[2][drl::QN_MAX_LAYERS], tm[drl::QN_MAX_LAYERS], tv[drl::QN_MAX_LAYERS], tr;
     size_t lds;
 };
 
 static int64_t r4(int64_t v) { return (v + 3) / 4 * 4; }
+
+// DqSeg::rm: i / row == umulhi(i, rm) exactly for i * row < 2^32 (drl::FastDiv's multiplier)
+static uint32_t rm_of(int row) { return row > 1 ? drl::make_fastdiv((uint32_t)row).m : 0u; }
 
 static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout& L, DqnPlan* P) {
     if (batch < 1 || batch > drl::DQN_MAX_BATCH) return fail("batch must be in [1, 64]");
@@ -171,6 +175,8 @@ static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout
     sc += r4((int64_t)batch * P->in4);
     P->sz0 = sc;
     sc += r4(2ll * batch * L.out[0]);
+    P->smx = sc;
+    sc += r4(batch);
     for (int l = 0; l + 1 < L.n_layers; ++l) {
         P->sh[l] = sc;
         sc += r4((int64_t)batch * L.out[l]);
@@ -179,20 +185,55 @@ static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout
         P->sd[l] = sc;
         sc += r4((int64_t)batch * L.out[l]);
     }
+#ifdef DRL_DQN_STAMPS
+    sc += 2048;  // 8 KB of stamps (tools/learn_stamps.py)
+#endif
     o.bytes = o.scratch_off + sc * 4;
     P->tiles0 = (L.out[0] + drl::DQN_TILE - 1) / drl::DQN_TILE;
-    o.grad_workgroups = 2 * P->tiles0;
-    // layer 0 (X, the weight tile, a code net's sampled rows) and the last workgroup (two activation buffers
-    // of one net, one layer's weights with rows of in + 4 floats, the online net's ReLU masks)
+    o.grad_workgroups = 2 * P->tiles0 + 2;
+    // region A: layer 0 (X, the weight tile and its biases, a code net's sampled rows), then the last
+    // workgroup's two activation buffers of one net and the online net's ReLU masks (+ one layer's weights
+    // with rows of in + 4 floats when the tail is not prefetched)
     int ws = 0;
     for (int l = 1; l < L.n_layers; ++l) ws = std::max(ws, L.out[l] * (L.in[l] + 4));
     P->ws_floats = ws;
+    P->xs0 = L.in[0] + ((2 - L.in[0]) % 32 + 32) % 32;
     const int rw = L.code_w ? drl::lay::code_bytes(L.code_w) / 4 : 0;
-    const size_t a0 = ((size_t)(batch + drl::DQN_TILE) * P->in4 + (size_t)batch * rw) * 4;
-    const size_t a1 = ((size_t)2 * batch * P->maxw + ws) * 4 + (size_t)r4((int64_t)(L.n_layers - 1) * batch * P->maxw);
-    P->lds = a0 > a1 ? a0 : a1;
+    // the layer-0 workgroups: X, the weight tile and its biases, a code net's sampled rows
+    const int64_t a0 = (int64_t)batch * P->in4 + (int64_t)drl::DQN_TILE * P->xs0 + drl::DQN_TILE + (int64_t)batch * rw;
+    // the tail workgroup: two activation buffers of one net, the online net's ReLU masks (+ one layer's weights
+    // with rows of in + 4 floats when the tail does not hold them), then the tail
+    const int64_t masks = r4((int64_t)(L.n_layers - 1) * batch * P->maxw) / 4;
+    const int64_t a1p = 2ll * batch * P->maxw + masks, a1s = a1p + ws;
+    // the prefetched tail: every bias of both nets, the online biases' moments, the sampled rows' action /
+    // reward / done, then (when they fit) the later layers' weights of both nets
+    int64_t t = 0;
+    for (int n = 0; n < 2; ++n)
+        for (int l = 0; l < L.n_layers; ++l) {
+            P->tb[n][l] = (int)t;
+            t += r4(L.out[l]);
+        }
+    for (int l = 0; l < L.n_layers; ++l) {
+        P->tm[l] = (int)t;
+        t += r4(L.out[l]);
+        P->tv[l] = (int)t;
+        t += r4(L.out[l]);
+    }
+    P->tr = (int)t;
+    t += r4(3ll * batch);
+    const int64_t t_small = t;
+    for (int l = 1; l < L.n_layers; ++l) {  // (each tail holds its own net's weights: the same offsets)
+        P->tw[0][l] = P->tw[1][l] = (int)t;
+        t += (int64_t)L.out[l] * (L.in[l] + 4);
+    }
+    constexpr int64_t kMaxFloats = 156 * 1024 / 4;
+    P->prefetch = std::max(a0, a1p + t) <= kMaxFloats;
+    if (!P->prefetch) t = t_small;
+    P->region_a = (int)(P->prefetch ? a1p : a1s);
+    P->lds = (size_t)std::max(a0, P->region_a + t) * 4;
     o.grad_lds_bytes = (int32_t)P->lds;
     if (P->lds > 156 * 1024) return fail("the learner's batch and widths do not fit the LDS of a CU");
+    (void)d;
     return 0;
 }
 
@@ -502,7 +543,21 @@ int drl_dqn_train(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agen
     a.nblk0 = 2 * P.tiles0;
     a.maxw = P.maxw;
     a.in4 = P.in4;
+    a.xs0 = P.xs0;
+    a.rm_in = rm_of(L.in[0]);
+    a.rm_rw = rm_of((int)r->obs_floats);
     a.ws_floats = P.ws_floats;
+    a.region_a = P.region_a;
+    a.prefetch = P.prefetch;
+    a.tr = P.tr;
+    for (int l = 0; l < L.n_layers; ++l) {
+        a.tw[0][l] = P.tw[0][l];
+        a.tw[1][l] = P.tw[1][l];
+        a.tb[0][l] = P.tb[0][l];
+        a.tb[1][l] = P.tb[1][l];
+        a.tm[l] = P.tm[l];
+        a.tv[l] = P.tv[l];
+    }
     for (int l = 0; l < L.n_layers; ++l) {
         a.in[l] = L.in[l];
         a.out[l] = L.out[l];
@@ -517,6 +572,7 @@ int drl_dqn_train(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agen
     float* sc = reinterpret_cast<float*>(base + P.pub.scratch_off);
     a.sx = sc + P.sx;
     a.sz0 = sc + P.sz0;
+    a.smx = sc + P.smx;
     for (int l = 0; l < L.n_layers; ++l) {
         a.sh[l] = l + 1 < L.n_layers ? sc + P.sh[l] : nullptr;
         a.sd[l] = sc + P.sd[l];
@@ -546,7 +602,43 @@ int drl_dqn_train(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agen
     a.b2d = h->beta2;
     a.target_every = h->target_update_interval;
     a.eps_every = h->epsilon_decay_every;
+    {  // the tails' segments (drl::DqSeg): the online tail's, then the target tail's; the later layers'
+       // weights only when they fit (a.prefetch)
+        int ns = 0;
+        const float* sets[2] = {a.online, a.target};
+        auto seg = [&](const void* src, int n, int dst, int row, int pad, int kind) {
+            a.tail[ns++] = drl::DqSeg{src, n, P.region_a + dst, row, pad, kind, rm_of(row)};
+        };
+        for (int n = 0; n < 2; ++n) {
+            const int first = ns;
+            if (a.prefetch)
+                for (int l = 1; l < L.n_layers; ++l)
+                    seg(sets[n] + P.pub.weight_off[l], L.in[l] * L.out[l] / 4, P.tw[n][l], L.in[l] / 4, 1, 4);
+            if (n == 0) {
+                for (int m = 0; m < 2; ++m)
+                    for (int l = 0; l < L.n_layers; ++l) seg(sets[m] + P.pub.bias_off[l], L.out[l], P.tb[m][l], 1, 0, 0);
+                for (int l = 0; l < L.n_layers; ++l) {
+                    seg(a.adam_m + P.pub.bias_off[l], L.out[l], P.tm[l], 1, 0, 0);
+                    seg(a.adam_v + P.pub.bias_off[l], L.out[l], P.tv[l], 1, 0, 0);
+                }
+                seg(r->actions, h->batch, P.tr, 1, 0, 1);
+                seg(r->rewards, h->batch, P.tr + h->batch, 1, 0, 1);
+                seg(r->dones, h->batch, P.tr + 2 * h->batch, 1, 0, 2);
+            } else {
+                for (int l = 1; l < L.n_layers; ++l) seg(sets[1] + P.pub.bias_off[l], L.out[l], P.tb[1][l], 1, 0, 0);
+            }
+            a.ntail_of[n] = ns - first;
+        }
+        a.ntail = ns;
+        a.tail_start[0] = 0;
+        for (int g = 0; g < ns; ++g) a.tail_start[g + 1] = a.tail_start[g] + a.tail[g].n;
+    }
     fill_pack(L, d_packed, nullptr, nullptr, &a.pack);
+#ifdef DRL_DQN_STAMPS
+    a.stamps = reinterpret_cast<uint64_t*>(base + P.pub.bytes - 8192);
+#endif
+    a.wstart[0] = 0;
+    for (int l = 0; l < L.n_layers; ++l) a.wstart[l + 1] = a.wstart[l] + (int64_t)L.in[l] * L.out[l];
     hipError_t e = drl::launch_dqn_train(a, P.lds, stream);
     return e == hipSuccess ? 0 : hip_fail(e, "drl_dqn_train launch");
 }

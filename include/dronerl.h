@@ -79,8 +79,9 @@ typedef struct ihipStream_t* hipStream_t;
 /* error bits written to drl_step's optional err word */
 #define DRL_ERR_BAD_ACTION 1   /* action outside [-5, 4] (IndexError in the reference) */
 #define DRL_ERR_NO_FREE_CELL 2 /* respawn found no free cell (the reference loops forever) */
-#define DRL_ERR_BAD_STATE 4    /* drl_env_set_state: MT index outside [0, 624] (CPython setstate's ValueError);
-                                  clamped to 624 */
+#define DRL_ERR_BAD_STATE 4    /* drl_env_set_state: MT index outside [0, 624] (CPython setstate's ValueError;
+                                  clamped to 624), or a ground code outside {0, 2, 3, 4, 5} (stored as
+                                  its low 4 bits) */
 #define DRL_ERR_QNET_RANGE 8   /* drl_qnet_act (DRL_QNET_F32): an input or hidden activation at or beyond fp16's
                                   range (|v| >= 65520) or NaN; that env's Q values are not valid */
 
@@ -326,9 +327,12 @@ int drl_env_obs(drl_env* env, int32_t k, float* d_obs, hipStream_t stream);
 int drl_env_grid_obs(drl_env* env, float* d_grid, hipStream_t stream);
 /* Copy the state out to / in from a caller-owned SoA view (NULL fields are
  * skipped by get_state; set_state needs all of them and trusts their
- * validity: positions on the grid, distinct cells, charge in [0, 100]; an MT
- * index outside [0, 624] is clamped to 624 and raises DRL_ERR_BAD_STATE in
- * the handle's error word). */
+ * validity: positions on the grid, distinct cells, charge in [0, 100]; ground
+ * codes are common/constants.py Object values {0, 2, 3, 4, 5} (< 8: the
+ * packed ground holds a nibble per cell, the policy code 3 bits); an MT index
+ * outside [0, 624] is clamped to 624, and a ground code outside that set is
+ * stored as its low 4 bits; both raise DRL_ERR_BAD_STATE in the handle's
+ * error word). */
 int drl_env_get_state(drl_env* env, const drl_state_view* v, hipStream_t stream);
 int drl_env_set_state(drl_env* env, const drl_state_view* v, hipStream_t stream);
 /* The handle's raw buffers, params and layout (any output may be NULL). */
