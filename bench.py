@@ -606,8 +606,9 @@ class TrainSegment:
     respawn-candidate refill (env.step()'s cadence, launched on its own branch
     after the step it follows: it overlaps the next act, and the next step
     waits for it).  The learner follows the add of its step on the main
-    stream (it samples the ring the add fills), and the next act follows the
-    learner (it acts with the updated net).  Observations, actions,
+    stream without waiting for the add of its step (it reads that step's
+    transitions from the step's buffers: drl_dqn_train_fresh), and the next
+    act follows the learner (it acts with the updated net).  Observations, actions,
     rewards and dones rotate through 3 buffers, so step t only waits for the
     replay add of step t-2 and the actions of step t are drawn while step t-1
     runs.  parallel=False issues the same calls in the same order on one
@@ -672,11 +673,11 @@ class TrainSegment:
 
     def _replay(self, t):
         b, nb = t % self.NB, (t + 1) % self.NB
-        self.rb.add_many(self.obs[b], self.acts[b], self.rewards[b], self.obs[nb], self.dones[b])
+        return self.rb.add_many(self.obs[b], self.acts[b], self.rewards[b], self.obs[nb], self.dones[b])
 
-    def _learn(self):
+    def _learn(self, fresh=None):
         if self.learner is not None:
-            self.learner.train(self.rb)
+            self.learner.train(self.rb, fresh=fresh)
 
     def run(self):
         main = torch.cuda.current_stream(self.env.device)
@@ -724,11 +725,14 @@ class TrainSegment:
                             ev_ref.record(self.s_ref)
                     with torch.cuda.stream(self.s_rep):
                         self.s_rep.wait_event(ev_step[t])
-                        self._replay(t)
+                        batch = self._replay(t)
                         ev_rep[t].record(self.s_rep)
-                    if self.learner is not None:  # samples the ring the add fills; the next act reads its net
-                        main.wait_event(ev_rep[t])
-                        self._learn()
+                    if self.learner is not None:
+                        # the learner reads step t's transitions from the step's own buffers (fresh), so it
+                        # overlaps the add of step t; the ring rows of step t - 1 must have landed
+                        if t >= 1:
+                            main.wait_event(ev_rep[t - 1])
+                        self._learn(fresh=batch)
                 main.wait_stream(self.s_syn)
                 main.wait_stream(self.s_rep)
                 main.wait_stream(self.s_ref)

@@ -393,16 +393,18 @@ constexpr int DQN_STAGE = 8;      // loads each thread keeps in flight when the 
 constexpr int DQN_MAX_SEGS = 28;  // copy segments of the gradient kernel's prefetch
 
 // One segment of the gradient kernel's one-round staging into LDS: element
-// i < n of `src` lands at LDS float dst + (pad ? (i / row) * (row + pad) +
-// i % row : i) (kind 4: in float4 units, dst still in floats).  kind 0: f32
-// (or raw 32-bit) at src[i]; 1: 32-bit at src[sample[i]]; 2: u8 at
-// src[sample[i]], as 0.0f / 1.0f; 3: replay rows, element (b, k) =
-// src[sample[b] * row_words + k], k < row; 4: float4 at src[i].  rm: the
+// i < n lands at LDS float dst + (pad ? (i / row) * (row + pad) + i % row :
+// i) (kind 4: in float4 units, dst still in floats).  kind 0: f32 (or raw
+// 32-bit) at src[i]; 4: float4 at src[i]; the sampled rows' data through the
+// per-row pointer table tbl (0 obs row, 1 next_obs row, 2 action, 3 reward,
+// 4 done): kind 1: the 32-bit word at table[i]; 2: the u8 at table[i], as
+// 0.0f / 1.0f; 3: element (b, k) = table[b][k], k < row.  rm: the
 // multiply-shift reciprocal of row (i / row == umulhi(i, rm); 0 when row == 1).
 struct DqSeg {
     const void* src;
     int n, dst, row, pad, kind;
     uint32_t rm;
+    int tbl;
 };
 
 struct LearnArgs {
@@ -439,7 +441,17 @@ struct LearnArgs {
     const int32_t* r_act;
     const float* r_rew;
     const uint8_t* r_done;
-    int64_t size;
+    int64_t size, capacity;
+    // fresh != 0: an add_many landing this step (rows f_first + off at slots f_base + off, off < f_rows) may
+    // still be running: its rows are read from its own buffers (drl_replay_batch; strides in elements)
+    int fresh;
+    int64_t f_base, f_rows, f_first;
+    const uint32_t* f_obs;
+    const uint32_t* f_next;
+    const int32_t* f_act;
+    const float* f_rew;
+    const uint8_t* f_done;
+    int64_t f_obs_stride, f_next_stride, f_act_stride, f_rew_stride, f_done_stride;
     uint64_t seed;
     // hyperparameters, as the f32 constants jax's weak typing makes of the python floats
     float gamma, b1, b2, c1, c2, adam_eps, neg_lr, tau, one_minus_tau, eps_decay, eps_end, inv_batch;

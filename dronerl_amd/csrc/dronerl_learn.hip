@@ -171,14 +171,15 @@ typedef const __attribute__((address_space(1))) uint8_t gcu8;
 __device__ __forceinline__ uint32_t dq_div(uint32_t i, const DqSeg& g) { return g.rm ? __umulhi(i, g.rm) : i; }
 
 // (global-address-space loads: a flat load would also count against the LDS counter)
-__device__ __forceinline__ dq_f4 dq_seg_load(const DqSeg& g, int i, const int64_t* sidx, int64_t row_words) {
+typedef const void* dq_tab[5][DQN_MAX_BATCH];  // the sampled rows' obs, next_obs, action, reward, done pointers
+__device__ __forceinline__ dq_f4 dq_seg_load(const DqSeg& g, int i, const dq_tab& tab) {
     switch (g.kind) {
         case 0: return dq_f4{((gcf32*)g.src)[i], 0.0f, 0.0f, 0.0f};
-        case 1: return dq_f4{((gcf32*)g.src)[sidx[i]], 0.0f, 0.0f, 0.0f};
-        case 2: return dq_f4{((gcu8*)g.src)[sidx[i]] ? 1.0f : 0.0f, 0.0f, 0.0f, 0.0f};
+        case 1: return dq_f4{*(gcf32*)tab[g.tbl][i], 0.0f, 0.0f, 0.0f};
+        case 2: return dq_f4{*(gcu8*)tab[4][i] ? 1.0f : 0.0f, 0.0f, 0.0f, 0.0f};
         case 3: {
             const int b = (int)dq_div((uint32_t)i, g);
-            return dq_f4{((gcf32*)g.src)[sidx[b] * row_words + (i - b * g.row)], 0.0f, 0.0f, 0.0f};
+            return dq_f4{((gcf32*)tab[g.tbl][b])[i - b * g.row], 0.0f, 0.0f, 0.0f};
         }
         default: return ((gcf4*)g.src)[i];
     }
@@ -194,7 +195,7 @@ __device__ __forceinline__ int dq_seg_dst(const DqSeg& g, int i) {
 // thread's elements only move forward, so its segment is carried in
 // registers and re-read from LDS only when it crosses into the next one.
 __device__ __forceinline__ void dq_stage_segs(float* lds, const DqSeg* seg, const int* start, int ns,
-                                              const int64_t* sidx, int64_t row_words) {
+                                              const dq_tab& tab) {
     const int n = start[ns], nt = blockDim.x;
     int g = 0, ge = start[1], gs = 0;
     DqSeg cur = seg[0];
@@ -214,7 +215,7 @@ __device__ __forceinline__ void dq_stage_segs(float* lds, const DqSeg* seg, cons
                     gs = ge;
                     ge = start[g + 1];
                 }
-                v[q] = dq_seg_load(cur, i - gs, sidx, row_words);
+                v[q] = dq_seg_load(cur, i - gs, tab);
                 d[q] = dq_seg_dst(cur, i - gs);
                 w4[q] = cur.kind == 4;
             }
@@ -360,7 +361,7 @@ __device__ __forceinline__ bool dq_wait(const LearnArgs& a, int32_t* word, uint3
 __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) {
     extern __shared__ float4 dq_lds4[];
     float* lds = reinterpret_cast<float*>(dq_lds4);
-    __shared__ int64_t s_idx[DQN_MAX_BATCH];
+    __shared__ dq_tab s_tab;
     __shared__ float s_d[DQN_MAX_BATCH], s_mx[DQN_MAX_BATCH], s_q[DQN_MAX_BATCH * 8];
     __shared__ int s_act[DQN_MAX_BATCH];
     __shared__ DqSeg s_seg[DQN_MAX_SEGS];
@@ -387,7 +388,24 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) 
         dq_finish(a, ctr, 0, 0.0f, 0.0f, 0.0f);
         return;
     }
-    if (tid < B) s_idx[tid] = dq_sample(a.seed, ctr.step, tid, a.size);
+    if (tid < B) {  // buffers.py:79-90 sample: the rows' pointers (a pending add's rows from its own buffers)
+        const int64_t s = dq_sample(a.seed, ctr.step, tid, a.size);
+        const void* p[5] = {a.r_obs + s * a.row_words, a.r_next + s * a.row_words, a.r_act + s, a.r_rew + s,
+                            a.r_done + s};
+        if (a.fresh) {
+            int64_t off = s - a.f_base;
+            if (off < 0) off += a.capacity;
+            if (off < a.f_rows) {
+                const int64_t i = a.f_first + off;
+                p[0] = a.f_obs + i * a.f_obs_stride;
+                p[1] = a.f_next + i * a.f_next_stride;
+                p[2] = a.f_act + i * a.f_act_stride;
+                p[3] = a.f_rew + i * a.f_rew_stride;
+                p[4] = a.f_done + i * a.f_done_stride;
+            }
+        }
+        for (int t = 0; t < 5; ++t) s_tab[t][tid] = p[t];
+    }
     const int in = a.in[0], in4 = a.in4, xs0 = a.xs0, out0 = a.out[0];
     if (blockIdx.x < (unsigned)a.nblk0) {
         // ---- layer 0 of one net for DQN_TILE units
@@ -399,14 +417,13 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) 
         const int rw = (int)a.row_words;
         const float* P = net ? a.target : a.online;
         if (tid == 0) {
-            const uint32_t* rows = net ? a.r_next : a.r_obs;
             // the tile's weight rows are contiguous in the set: one flat copy into rows of xs0
-            s_seg[0] = DqSeg{P + a.woff[0] + (int64_t)u0 * in, nu * in, B * in4, in, xs0 - in, 0, a.rm_in};
-            s_seg[1] = DqSeg{P + a.boff[0] + u0, nu, B * in4 + DQN_TILE * xs0, 1, 0, 0, 0u};
+            s_seg[0] = DqSeg{P + a.woff[0] + (int64_t)u0 * in, nu * in, B * in4, in, xs0 - in, 0, a.rm_in, 0};
+            s_seg[1] = DqSeg{P + a.boff[0] + u0, nu, B * in4 + DQN_TILE * xs0, 1, 0, 0, 0u, 0};
             if (a.code_w)  // the code rows, decoded from LDS below
-                s_seg[2] = DqSeg{rows, B * rw, B * in4 + DQN_TILE * xs0 + DQN_TILE, rw, 0, 3, a.rm_rw};
+                s_seg[2] = DqSeg{nullptr, B * rw, B * in4 + DQN_TILE * xs0 + DQN_TILE, rw, 0, 3, a.rm_rw, net};
             else
-                s_seg[2] = DqSeg{rows, B * in, 0, in, in4 - in, 3, a.rm_in};
+                s_seg[2] = DqSeg{nullptr, B * in, 0, in, in4 - in, 3, a.rm_in, net};
             s_start[0] = 0;
             s_start[1] = nu * in;
             s_start[2] = nu * in + nu;
@@ -416,7 +433,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) 
             for (int e = tid; e < B * (in4 - in); e += nt) X[(e / (in4 - in)) * in4 + in + e % (in4 - in)] = 0.0f;
         __syncthreads();
         DQ_STAMP(8 * blockIdx.x + 1);
-        dq_stage_segs(lds, s_seg, s_start, 3, s_idx, a.row_words);
+        dq_stage_segs(lds, s_seg, s_start, 3, s_tab);
         __syncthreads();
         DQ_STAMP(8 * blockIdx.x + 2);
         if (a.code_w) {  // one thread per (row, cell): its six channels
@@ -465,7 +482,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) 
     if (tid <= ns) s_start[tid] = a.tail_start[g0 + tid] - a.tail_start[g0];
     __syncthreads();
     DQ_STAMP(8 * blockIdx.x + 1);
-    dq_stage_segs(lds, s_seg, s_start, ns, s_idx, a.row_words);
+    dq_stage_segs(lds, s_seg, s_start, ns, s_tab);
     DQ_STAMP(8 * blockIdx.x + 2);
     if (tid == 0) s_flag = dq_wait(a, &a.ctr->arrive, (uint32_t)a.nblk0);  // every layer-0 workgroup's ticket
     __syncthreads();

@@ -226,13 +226,13 @@ static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout
         P->tw[0][l] = P->tw[1][l] = (int)t;
         t += (int64_t)L.out[l] * (L.in[l] + 4);
     }
-    constexpr int64_t kMaxFloats = 156 * 1024 / 4;
+    constexpr int64_t kMaxFloats = 150 * 1024 / 4;  // (+ ~7 KB of the kernel's own LDS arrays)
     P->prefetch = std::max(a0, a1p + t) <= kMaxFloats;
     if (!P->prefetch) t = t_small;
     P->region_a = (int)(P->prefetch ? a1p : a1s);
     P->lds = (size_t)std::max(a0, P->region_a + t) * 4;
     o.grad_lds_bytes = (int32_t)P->lds;
-    if (P->lds > 156 * 1024) return fail("the learner's batch and widths do not fit the LDS of a CU");
+    if (P->lds > 150 * 1024) return fail("the learner's batch and widths do not fit the LDS of a CU");
     (void)d;
     return 0;
 }
@@ -509,8 +509,8 @@ int drl_dqn_init(const drl_qnet_desc* d, int32_t batch, void* d_agent, float eps
     return e == hipSuccess ? 0 : hip_fail(e, "drl_dqn_init launch");
 }
 
-int drl_dqn_train(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agent, void* d_packed, const drl_replay* r,
-                  int64_t size, hipStream_t stream) {
+static int dqn_train_impl(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agent, void* d_packed,
+                          const drl_replay* r, int64_t size, const drl_replay_batch* fresh, hipStream_t stream) {
     drl::QnetLayout L;
     if (qnet_layout(d, &L)) return -1;
     if (!h) return fail("hparams is NULL");
@@ -584,7 +584,31 @@ int drl_dqn_train(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agen
     a.r_rew = r->rewards;
     a.r_done = r->dones;
     a.size = size;
+    a.capacity = r->capacity;
     a.seed = h->sample_seed;
+    if (fresh && fresh->n > 0) {
+        if (!fresh->obs || !fresh->next_obs || !fresh->actions || !fresh->rewards || !fresh->dones)
+            return fail("fresh batch pointers are NULL");
+        if (fresh->cursor < 0 || fresh->obs_stride < r->obs_floats || fresh->next_obs_stride < r->obs_floats ||
+            fresh->action_stride < 1 || fresh->reward_stride < 1 || fresh->done_stride < 1)
+            return fail("fresh batch: bad cursor or strides");
+        if ((uintptr_t)fresh->obs % 4 || (uintptr_t)fresh->next_obs % 4) return fail("fresh rows must be 4-byte aligned");
+        const int64_t first = fresh->n > r->capacity ? fresh->n - r->capacity : 0;
+        a.fresh = 1;
+        a.f_first = first;
+        a.f_rows = fresh->n - first;
+        a.f_base = (fresh->cursor % r->capacity + first % r->capacity) % r->capacity;
+        a.f_obs = static_cast<const uint32_t*>(fresh->obs);
+        a.f_next = static_cast<const uint32_t*>(fresh->next_obs);
+        a.f_act = fresh->actions;
+        a.f_rew = fresh->rewards;
+        a.f_done = fresh->dones;
+        a.f_obs_stride = fresh->obs_stride;
+        a.f_next_stride = fresh->next_obs_stride;
+        a.f_act_stride = fresh->action_stride;
+        a.f_rew_stride = fresh->reward_stride;
+        a.f_done_stride = fresh->done_stride;
+    }
     // the python floats as jax's weak typing rounds them into f32 arithmetic
     a.gamma = (float)h->gamma;
     a.b1 = (float)h->beta1;
@@ -607,7 +631,7 @@ int drl_dqn_train(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agen
         int ns = 0;
         const float* sets[2] = {a.online, a.target};
         auto seg = [&](const void* src, int n, int dst, int row, int pad, int kind) {
-            a.tail[ns++] = drl::DqSeg{src, n, P.region_a + dst, row, pad, kind, rm_of(row)};
+            a.tail[ns++] = drl::DqSeg{src, n, P.region_a + dst, row, pad, kind, rm_of(row), 0};
         };
         for (int n = 0; n < 2; ++n) {
             const int first = ns;
@@ -621,9 +645,12 @@ int drl_dqn_train(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agen
                     seg(a.adam_m + P.pub.bias_off[l], L.out[l], P.tm[l], 1, 0, 0);
                     seg(a.adam_v + P.pub.bias_off[l], L.out[l], P.tv[l], 1, 0, 0);
                 }
-                seg(r->actions, h->batch, P.tr, 1, 0, 1);
-                seg(r->rewards, h->batch, P.tr + h->batch, 1, 0, 1);
-                seg(r->dones, h->batch, P.tr + 2 * h->batch, 1, 0, 2);
+                seg(nullptr, h->batch, P.tr, 1, 0, 1);  // (the sampled rows' action, reward, done: tables 2-4)
+                a.tail[ns - 1].tbl = 2;
+                seg(nullptr, h->batch, P.tr + h->batch, 1, 0, 1);
+                a.tail[ns - 1].tbl = 3;
+                seg(nullptr, h->batch, P.tr + 2 * h->batch, 1, 0, 2);
+                a.tail[ns - 1].tbl = 4;
             } else {
                 for (int l = 1; l < L.n_layers; ++l) seg(sets[1] + P.pub.bias_off[l], L.out[l], P.tb[1][l], 1, 0, 0);
             }
@@ -641,6 +668,17 @@ int drl_dqn_train(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agen
     for (int l = 0; l < L.n_layers; ++l) a.wstart[l + 1] = a.wstart[l] + (int64_t)L.in[l] * L.out[l];
     hipError_t e = drl::launch_dqn_train(a, P.lds, stream);
     return e == hipSuccess ? 0 : hip_fail(e, "drl_dqn_train launch");
+}
+
+int drl_dqn_train(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agent, void* d_packed, const drl_replay* r,
+                  int64_t size, hipStream_t stream) {
+    return dqn_train_impl(d, h, d_agent, d_packed, r, size, nullptr, stream);
+}
+
+int drl_dqn_train_fresh(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agent, void* d_packed,
+                        const drl_replay* r, int64_t size, const drl_replay_batch* fresh, hipStream_t stream) {
+    if (!fresh) return fail("fresh batch is NULL");
+    return dqn_train_impl(d, h, d_agent, d_packed, r, size, fresh, stream);
 }
 
 }  // extern "C"

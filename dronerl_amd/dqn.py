@@ -42,6 +42,13 @@ class DrlReplay(ctypes.Structure):
                 ("dones", ctypes.c_void_p)]
 
 
+class DrlReplayBatch(ctypes.Structure):
+    _fields_ = [("cursor", ctypes.c_int64), ("n", ctypes.c_int64), ("obs", ctypes.c_void_p),
+                ("obs_stride", ctypes.c_int64), ("next_obs", ctypes.c_void_p), ("next_obs_stride", ctypes.c_int64),
+                ("actions", ctypes.c_void_p), ("action_stride", ctypes.c_int64), ("rewards", ctypes.c_void_p),
+                ("reward_stride", ctypes.c_int64), ("dones", ctypes.c_void_p), ("done_stride", ctypes.c_int64)]
+
+
 class DrlDqnHParams(ctypes.Structure):
     _fields_ = [("batch", ctypes.c_int32), ("target_update_interval", ctypes.c_int32),
                 ("epsilon_decay_every", ctypes.c_int32), ("reserved", ctypes.c_int32),
@@ -76,6 +83,8 @@ def _bind(L):
         "drl_dqn_layout_query": [D, i32, ctypes.POINTER(DrlDqnLayout)],
         "drl_dqn_init": [D, i32, _vp, f32, _vp],
         "drl_dqn_train": [D, ctypes.POINTER(DrlDqnHParams), _vp, _vp, ctypes.POINTER(DrlReplay), i64, _vp],
+        "drl_dqn_train_fresh": [D, ctypes.POINTER(DrlDqnHParams), _vp, _vp, ctypes.POINTER(DrlReplay), i64,
+                                ctypes.POINTER(DrlReplayBatch), _vp],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -338,7 +347,9 @@ class ReplayBuffer:
                  dones: torch.Tensor):
         """buffers.py:57-80.  obs/next_obs [E, >= obs_floats] f32 rows (a code
         buffer: uint8 [E, code_bytes] policy-code rows); actions i32, rewards
-        f32, dones u8 as [E] or [E, n_drones] (column 0 taken)."""
+        f32, dones u8 as [E] or [E, n_drones] (column 0 taken).  Returns the
+        batch's description (DQNLearner.train(fresh=...): a learner step that
+        may run while this add is still in flight)."""
         E = obs.shape[0]
         dev = self.obs.device
         odt = torch.uint8 if self.code_radius else torch.float32
@@ -362,8 +373,12 @@ class ReplayBuffer:
                                              _vp(no.data_ptr()), no.stride(0), _vp(actions.data_ptr()), col(actions),
                                              _vp(rewards.data_ptr()), col(rewards), _vp(dones.data_ptr()), col(dones),
                                              _stream(self.obs.device)))
+        batch = DrlReplayBatch(self.cursor, E, o.data_ptr(), o.stride(0), no.data_ptr(), no.stride(0),
+                               actions.data_ptr(), col(actions), rewards.data_ptr(), col(rewards), dones.data_ptr(),
+                               col(dones))
         self.cursor = (self.cursor + E) % self.capacity
         self.size = min(self.size + E, self.capacity)
+        return batch
 
     def can_sample(self, batch: int = 64) -> bool:
         return self.size >= batch
@@ -477,14 +492,29 @@ class DQNLearner:
             out.append((s[wo:wo + w.numel()].view(w.shape), s[bo:bo + b.numel()]))
         return out
 
-    def train(self, rb: "ReplayBuffer"):
+    def train(self, rb: "ReplayBuffer", fresh: Optional[DrlReplayBatch] = None):
         """One learner block (train_jax.py:68-98) on the replay's current
-        contents (rb.size transitions)."""
+        contents (rb.size transitions).  fresh: the value of the
+        rb.add_many call that filled the latest rows; their transitions are
+        then read from that call's buffers, so the add may still be running
+        on another stream (drl_dqn_train_fresh)."""
         if rb.obs.device != self.block.device:
             raise ValueError("the replay buffer must be on the learner's device")
+        if fresh is not None:
+            _check(self.L, self.L.drl_dqn_train_fresh(ctypes.byref(self.net.desc), ctypes.byref(self._hp),
+                                                      _vp(self.block.data_ptr()), _vp(self.net.packed.data_ptr()),
+                                                      ctypes.byref(rb._c), rb.size, ctypes.byref(fresh),
+                                                      _stream(self.block.device)))
+            return
         _check(self.L, self.L.drl_dqn_train(ctypes.byref(self.net.desc), ctypes.byref(self._hp),
                                             _vp(self.block.data_ptr()), _vp(self.net.packed.data_ptr()),
                                             ctypes.byref(rb._c), rb.size, _stream(self.block.device)))
+
+    def check_errors(self):
+        """Synchronise; raise if a gradient launch gave up waiting for its
+        workgroups (a hardware-scheduling fault, never expected)."""
+        if int(self._ctr_i[13].item()):
+            raise DroneRLError("drl_dqn_train: a tail workgroup timed out waiting for the layer-0 workgroups")
 
     def counters(self) -> dict:
         """Host copy of the device counters (synchronises)."""

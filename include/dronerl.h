@@ -523,6 +523,27 @@ int drl_dqn_init(const drl_qnet_desc* d, int32_t batch, void* d_agent, float eps
  * the online net's packed image (drl_qnet_pack of the online set). */
 int drl_dqn_train(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agent, void* d_packed,
                   const struct drl_replay* r, int64_t size, hipStream_t stream);
+/* A drl_replay_add batch (its arguments; strides in elements, obs strides in
+ * 32-bit words). */
+typedef struct drl_replay_batch {
+    int64_t cursor, n;
+    const void* obs;
+    int64_t obs_stride;
+    const void* next_obs;
+    int64_t next_obs_stride;
+    const int32_t* actions;
+    int64_t action_stride;
+    const float* rewards;
+    int64_t reward_stride;
+    const uint8_t* dones;
+    int64_t done_stride;
+} drl_replay_batch;
+/* drl_dqn_train as if drl_replay_add(r, fresh->cursor, fresh->n, ...) had
+ * already run (`size` counts its rows): the rows that add writes are read
+ * from its own buffers, so the add may run concurrently on another stream
+ * (the learner reads no slot it writes). */
+int drl_dqn_train_fresh(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agent, void* d_packed,
+                        const struct drl_replay* r, int64_t size, const drl_replay_batch* fresh, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -379,3 +379,38 @@ def test_learner_act_reads_device_epsilon():
     onet.act(x, learner.epsilon, seed=5, step=2, actions=b1)
     onet.act(x, 0.37, seed=5, step=2, actions=b2)
     assert torch.equal(b1, b2)
+
+
+@gpu
+@pytest.mark.parametrize("cap,E", [(300, 64), (100, 160)])
+def test_learner_fresh_batch_equals_serial(cap, E):
+    """drl_dqn_train_fresh (the learner reads the latest add's rows from that
+    add's own buffers, so the add may overlap it) leaves the same state, bit
+    for bit, as drl_dqn_train after the add; also when the add overwrites the
+    whole ring (E > capacity)."""
+    from dronerl_amd.dqn import DQNHParams, DQNLearner, QNetwork, ReplayBuffer
+    from dronerl_amd import BatchedDeliveryDrones, EnvParams
+    env = BatchedDeliveryDrones(EnvParams(n_drones=8, grid_size=16), E)
+    env.reset(seed=4)
+    nets = [QNetwork(294, (128, 64), generator=torch.Generator().manual_seed(8), input="code") for _ in range(2)]
+    hp = DQNHParams(batch=16, target_update_interval=3)
+    lrs = [DQNLearner(n, hp, generator=torch.Generator().manual_seed(9)) for n in nets]
+    rb = ReplayBuffer(cap, 294, torch.device("cuda"), code_radius=3)
+    cur, nxt = env.new_code(), env.new_code()
+    env.get_code(out=cur)
+    acts = torch.empty((E, 8), dtype=torch.int32, device="cuda")
+    for t in range(12):
+        nets[0].act(cur, lrs[0].epsilon, seed=1, step=t, actions=acts, synth=(2, t))
+        r, d = env.step(acts, code=nxt)
+        batch = rb.add_many(cur, acts, r, nxt, d)
+        lrs[0].train(rb)
+        lrs[1].train(rb, fresh=batch)
+        cur, nxt = nxt, cur
+    torch.cuda.synchronize()
+    for k in ("online", "target", "m", "v"):
+        for (w0, b0), (w1, b1) in zip(lrs[0].params(k), lrs[1].params(k)):
+            assert torch.equal(w0, w1) and torch.equal(b0, b1), k
+    assert lrs[0].counters() == lrs[1].counters()
+    assert torch.equal(nets[0].packed, nets[1].packed)
+    for lr in lrs:
+        lr.check_errors()
