@@ -301,6 +301,9 @@ int drl_reset(const drl_params* p, const drl_state* s, int32_t reseed, uint64_t 
         a.fy_serial = c ? atoi(c) : kFySerial;
         a.fy_bwords = drl::lay::fy_bitmap_words(GG);
         a.wave_lds += (a.fy_bwords + 64) * 4;
+        const char* wp = getenv("DRL_RESET_WPB");  // A/B knob: envs per workgroup of the wave kernel
+        const int wv = wp ? atoi(wp) : 0;
+        a.wpb = (wv == 1 || wv == 2 || wv == 4 || wv == 8) ? wv : 0;
         const char* pad = getenv("DRL_RESET_LDS_PAD");  // diagnostic: fewer waves per CU
         if (pad) a.wave_lds += atoi(pad) / 16 * 16;
     }

@@ -211,6 +211,7 @@ struct ResetArgs {
     const uint8_t* mask;
     int lanes, lane_lds, list_cap, block_lds, pool_branch;
     int wave_per_env, wave_lds;  // drl_reset_wave_kernel (large grids) and its LDS bytes
+    int wpb;                     // ... envs (waves) per workgroup: 0 = the default, or 1, 2, 4, 8 (DRL_RESET_WPB)
     int fy_batch_min;            // wave kernel: shuffle 64 draws at a time while si >= this
     int fy_serial;               // ... i-range writers per chunk resolved by readlanes (more: table + jumps)
     int fy_bwords;               // ... words of its j bitmap (lay::fy_bitmap_words)

@@ -2376,12 +2376,7 @@ hipError_t launch_reset(const ResetArgs& a, hipStream_t s) {
     if (a.wave_per_env) {
         // waves (envs) per workgroup: 4 on large grids (C5 2.00e7 vs 1.91e7 resets/s), 1 below (C3 / C4 alike
         // within noise at 1, 2, 4; profiles/r04_reset/); DRL_RESET_WPB = 1, 2, 4 or 8 overrides (A/B knob)
-        static const int wpb_env = [] {
-            const char* e = getenv("DRL_RESET_WPB");
-            const int v = e ? atoi(e) : 0;
-            return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
-        }();
-        const int wpb = wpb_env ? wpb_env : (a.cells >= 4096 ? 4 : 1);
+        const int wpb = a.wpb ? a.wpb : (a.cells >= 4096 ? 4 : 1);
         const unsigned nb = (unsigned)((a.E + wpb - 1) / wpb);
         if (wpb == 8 && 8 * (size_t)a.wave_lds <= 160 * 1024)
             hipLaunchKernelGGL(drl_reset_wave_kernel<8>, dim3((unsigned)((a.E + 7) / 8)), dim3(512), 8 * (size_t)a.wave_lds, s, a);

@@ -155,3 +155,58 @@ def test_ground_pack_roundtrip():
         assert not packed[:, (side * side + 1) // 2:].any()  # zero padding
     with pytest.raises(ValueError):
         pack_ground(torch.full((1, 4), 16, dtype=torch.uint8), 16)
+
+
+# Every __global__ kernel of the product library and the -m gpu test that
+# launches it (no shipped kernel without a GPU test).  A new
+# kernel must be listed here with its test; a listed test must exist.
+KERNEL_TESTS = {
+    "drl_step_kernel": "test_gpu_parity.py::test_rollout_matches_oracle",
+    "drl_rollout_kernel": "test_gpu_parity.py::test_rollout_equals_steps",
+    "drl_obs_kernel": "test_gpu_parity.py::test_obs_variants",
+    "drl_grid_obs_kernel": "test_gpu_parity.py::test_grid_obs_vs_oracle_state_and_compat_gridview",
+    "drl_reset_wave_kernel": "test_gpu_parity.py::test_reset_matches_oracle",  # every WPB instance: RESET_KERNELS
+    "drl_reset_kernel": "test_gpu_parity.py::test_reset_matches_oracle",       # the "lane" variant
+    "drl_refill_list_kernel": "test_gpu_parity.py::test_candidate_ring_cadence_matches_oracle",
+    "drl_refill_kernel": "test_gpu_parity.py::test_candidate_ring_cadence_matches_oracle",  # refill_kernel "wave"
+    "drl_mt_get_kernel": "test_gpu_parity.py::test_candidate_ring_holds_the_streams_randint_pairs",
+    "drl_mt_set_kernel": "test_gpu_parity.py::test_reference_trajectory_on_gpu",
+    "drl_decode_kernel": "test_gpu_parity.py::test_reset_matches_oracle",
+    "drl_encode_kernel": "test_gpu_validation.py::test_full_grid_respawn_raises_no_free_cell",
+    "drl_ground_pack_kernel": "test_gpu_validation.py::test_handle_set_state_flags_bad_ground_code",
+    "drl_ground_unpack_kernel": "test_gpu_validation.py::test_handle_set_state_clamps_and_flags_bad_mt_index",
+    "drl_synth_actions_kernel": "test_dqn.py::test_qnet_act_synth_equals_synth_then_act",
+    "drl_code_decode_kernel": "test_policy_code.py::test_code_decode_and_get_code",
+    "drl_hbm_probe_kernel": "test_gpu_validation.py::test_hbm_probe_copies_and_reads",
+    "drl_qnet_pack_kernel": "test_dqn.py::test_qnet_load_repacks",
+    "drl_qnet_act_kernel": "test_dqn.py::test_qnet_greedy_matches_torch_reference",   # bf16
+    "drl_qnet_act_f32_kernel": "test_dqn.py::test_qnet_f32_matches_fp32_forward",
+    "drl_qnet_act_code_kernel": "test_policy_code.py::test_qnet_act_code_matches_f32_forward",   # other nets
+    "drl_qnet_act_code2_kernel": "test_policy_code.py::test_qnet_act_code_matches_f32_forward",  # radius 4
+    "drl_qnet_act_code4_kernel": "test_policy_code.py::test_qnet_act_code_matches_f32_forward",  # benchmark net
+    "drl_replay_add16_kernel": "test_policy_code.py::test_code_replay_buffer_samples_decode_to_obs_buffer",
+    "drl_replay_add_kernel": "test_dqn.py::test_replay_add_many_matches_sequential_add",
+    "drl_replay_add_rows_kernel": "test_dqn.py::test_replay_add_two_float_rows",
+    "drl_dqn_grad_kernel": "test_dqn_learner.py::test_learner_matches_oracle_bit_exact",
+    "drl_dqn_update_kernel": "test_dqn_learner.py::test_learner_matches_oracle_bit_exact",
+    "drl_dqn_init_kernel": "test_dqn_learner.py::test_learner_matches_oracle_bit_exact",
+}
+
+
+def test_every_kernel_has_a_gpu_test():
+    import glob
+    import re
+    csrc = os.path.join(REPO, "dronerl_amd", "csrc")
+    found = set()
+    for f in glob.glob(os.path.join(csrc, "*.hip")):
+        src = open(f).read()
+        for m in re.finditer(r"__global__", src):
+            k = re.search(r"\b(drl_[a-z0-9_]+_kernel)\s*\(", src[m.end():m.end() + 300])
+            if k:
+                found.add(k.group(1))
+    assert found == set(KERNEL_TESTS), (sorted(found - set(KERNEL_TESTS)), sorted(set(KERNEL_TESTS) - found))
+    for kern, ref in KERNEL_TESTS.items():
+        fname, test = ref.split("::")
+        text = open(os.path.join(REPO, "tests", fname)).read()
+        assert re.search(rf"^def {test}\(", text, re.M), (kern, ref)
+        assert "gpu" in text, ref

@@ -328,6 +328,30 @@ def test_replay_add_many_matches_sequential_add(cap, batches):
 
 
 @gpu
+def test_replay_add_two_float_rows():
+    """Rows of one float2 (obs_floats 2): drl_replay_add_rows_kernel, the
+    block-per-row form, against a sequential add() loop."""
+    from dronerl_amd.dqn import ReplayBuffer
+    cap, D = 50, 2
+    rb = ReplayBuffer(cap, D, torch.device("cuda"))
+    ref = dict(obs=np.zeros((cap, D), np.float32), next_obs=np.zeros((cap, D), np.float32),
+               actions=np.zeros(cap, np.int32), rewards=np.zeros(cap, np.float32), dones=np.zeros(cap, np.uint8))
+    g = torch.Generator(device="cuda").manual_seed(1)
+    cursor = 0
+    for n in (30, 40, 77):
+        obs, nobs = torch.rand((n, D), device="cuda", generator=g), torch.rand((n, D), device="cuda", generator=g)
+        acts = torch.randint(0, 5, (n,), dtype=torch.int32, device="cuda", generator=g)
+        rews = torch.rand((n,), device="cuda", generator=g)
+        dones = (torch.rand((n,), device="cuda", generator=g) < 0.3).to(torch.uint8)
+        rb.add_many(obs, acts, rews, nobs, dones)
+        _seq_add(ref, obs.cpu().numpy(), acts.cpu().numpy(), rews.cpu().numpy(), nobs.cpu().numpy(),
+                 dones.cpu().numpy(), cursor, cap)
+        cursor = (cursor + n) % cap
+    for k in ref:
+        np.testing.assert_array_equal(getattr(rb, k).cpu().numpy(), ref[k], err_msg=k)
+
+
+@gpu
 def test_train_loop_shape_step_act_add():
     """train_jax.py:42-64 loop shape: act on obs -> step(+obs) -> add_many."""
     from dronerl_amd.dqn import QNetwork, ReplayBuffer

@@ -155,6 +155,10 @@ RESET_KERNELS = {
     "wave_ser0": {"DRL_FY_SERIAL": "0"},                         # i-range writers: slot table + pointer jumps
     "wave_ser64": {"DRL_FY_SERIAL": "64"},                       # i-range writers: readlane pass only
     "lane": {"DRL_RESET_WAVE": "0"},                             # lane per env
+    "wave_wpb1": {"DRL_RESET_WPB": "1"},                         # 1, 2, 4, 8 envs (waves) per workgroup:
+    "wave_wpb2": {"DRL_RESET_WPB": "2"},                         # every drl_reset_wave_kernel instance
+    "wave_wpb4": {"DRL_RESET_WPB": "4"},
+    "wave_wpb8": {"DRL_RESET_WPB": "8"},
 }
 
 
@@ -696,7 +700,8 @@ def test_train_segment_parallel_matches_serial():
     """bench.TrainSegment: synthetic actions and replay add_many on parallel
     stream branches (3 rotating buffers), and the one-stream loop with the
     synthetic actions fused into the act launch, leave the same env state,
-    replay buffer and next observation as the plain calls on one stream."""
+    replay buffer, next observation and learner state as the plain calls on
+    one stream."""
     from bench import TrainSegment
     p = EnvParams(n_drones=8, grid_size=16)
     E, seg = 3000, 13
@@ -717,6 +722,13 @@ def test_train_segment_parallel_matches_serial():
             assert torch.equal(getattr(l0.rb, k), getattr(l1.rb, k)), (name, k)
         assert l0.rb.cursor == l1.rb.cursor
         assert torch.equal(l0.obs[0], l1.obs[0]), name
+        # the learner: the parallel loop trains from the step's own buffers (drl_dqn_train_fresh) while the
+        # add runs beside it; the serial loop after the add -- the same learned state, bit for bit
+        for k in ("online", "target", "m", "v"):
+            for (w0, b0), (w1, b1) in zip(l0.learner.params(k), l1.learner.params(k)):
+                assert torch.equal(w0, w1) and torch.equal(b0, b1), (name, k)
+        assert l0.learner.counters() == l1.learner.counters(), name
+        assert torch.equal(l0.net.packed, l1.net.packed), name
 
 
 @pytest.mark.parametrize("kernel", list(RESET_KERNELS))

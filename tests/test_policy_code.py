@@ -168,7 +168,9 @@ def _f32_forward(net, x):
                                                     (8, 3, 2, 777, (96, 32)), (16, 8, 4, 2048, (64, 32)),
                                                     (16, 8, 4, 500, (96, 32)), (16, 8, 2, 31, (64, 64, 32)),
                                                     (8, 3, 2, 777, (128, 64)), (16, 8, 3, 100, (128, 64)),
-                                                    (32, 16, 3, 131072, (128, 64))])
+                                                    (32, 16, 3, 131072, (128, 64)),
+                                                    # radius 4 with the benchmark net: drl_qnet_act_code2_kernel
+                                                    (16, 8, 4, 2048, (128, 64))])
 def test_qnet_act_code_matches_f32_forward(side, n, radius, E, hidden):
     """Q from the code == an f32 forward of drone 0's observation (and the
     obs-input f32 kernel's Q) within Q_TOL; greedy = the f32 argmax wherever
