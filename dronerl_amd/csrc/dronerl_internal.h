@@ -392,6 +392,7 @@ constexpr int DQN_TILE = 16;      // layer-0 units per workgroup of the gradient
 constexpr int DQN_THREADS = 512;  // the gradient kernel's workgroup
 constexpr int DQN_STAGE = 8;      // loads each thread keeps in flight when the learner stages data
 constexpr int DQN_MAX_SEGS = 28;  // copy segments of the gradient kernel's prefetch
+constexpr int DQN_UB = 4;         // weights whose loads a thread issues together in the update phase
 
 // One segment of the gradient kernel's one-round staging into LDS: element
 // i < n lands at LDS float dst + (pad ? (i / row) * (row + pad) + i % row :
@@ -426,12 +427,12 @@ struct LearnArgs {
     float* smx;                       // scratch: max_a Q_target [batch] (the target tail's hand-off)
     int tw[2][QN_MAX_LAYERS], tb[2][QN_MAX_LAYERS], tm[QN_MAX_LAYERS], tv[QN_MAX_LAYERS], tr;  // LDS float offsets
     int64_t woff[QN_MAX_LAYERS], boff[QN_MAX_LAYERS];  // float offsets of W_l / b_l in a parameter set
+    int64_t n_params;                 // floats of a parameter set
     float* online;
     float* target;
     float* adam_m;
     float* adam_v;
     DqnCounters* ctr;
-    float* sx;                        // scratch: the online net's inputs X [batch][in4]
     float* sz0;                       // scratch: layer-0 pre-activations [2 nets][batch][out0]
     float* sh[QN_MAX_LAYERS];         // scratch: online hidden activations h_l [batch][out_l]
     float* sd[QN_MAX_LAYERS];         // scratch: deltas dL/dz_l [batch][out_l]
@@ -460,7 +461,7 @@ struct LearnArgs {
     int target_every, eps_every;
     // the act kernels' packed image of the online net (drl_dqn_update_kernel refreshes it)
     QnetPack pack;
-    int64_t wstart[QN_MAX_LAYERS + 1];  // update kernel: thread index of layer l's first weight; [L] = weights total
+    int64_t wstart[QN_MAX_LAYERS + 1];  // the weights in set order: index of layer l's first; [L] = their total
     uint64_t* stamps;                   // DRL_DQN_STAMPS builds: [8 per workgroup (<= 64)][512 + last workgroup's]
 };
 

@@ -13,18 +13,15 @@
 // device memory (DqnCounters), so a captured HIP graph of the loop replays a
 // continuing schedule.
 //
-// Two launches:
-//   drl_dqn_grad_kernel: workgroups split layer 0 of both nets (online on
-//     the sampled obs, target on next_obs) in 16-unit tiles and hand their
-//     pre-activations over with write-through stores and a ticket counter;
-//     one more workgroup prefetches everything else into LDS meanwhile, waits
-//     for the tickets, and runs the later layers of both nets, the TD error,
-//     the loss, the backward pass to layer 0's deltas and the bias updates;
-//     it writes the step's plan.
-//   drl_dqn_update_kernel: one thread per element of the act kernels' packed
-//     net (qnet_pack_slot: each weight has exactly one): the weight's gradient
-//     (sum over the batch of delta x input), the Adam update, the packed
-//     fp16 hi/lo (or bf16) image the next act reads, and the target blend.
+// One launch (drl_dqn_train_kernel) per learner step: workgroups split
+// layer 0 of both nets (online on the sampled obs, target on next_obs) in
+// 16-unit tiles and hand their pre-activations over with write-through
+// stores and a ticket counter; two more workgroups (the tails, one per net)
+// prefetch everything else into LDS meanwhile, wait for the tickets, and run
+// their net's later layers; the online tail then runs the TD error, the loss,
+// the backward pass and the bias updates, and hands the deltas over behind an
+// epoch word, on which the layer-0 workgroups update the weights (gradient,
+// Adam, the act kernels' packed fp16 hi/lo or bf16 image, the target blend).
 //
 // Arithmetic order is fixed and contraction-free (each product rounded, then
 // each sum), so oracle/dqn_learner.py reproduces the result bit for bit:
@@ -107,9 +104,9 @@ __device__ __forceinline__ float dq_blend(const LearnArgs& a, float nw, float ol
     return a.tau * nw + a.one_minus_tau * old;
 }
 
-// The counters at the end of a learner step (thread 0 of the last workgroup,
+// The counters at the end of a learner step (thread 0 of the online tail,
 // or of the one workgroup of a step without a sample): Adam's count and
-// powers, the loss, the epsilon decay, the plan drl_dqn_update_kernel reads,
+// powers, the loss, the epsilon decay, the step's plan (informative),
 // step + 1.  ctr: the values the kernel read at its start.
 __device__ void dq_finish(const LearnArgs& a, const DqnCounters& ctr, int trained, float loss, float bc1, float bc2) {
     if (threadIdx.x != 0) return;
@@ -291,9 +288,9 @@ __device__ __forceinline__ void dq_mm(const float* X, int xs, int xk, const floa
 
 // The later layers of net n (1 = target, 0 = online) for the B sampled rows,
 // from its layer-0 pre-activations (handed over write-through) and its
-// prefetched (or staged) weights; Pa ends holding Q [B][A].  The online net
-// also stores its hidden activations (the update kernel's inputs) and ReLU
-// masks.  Returns the buffer holding Q.
+// prefetched (or staged) weights; returns the buffer holding Q [B][A].  The
+// online net also hands its hidden activations over (write-through: the
+// update phase reads them) and keeps its ReLU masks in LDS.
 __device__ float* dq_forward(const LearnArgs& a, int n, float* Pa, float* Qa, float* Ws, uint8_t* M, const float* T) {
     const int B = a.batch, L = a.n_layers, mw = a.maxw, out0 = a.out[0];
     const float* Pn = n ? a.target : a.online;
@@ -302,7 +299,7 @@ __device__ float* dq_forward(const LearnArgs& a, int n, float* Pa, float* Qa, fl
         const float h = z > 0.0f ? z : 0.0f;
         Pa[b * mw + j] = h;
         if (n == 0) {
-            a.sh[0][i] = h;
+            dq_store_sc1(a.sh[0] + i, h);
             M[b * mw + j] = z > 0.0f;
         }
     });
@@ -319,7 +316,7 @@ __device__ float* dq_forward(const LearnArgs& a, int n, float* Pa, float* Qa, fl
                 const float h = z > 0.0f ? z : 0.0f;
                 Qa[b * mw + j] = h;
                 if (n == 0) {
-                    a.sh[l][b * lo + j] = h;
+                    dq_store_sc1(a.sh[l] + b * lo + j, h);
                     M[(l * B + b) * mw + j] = z > 0.0f;
                 }
             } else {
@@ -334,7 +331,7 @@ __device__ float* dq_forward(const LearnArgs& a, int n, float* Pa, float* Qa, fl
     return Pa;
 }
 
-// Poll an agent-scope counter (sc1 loads, one lane) until it reaches `want`;
+// Poll an agent-scope word (sc1 loads, one lane) until it reaches `want`;
 // false after a bounded wait (DqnCounters::pad[0] = 1).
 __device__ __forceinline__ bool dq_wait(const LearnArgs& a, int32_t* word, uint32_t want) {
     uint32_t spins = 0;
@@ -348,17 +345,56 @@ __device__ __forceinline__ bool dq_wait(const LearnArgs& a, int32_t* word, uint3
     return true;
 }
 
+// The weight step of DQN_UB weights at a time (their loads issued together):
+// gradient g[q] (the caller's batch sum), Adam, the act kernels' packed
+// image (qnet_pack_elem), the target blend when due.
+struct DqW {
+    int l, row, k;
+    int64_t wi;
+    float g;
+};
+__device__ __forceinline__ void dq_update_weights(const LearnArgs& a, const DqW (&w)[DQN_UB], int cnt, float bc1,
+                                                  float bc2, bool due) {
+    float p[DQN_UB], m[DQN_UB], v[DQN_UB], t[DQN_UB];
+#pragma unroll
+    for (int q = 0; q < DQN_UB; ++q) {
+        const int64_t wi = q < cnt ? w[q].wi : w[0].wi;
+        p[q] = a.online[wi];
+        m[q] = a.adam_m[wi];
+        v[q] = a.adam_v[wi];
+        t[q] = due ? a.target[wi] : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < DQN_UB; ++q) {
+        if (q >= cnt) break;
+        const float nw = dq_adam(a, p[q], w[q].g, &m[q], &v[q], bc1, bc2);
+        a.online[w[q].wi] = nw;
+        a.adam_m[w[q].wi] = m[q];
+        a.adam_v[w[q].wi] = v[q];
+        qnet_pack_write(a.pack, w[q].l, qnet_pack_elem(w[q].l, w[q].row, w[q].k, a.pack.kt[w[q].l], a.pack.code_w),
+                        w[q].k, nw);
+        if (due) a.target[w[q].wi] = dq_blend(a, nw, t[q]);
+    }
+}
+
 }  // namespace
 
-// Workgroups 0 .. nblk0-1: layer 0 of one net for DQN_TILE units each;
-// workgroup nblk0 (target tail) and nblk0 + 1 (online tail): each prefetches
-// its net's later layers (the online tail also the biases, their moments and
-// the sampled rows' action / reward / done) while the layer-0 workgroups
-// compute, waits for their tickets, and runs its net's later layers; the
-// target tail hands max_a Q_target over (write-through, a second counter), the
-// online tail then runs the TD error, the loss, the backward pass and the bias
-// updates.
-__global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) {
+// One launch per learner step.  Workgroup 0 is the online tail, 1 the target
+// tail, 2 .. 2 + nblk0 - 1 the layer-0 workgroups (net = (w - 2) / tiles0):
+//  1. layer-0 workgroups: their net's layer 0 for DQN_TILE units on the
+//     sampled rows, handed over write-through behind one ticket each; the
+//     tails prefetch their net's later layers (the online tail also the
+//     biases, their moments and the rows' action / reward / done) meanwhile;
+//  2. the target tail: the target net's later layers, max_a Q_target handed
+//     over; the online tail: the online net's later layers, the TD error, the
+//     loss, the backward pass, the bias updates (Adam, packed image, target
+//     blend), the deltas and activations handed over behind an epoch word;
+//  3. the layer-0 workgroups take the weights: the online ones their own
+//     units' layer-0 rows (inputs still in LDS), the target ones a share of
+//     the later layers: gradient, Adam, packed image, target blend.
+// The tails are workgroups 0 and 1 so that they are dispatched first: every
+// wait in the kernel is on work that is already running.
+__global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs a) {
     extern __shared__ float4 dq_lds4[];
     float* lds = reinterpret_cast<float*>(dq_lds4);
     __shared__ dq_tab s_tab;
@@ -369,25 +405,23 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) 
     __shared__ int s_flag;
     const int tid = threadIdx.x, nt = blockDim.x;
     const int B = a.batch, L = a.n_layers;
-    // the counters as this step starts (the online tail writes them after
-    // every other workgroup has arrived)
+    // the counters as this step starts (the online tail writes them at the end)
     DqnCounters ctr;
     ctr.step = a.ctr->step;
     ctr.count = a.ctr->count;
     ctr.epsilon = a.ctr->epsilon;
     ctr.beta1_pow = a.ctr->beta1_pow;
     ctr.beta2_pow = a.ctr->beta2_pow;
+    const bool due = ctr.step % a.target_every == 0;
     DQ_STAMP(8 * blockIdx.x + 0);
-    if (!a.trained) {  // buffer.can_sample is false: no train_step this step (loss 0); the bias half of the target blend
-        if (ctr.step % a.target_every == 0)
-            for (int l = 0; l < L; ++l)
-                for (int j = tid; j < a.out[l]; j += nt) {
-                    const int64_t bi = a.boff[l] + j;
-                    a.target[bi] = dq_blend(a, a.online[bi], a.target[bi]);
-                }
+    if (!a.trained) {  // buffer.can_sample is false: no train_step this step (loss 0); the target blend when due
+        if (due)
+            for (int64_t i = tid; i < a.n_params; i += nt) a.target[i] = dq_blend(a, a.online[i], a.target[i]);
         dq_finish(a, ctr, 0, 0.0f, 0.0f, 0.0f);
         return;
     }
+    // Adam's bias corrections for this step (count + 1): 1 - beta^count in double, rounded once
+    const float bc1 = (float)(1.0 - ctr.beta1_pow * a.b1d), bc2 = (float)(1.0 - ctr.beta2_pow * a.b2d);
     if (tid < B) {  // buffers.py:79-90 sample: the rows' pointers (a pending add's rows from its own buffers)
         const int64_t s = dq_sample(a.seed, ctr.step, tid, a.size);
         const void* p[5] = {a.r_obs + s * a.row_words, a.r_next + s * a.row_words, a.r_act + s, a.r_rew + s,
@@ -407,9 +441,10 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) 
         for (int t = 0; t < 5; ++t) s_tab[t][tid] = p[t];
     }
     const int in = a.in[0], in4 = a.in4, xs0 = a.xs0, out0 = a.out[0];
-    if (blockIdx.x < (unsigned)a.nblk0) {
-        // ---- layer 0 of one net for DQN_TILE units
-        const int net = blockIdx.x / a.tiles0, u0 = (blockIdx.x % a.tiles0) * DQN_TILE;
+    const uint32_t epoch = (uint32_t)ctr.step + 1u;  // the online tail's hand-off word (pad[2]) for this step
+    if (blockIdx.x >= 2) {
+        // ---- 1. layer 0 of one net for DQN_TILE units
+        const int w = blockIdx.x - 2, net = w / a.tiles0, u0 = (w % a.tiles0) * DQN_TILE;
         const int nu = min(DQN_TILE, out0 - u0);
         float* X = lds;                   // [B][in4] the sampled rows (obs: online net, next_obs: target)
         float* Wt = lds + B * in4;        // [DQN_TILE][xs0] this tile's layer-0 weight rows, then its biases
@@ -429,8 +464,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) 
             s_start[2] = nu * in + nu;
             s_start[3] = nu * in + nu + s_seg[2].n;
         }
-        if (!a.code_w)  // the f32 rows' padding columns
-            for (int e = tid; e < B * (in4 - in); e += nt) X[(e / (in4 - in)) * in4 + in + e % (in4 - in)] = 0.0f;
+        for (int e = tid; e < B * (in4 - in); e += nt) X[(e / (in4 - in)) * in4 + in + e % (in4 - in)] = 0.0f;
         __syncthreads();
         DQ_STAMP(8 * blockIdx.x + 1);
         dq_stage_segs(lds, s_seg, s_start, 3, s_tab);
@@ -452,25 +486,97 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) 
                 x[4] = air ? (float)((int)(air & 0x7fu) - 1) / 100.0f : 0.0f;
                 x[5] = obj == OBJ_SKYSCRAPER ? 1.0f : 0.0f;
             }
-            for (int e = tid; e < B * (in4 - in); e += nt) X[(e / (in4 - in)) * in4 + in + e % (in4 - in)] = 0.0f;
             __syncthreads();
         }
-        if (net == 0 && u0 == 0)  // the update kernel's layer-0 inputs
-            for (int e = tid; e < B * in4; e += nt) a.sx[e] = X[e];
         float* z0 = a.sz0 + (int64_t)net * B * out0 + u0;
         dq_mm(X, in4, 1, Wt, xs0, 1, in, B, nu, [&](int b, int u, float z) { dq_store_sc1(z0 + b * out0 + u, z + Bt[u]); });
-        // hand-off: every wave drains its write-through stores, the workgroup
-        // barrier, one agent-scope ticket
+        // hand-off: every wave drains its write-through stores, the workgroup barrier, one agent-scope ticket
         DQ_STAMP(8 * blockIdx.x + 3);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) __hip_atomic_fetch_add(&a.ctr->arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // ---- 3. the weights, once the online tail has handed the deltas over
+        if (tid == 0) s_flag = dq_wait(a, &a.ctr->pad[2], epoch);
+        __syncthreads();
         DQ_STAMP(8 * blockIdx.x + 4);
+        if (!s_flag) return;
+        if (net == 0) {  // this tile's layer-0 rows: dW0[u][k] = sum_b dz0[b][u0 + u] * X[b][k]
+            float* Dz = Wt;  // [B][DQN_TILE] (the weight tile is dead)
+            dq_stage(B * nu, [&](int i) { return dq_load_sc1(a.sd[0] + (i / nu) * out0 + u0 + i % nu); },
+                     [&](int i, float d) { Dz[(i / nu) * DQN_TILE + i % nu] = d; });
+            __syncthreads();
+            const int n = nu * in;
+            for (int base = tid; base < n; base += DQN_UB * nt) {
+                DqW ws[DQN_UB];
+                int cnt = 0;
+#pragma unroll
+                for (int q = 0; q < DQN_UB; ++q) {
+                    const int e = base + q * nt;
+                    if (e >= n) break;
+                    const int u = (int)__umulhi((uint32_t)e, a.rm_in), k = e - u * in;
+                    float g = 0.0f;
+                    for (int b = 0; b < B; ++b) g = g + Dz[b * DQN_TILE + u] * X[b * in4 + k];
+                    ws[q] = DqW{0, u0 + u, k, a.woff[0] + (int64_t)(u0 + u) * in + k, g};
+                    cnt = q + 1;
+                }
+                if (cnt) dq_update_weights(a, ws, cnt, bc1, bc2, due);
+            }
+        } else {  // a share of the later layers' weights: dW_l[r][k] = sum_b D_l[b][r] * H_{l-1}[b][k]
+            // D_l and H_{l-1} of every later layer -> LDS (after X: the region is dead); segment table in LDS
+            int* off = s_start;                                       // [2 (L - 1) + 1] prefix offsets
+            const float** src = reinterpret_cast<const float**>(s_seg);  // [2 (L - 1)] sources
+            __syncthreads();
+            if (tid == 0) {
+                int ns = 0, tot = 0;
+                for (int l = 1; l < L; ++l) {
+                    off[ns] = tot;
+                    src[ns++] = a.sd[l];
+                    tot += B * a.out[l];
+                    off[ns] = tot;
+                    src[ns++] = a.sh[l - 1];
+                    tot += B * a.in[l];
+                }
+                off[ns] = tot;
+            }
+            __syncthreads();
+            float* S = lds;
+            const int tot = off[2 * (L - 1)];
+            dq_stage(tot, [&](int i) {
+                int g = 0;
+                while (i >= off[g + 1]) ++g;
+                return dq_load_sc1(src[g] + (i - off[g]));
+            }, [&](int i, float v) { S[i] = v; });
+            __syncthreads();
+            const int64_t nw = a.wstart[L] - a.wstart[1], share = (nw + a.tiles0 - 1) / a.tiles0;
+            const int64_t lo_i = (int64_t)(w % a.tiles0) * share, hi_i = min(nw, lo_i + share);
+            for (int64_t base = lo_i + tid; base < hi_i; base += (int64_t)DQN_UB * nt) {
+                DqW ws[DQN_UB];
+                int cnt = 0;
+#pragma unroll
+                for (int q = 0; q < DQN_UB; ++q) {
+                    const int64_t f = base + (int64_t)q * nt;
+                    if (f >= hi_i) break;
+                    const int64_t gi = a.wstart[1] + f;
+                    int l = 1;
+                    while (l + 1 < L && gi >= a.wstart[l + 1]) ++l;
+                    const int r0 = (int)(gi - a.wstart[l]), li = a.in[l], lo = a.out[l];
+                    const int row = r0 / li, k = r0 - row * li;
+                    const float* D = S + off[2 * (l - 1)];
+                    const float* H = S + off[2 * (l - 1) + 1];  // (LDS table reads)
+                    float g = 0.0f;
+                    for (int b = 0; b < B; ++b) g = g + D[b * lo + row] * H[b * li + k];
+                    ws[q] = DqW{l, row, k, a.woff[l] + r0, g};
+                    cnt = q + 1;
+                }
+                if (cnt) dq_update_weights(a, ws, cnt, bc1, bc2, due);
+            }
+        }
+        DQ_STAMP(8 * blockIdx.x + 5);
         return;
     }
 
-    // ---- the tails: n = 1 (target, workgroup nblk0), n = 0 (online, nblk0 + 1)
-    const int n = blockIdx.x == (unsigned)a.nblk0 ? 1 : 0;
+    // ---- 2. the tails: workgroup 0 the online net, 1 the target net
+    const int n = blockIdx.x == 0 ? 0 : 1;
     const int mw = a.maxw;
     float* Pa = lds;                   // [B][mw] activations of the current layer
     float* Qa = lds + B * mw;          // [B][mw] the next layer's
@@ -486,11 +592,11 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) 
     DQ_STAMP(8 * blockIdx.x + 2);
     if (tid == 0) s_flag = dq_wait(a, &a.ctr->arrive, (uint32_t)a.nblk0);  // every layer-0 workgroup's ticket
     __syncthreads();
-    DQ_STAMP(512 + 8 * n + 0);
+    DQ_STAMP(8 * blockIdx.x + 3);
     if (!s_flag) return;
     Pa = dq_forward(a, n, Pa, Qa, Ws, M, T);
     Qa = Pa == lds ? lds + B * mw : lds;
-    DQ_STAMP(512 + 8 * n + 1);
+    DQ_STAMP(8 * blockIdx.x + 4);
     const int A = a.out[L - 1];
     if (n == 1) {  // max_a Q_target, handed over write-through behind the second ticket
         for (int b = tid; b < B; b += nt) {
@@ -505,7 +611,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) 
     }
     for (int b = tid; b < B; b += nt)
         for (int j = 0; j < A; ++j) s_q[b * 8 + j] = Pa[b * mw + j];
-    if (tid == 0) {  // the target tail's ticket; then both counters are free for the next step
+    if (tid == 0) {  // the target tail's ticket; then both tickets are free for the next step
         s_flag = dq_wait(a, &a.ctr->pad[1], 1u);
         __hip_atomic_store((gu32*)&a.ctr->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store((gu32*)&a.ctr->pad[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -514,7 +620,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) 
     if (!s_flag) return;
     for (int b = tid; b < B; b += nt) s_mx[b] = dq_load_sc1(a.smx + b);
     __syncthreads();
-    DQ_STAMP(512 + 2);
+    DQ_STAMP(8 * blockIdx.x + 5);
     float loss = 0.0f;
     for (int b = tid; b < B; b += nt) {
         const int act = __float_as_int(T[a.tr + b]);
@@ -528,7 +634,6 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) 
     __syncthreads();
     for (int b = 0; b < B; ++b) loss = loss + s_d[b] * s_d[b];
     loss = loss / (float)B;  // jnp.mean(jnp.square(q - td))
-    DQ_STAMP(512 + 3);
     // d loss / d q[b][a_b] = 2 (q - td) / B: the output layer's deltas
     float* D = Pa;   // [B][mw] deltas of layer l
     float* D2 = Qa;  // [B][mw] deltas of layer l - 1
@@ -536,16 +641,12 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) 
         const int b = o / A, j = o - b * A;
         const float dq = (s_act[b] == j) ? (s_d[b] + s_d[b]) / (float)B : 0.0f;
         D[b * mw + j] = dq;
-        a.sd[L - 1][o] = dq;
+        dq_store_sc1(a.sd[L - 1] + o, dq);
     }
     __syncthreads();
-    // Adam's bias corrections for this step (count + 1): 1 - beta^count in double, rounded once
-    const double p1 = ctr.beta1_pow * a.b1d, p2 = ctr.beta2_pow * a.b2d;
-    const float bc1 = (float)(1.0 - p1), bc2 = (float)(1.0 - p2);
-    const bool due = ctr.step % a.target_every == 0;
     for (int l = L - 1; l >= 0; --l) {
         const int lo = a.out[l];
-        for (int j = tid; j < lo; j += nt) {  // the bias: sum of the deltas over the batch, Adam, target blend
+        for (int j = tid; j < lo; j += nt) {  // the bias: the batch sum of the deltas, Adam, packed, target blend
             float g = 0.0f;
             for (int b = 0; b < B; ++b) g = g + D[b * mw + j];
             const int64_t bi = a.boff[l] + j;
@@ -555,6 +656,9 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) 
             a.online[bi] = nb;
             a.adam_m[bi] = m;
             a.adam_v[bi] = v;
+            a.pack.packed_b[a.pack.bias_off[l] + j] = nb;
+            if (l == 0 && a.pack.code_w > 0)
+                qnet_pack_write(a.pack, 0, qnet_pack_elem(0, j, -1, a.pack.kt[0], a.pack.code_w), -1, nb);
             if (due) a.target[bi] = dq_blend(a, nb, tb);
         }
         if (l == 0) break;
@@ -562,82 +666,26 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_grad_kernel(LearnArgs a) 
         const float* W = a.prefetch ? T + a.tw[0][l] : Ws;
         if (!a.prefetch && l < L - 1) {  // (W_{L-1} is still staged from the forward pass)
             __syncthreads();
-            dq_stage_w(a, a.online, l, Ws);  // (this step's weights: the update kernel writes them next)
+            dq_stage_w(a, a.online, l, Ws);  // (this step's weights: the layer-0 workgroups write them after)
             __syncthreads();
         }
         // delta_{l-1}[b][i] = relu'(z) * sum_j D[b][j] W[j][i]: the same micro-tiles over the out index j
         dq_mm(D, mw, 1, W, 1, ls, lo, B, li, [&](int b, int i, float s) {
             const float dz = M[((l - 1) * B + b) * mw + i] ? s : 0.0f;
             D2[b * mw + i] = dz;
-            a.sd[l - 1][b * li + i] = dz;
+            dq_store_sc1(a.sd[l - 1] + b * li + i, dz);
         });
         __syncthreads();
         float* t = D;
         D = D2;
         D2 = t;
     }
-    DQ_STAMP(512 + 4);
+    // hand the deltas and activations over: every wave drains, the barrier, the epoch word
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store((gu32*)&a.ctr->pad[2], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    DQ_STAMP(8 * blockIdx.x + 6);
     dq_finish(a, ctr, 1, loss, bc1, bc2);
-    DQ_STAMP(512 + 5);
-}
-
-// One thread per parameter in the set's order (each layer's W row-major, then
-// the biases): the weight's gradient (the batch sum of delta x input, in row
-// order), Adam, the target blend, and its element of the act kernels' packed
-// image (qnet_pack_elem); the bias threads write the packed biases (the
-// gradient kernel updated them).  Coalesced loads and stores of the sets.
-__global__ void __launch_bounds__(256) drl_dqn_update_kernel(LearnArgs a) {
-    const int trained = a.ctr->trained, due = a.ctr->target_due;
-    if (!trained && !due) return;
-    const QnetPack& p = a.pack;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int L = a.n_layers;
-    if (i < a.wstart[L]) {
-        int l = 0;
-        while (l + 1 < L && i >= a.wstart[l + 1]) ++l;
-        const int li = a.in[l], lo = a.out[l];
-        const int64_t r = i - a.wstart[l];
-        const int row = (int)(r / li), k = (int)(r - (int64_t)row * li);
-        const int64_t wi = a.woff[l] + r;
-        float w = a.online[wi];
-        if (trained) {
-            const float* D = a.sd[l] + row;
-            const float* X = (l ? a.sh[l - 1] : a.sx) + k;
-            const int xs = l ? li : a.in4;
-            const float m0 = a.adam_m[wi], v0 = a.adam_v[wi];
-            // the batch sum in row order, DQN_STAGE rows' operands loaded ahead
-            float g = 0.0f;
-            for (int b0 = 0; b0 < a.batch; b0 += DQN_STAGE) {
-                float dv[DQN_STAGE], xv[DQN_STAGE];
-#pragma unroll
-                for (int q = 0; q < DQN_STAGE; ++q) {
-                    const int b = b0 + q < a.batch ? b0 + q : a.batch - 1;
-                    dv[q] = D[b * lo];
-                    xv[q] = X[b * xs];
-                }
-#pragma unroll
-                for (int q = 0; q < DQN_STAGE; ++q)
-                    if (b0 + q < a.batch) g = g + dv[q] * xv[q];
-            }
-            float m = m0, v = v0;
-            w = dq_adam(a, w, g, &m, &v, a.ctr->bc1, a.ctr->bc2);
-            a.adam_m[wi] = m;
-            a.adam_v[wi] = v;
-            a.online[wi] = w;
-            qnet_pack_write(p, l, qnet_pack_elem(l, row, k, p.kt[l], p.code_w), k, w);
-        }
-        if (due) a.target[wi] = dq_blend(a, w, a.target[wi]);
-    } else if (i < a.wstart[L] + p.n_bias) {  // the packed biases (padded to 16 per unit tile)
-        if (!trained) return;
-        const int64_t bi = i - a.wstart[L];
-        int l = 0;
-        while (l + 1 < L && bi >= p.bias_off[l + 1]) ++l;
-        const int u = (int)(bi - p.bias_off[l]);
-        if (u >= p.out[l]) return;
-        const float b = a.online[a.boff[l] + u];
-        p.packed_b[bi] = b;
-        if (l == 0 && p.code_w > 0) qnet_pack_write(p, 0, qnet_pack_elem(0, u, -1, p.kt[0], p.code_w), -1, b);
-    }
 }
 
 __global__ void drl_dqn_init_kernel(DqnCounters* c, float epsilon) {
@@ -657,13 +705,11 @@ __global__ void drl_dqn_init_kernel(DqnCounters* c, float epsilon) {
     }
 }
 
-hipError_t launch_dqn_train(const LearnArgs& a, size_t lds_grad, hipStream_t s) {
+hipError_t launch_dqn_train(const LearnArgs& a, size_t lds, hipStream_t s) {
     if (a.trained)
-        hipLaunchKernelGGL(drl_dqn_grad_kernel, dim3((unsigned)a.nblk0 + 2), dim3(DQN_THREADS), lds_grad, s, a);
+        hipLaunchKernelGGL(drl_dqn_train_kernel, dim3((unsigned)a.nblk0 + 2), dim3(DQN_THREADS), lds, s, a);
     else
-        hipLaunchKernelGGL(drl_dqn_grad_kernel, dim3(1), dim3(DQN_THREADS), 0, s, a);
-    const int64_t n = a.wstart[a.n_layers] + a.pack.n_bias;
-    hipLaunchKernelGGL(drl_dqn_update_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(drl_dqn_train_kernel, dim3(1), dim3(DQN_THREADS), 0, s, a);
     return hipGetLastError();
 }
 

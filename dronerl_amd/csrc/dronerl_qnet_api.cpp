@@ -136,7 +136,7 @@ int num_cus() {
 // regions of drl::LearnArgs, and the gradient launch's LDS.
 struct DqnPlan {
     drl_dqn_layout pub;
-    int64_t sx, sz0, smx, sh[drl::QN_MAX_LAYERS], sd[drl::QN_MAX_LAYERS];  // float offsets within the scratch
+    int64_t sz0, smx, sh[drl::QN_MAX_LAYERS], sd[drl::QN_MAX_LAYERS];  // float offsets within the scratch
     int in4, xs0, maxw, tiles0, ws_floats, region_a, prefetch;
     int tw[2][drl::QN_MAX_LAYERS], tb[2][drl::QN_MAX_LAYERS], tm[drl::QN_MAX_LAYERS], tv[drl::QN_MAX_LAYERS], tr;
     size_t lds;
@@ -171,8 +171,6 @@ static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout
     for (int l = 0; l < L.n_layers; ++l) maxw = L.out[l] > maxw ? L.out[l] : maxw;
     P->maxw = (int)r4(maxw);
     int64_t sc = 0;
-    P->sx = sc;
-    sc += r4((int64_t)batch * P->in4);
     P->sz0 = sc;
     sc += r4(2ll * batch * L.out[0]);
     P->smx = sc;
@@ -200,7 +198,10 @@ static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout
     P->xs0 = L.in[0] + ((2 - L.in[0]) % 32 + 32) % 32;
     const int rw = L.code_w ? drl::lay::code_bytes(L.code_w) / 4 : 0;
     // the layer-0 workgroups: X, the weight tile and its biases, a code net's sampled rows
-    const int64_t a0 = (int64_t)batch * P->in4 + (int64_t)drl::DQN_TILE * P->xs0 + drl::DQN_TILE + (int64_t)batch * rw;
+    int64_t a0 = (int64_t)batch * P->in4 + (int64_t)drl::DQN_TILE * P->xs0 + drl::DQN_TILE + (int64_t)batch * rw;
+    int64_t later = 0;  // a target layer-0 workgroup's update phase: D_l and H_{l-1} of the later layers
+    for (int l = 1; l < L.n_layers; ++l) later += (int64_t)batch * (L.out[l] + L.in[l]);
+    a0 = std::max(a0, later);
     // the tail workgroup: two activation buffers of one net, the online net's ReLU masks (+ one layer's weights
     // with rows of in + 4 floats when the tail does not hold them), then the tail
     const int64_t masks = r4((int64_t)(L.n_layers - 1) * batch * P->maxw) / 4;
@@ -563,6 +564,7 @@ static int dqn_train_impl(const drl_qnet_desc* d, const drl_dqn_hparams* h, void
         a.out[l] = L.out[l];
         a.woff[l] = P.pub.weight_off[l];
         a.boff[l] = P.pub.bias_off[l];
+        a.n_params = P.pub.n_params;
     }
     a.online = reinterpret_cast<float*>(base + P.pub.online_off);
     a.target = reinterpret_cast<float*>(base + P.pub.target_off);
@@ -570,7 +572,6 @@ static int dqn_train_impl(const drl_qnet_desc* d, const drl_dqn_hparams* h, void
     a.adam_v = reinterpret_cast<float*>(base + P.pub.v_off);
     a.ctr = reinterpret_cast<drl::DqnCounters*>(base + P.pub.counters_off);
     float* sc = reinterpret_cast<float*>(base + P.pub.scratch_off);
-    a.sx = sc + P.sx;
     a.sz0 = sc + P.sz0;
     a.smx = sc + P.smx;
     for (int l = 0; l < L.n_layers; ++l) {

@@ -187,8 +187,7 @@ KERNEL_TESTS = {
     "drl_replay_add16_kernel": "test_policy_code.py::test_code_replay_buffer_samples_decode_to_obs_buffer",
     "drl_replay_add_kernel": "test_dqn.py::test_replay_add_many_matches_sequential_add",
     "drl_replay_add_rows_kernel": "test_dqn.py::test_replay_add_two_float_rows",
-    "drl_dqn_grad_kernel": "test_dqn_learner.py::test_learner_matches_oracle_bit_exact",
-    "drl_dqn_update_kernel": "test_dqn_learner.py::test_learner_matches_oracle_bit_exact",
+    "drl_dqn_train_kernel": "test_dqn_learner.py::test_learner_matches_oracle_bit_exact",
     "drl_dqn_init_kernel": "test_dqn_learner.py::test_learner_matches_oracle_bit_exact",
 }
 

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-phase timing of drl_dqn_grad_kernel from wall_clock64
+"""Diagnostic: per-phase timing of drl_dqn_train_kernel from wall_clock64
 stamps (100 MHz) of a -DDRL_DQN_STAMPS build (tools/var_dqnstamps.so, never
-the product library).
+the product library).  Every figure is the latest workgroup's, in us from the
+earliest workgroup start (median over steps).
 
 python tools/learn_stamps.py [--config c3] [--steps 20] [--build]
 Per workgroup: setup (segment table + sample), stage (the prefetch round),
@@ -51,7 +52,7 @@ def main():
         loop._replay(t)
         loop._learn()
     torch.cuda.synchronize()
-    nblk = lr.layout.grad_workgroups - 2  # (+ the target and online tail workgroups)
+    nblk = lr.layout.grad_workgroups - 2  # workgroup 0: online tail, 1: target tail, 2..: layer 0
     st = lr.block[lr.layout.bytes - 8192:].view(torch.int64)
     rows = []
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -61,31 +62,24 @@ def main():
         lr.train(loop.rb)
         ev[k][1].record()
         torch.cuda.synchronize()
-        s = st.cpu().numpy().astype(np.int64)
-        blk = s[:8 * nblk].reshape(nblk, 8)[:, :5]
-        tt = s[8 * nblk:8 * nblk + 3]          # target tail: start, setup, prefetch done
-        to = s[8 * nblk + 8:8 * nblk + 11]     # online tail
-        on = s[512:518]                        # online: wait done, fwd, mx, td, backward, end
-        tg = s[520:522]                        # target: wait done, fwd
-        t0 = min(blk[:, 0].min(), tt[0], to[0])
+        s = st.cpu().numpy().astype(np.int64).reshape(-1, 8)
+        on, tg, blk = s[0, :7], s[1, :5], s[2:2 + nblk, :6]
+        t0 = min(blk[:, 0].min(), on[0], tg[0])
         f = lambda x: (x - t0) / 100.0  # noqa: E731
-        rows.append({"blocks": f(blk), "tt": f(tt), "to": f(to), "on": f(on), "tg": f(tg),
-                     "event_us": ev[k][0].elapsed_time(ev[k][1]) * 1e3})
+        rows.append({"blocks": f(blk), "on": f(on), "tg": f(tg), "event_us": ev[k][0].elapsed_time(ev[k][1]) * 1e3})
     med = lambda xs: float(np.median(xs))  # noqa: E731
     bl = np.stack([r["blocks"] for r in rows])
-    R = {k: np.stack([r[k] for r in rows]) for k in ("tt", "to", "on", "tg")}
+    on = np.stack([r["on"] for r in rows])
+    tg = np.stack([r["tg"] for r in rows])
     out = {"config": args.config, "layer0_workgroups": nblk,
-           "grad_plus_update_event_us": med([r["event_us"] for r in rows]),
-           "layer0_phase_us_median": {name: med(bl[:, :, i + 1] - bl[:, :, i])
-                                      for i, name in enumerate(["setup", "stage", "compute", "drain_ticket"])},
-           "layer0_start_spread_us": med(bl[:, :, 0].max(1) - bl[:, :, 0].min(1)),
-           "last_ticket_us": med(bl[:, :, 4].max(1)),
-           "target_tail": {"prefetch_done": med(R["tt"][:, 2]), "wait_done": med(R["tg"][:, 0]),
-                           "forward_done": med(R["tg"][:, 1])},
-           "online_tail": {"prefetch_done": med(R["to"][:, 2]), "wait_done": med(R["on"][:, 0]),
-                           "forward_done": med(R["on"][:, 1]), "target_max_in": med(R["on"][:, 2]),
-                           "td_done": med(R["on"][:, 3]), "backward_done": med(R["on"][:, 4]),
-                           "end": med(R["on"][:, 5])}}
+           "kernel_event_us": med([r["event_us"] for r in rows]),
+           "layer0_us": {name: med(bl[:, :, i].max(1)) for i, name in
+                         enumerate(["start", "setup", "staged", "z0_handed", "deltas_in", "weights_done"])},
+           "target_tail_us": {name: med(tg[:, i]) for i, name in
+                              enumerate(["start", "setup", "prefetched", "tickets_in", "forward_done"])},
+           "online_tail_us": {name: med(on[:, i]) for i, name in
+                              enumerate(["start", "setup", "prefetched", "tickets_in", "forward_done", "target_max_in",
+                                         "deltas_handed"])}}
     print(json.dumps(out, indent=1))
 
 
