@@ -1934,10 +1934,10 @@ hipError_t launch_qnet_act_code(const QnetArgs& a, int window, int num_cus, hipS
 #define QN_CODE_LAUNCH(NT, W)                                                                                   \
     if (a.lo0_lds) hipLaunchKernelGGL((drl_qnet_act_code_kernel<NT, true, W, 0>), grid, block, lds, s, a);     \
     else hipLaunchKernelGGL((drl_qnet_act_code_kernel<NT, false, W, 0>), grid, block, lds, s, a)
-    static const bool v2 = [] {  // DRL_QN_CODE=2: the two-tile kernel for the benchmark nets too (A/B knob)
-        const char* e = getenv("DRL_QN_CODE");
-        return e && e[0] == '2';
-    }();
+    // DRL_QN_CODE=2: the two-tile kernel for the benchmark nets too (A/B knob, read per call so the parity
+    // test can reach drl_qnet_act_code2_kernel: no packable net needs it at 32-bit code offsets)
+    const char* v2e = getenv("DRL_QN_CODE");
+    const bool v2 = v2e && v2e[0] == '2';
     const int64_t ng4 = (nt + 3) / 4;  // drl_qnet_act_code4_kernel: four tiles per wave, four waves per workgroup
     int64_t nb4 = (ng4 + QC4_WAVES - 1) / QC4_WAVES;
     if (nb4 > num_cus) nb4 = num_cus;

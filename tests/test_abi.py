@@ -182,7 +182,7 @@ KERNEL_TESTS = {
     "drl_qnet_act_kernel": "test_dqn.py::test_qnet_greedy_matches_torch_reference",   # bf16
     "drl_qnet_act_f32_kernel": "test_dqn.py::test_qnet_f32_matches_fp32_forward",
     "drl_qnet_act_code_kernel": "test_policy_code.py::test_qnet_act_code_matches_f32_forward",   # other nets
-    "drl_qnet_act_code2_kernel": "test_policy_code.py::test_qnet_act_code_matches_f32_forward",  # radius 4
+    "drl_qnet_act_code2_kernel": "test_policy_code.py::test_qnet_act_code_matches_f32_forward",  # kernel="code2"
     "drl_qnet_act_code4_kernel": "test_policy_code.py::test_qnet_act_code_matches_f32_forward",  # benchmark net
     "drl_replay_add16_kernel": "test_policy_code.py::test_code_replay_buffer_samples_decode_to_obs_buffer",
     "drl_replay_add_kernel": "test_dqn.py::test_replay_add_many_matches_sequential_add",
