@@ -42,11 +42,11 @@
 namespace drl {
 
 // DRL_DQN_STAMPS (diagnostic builds, tools/learn_stamps.py): thread 0 of each
-// workgroup stores wall_clock64() (100 MHz) at phase boundaries into the 8 KB
+// workgroup stores wall_clock64() (100 MHz) at phase boundaries (16 slots each) into the 8 KB
 // the layout appends to the agent block's scratch.
 #ifdef DRL_DQN_STAMPS
 #define DQ_STAMP(i) \
-    do { if (threadIdx.x == 0) a.stamps[(i)] = wall_clock64(); } while (0)
+    do { if (threadIdx.x == 0) a.stamps[16 * blockIdx.x + (i)] = wall_clock64(); } while (0)
 #else
 #define DQ_STAMP(i) do { } while (0)
 #endif
@@ -237,6 +237,33 @@ __device__ __forceinline__ float dq_load_sc1(const float* p) {
     return __uint_as_float(__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
+// 16-B write-through stores and loads (buffer ops, aux 16 = sc1: the same hand-off form as the 4-B ones, at
+// one fabric write per 16 B instead of per 4 B: MI355X_MICROARCH.md § visibility, stores of each flavour).
+typedef unsigned dq_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dq_rsrc(const float* p, int nfloats) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, nfloats * 4, 0x00020000);
+}
+// rows b < B of an LDS buffer (stride ss, the first n floats, n % 4 == 0) -> global rows of stride ds
+__device__ __forceinline__ void dq_publish(const float* src, int ss, float* dst, int ds, int B, int n) {
+    const __amdgpu_buffer_rsrc_t r = dq_rsrc(dst, (B - 1) * ds + n);
+    const int n4 = n >> 2;
+    for (int i = threadIdx.x; i < B * n4; i += blockDim.x) {
+        const int b = i / n4, j = 4 * (i - b * n4);
+        const dq_f4 v = *reinterpret_cast<const dq_f4*>(src + b * ss + j);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dq_u4, v), r, (b * ds + j) * 4, 0, 16);
+    }
+}
+// global rows (stride ds, the first n floats, n % 4 == 0) -> f(b, j, four values), one 16-B load per lane
+template <class F>
+__device__ __forceinline__ void dq_fetch(const float* src, int ds, int B, int n, F f) {
+    const __amdgpu_buffer_rsrc_t r = dq_rsrc(src, (B - 1) * ds + n);
+    const int n4 = n >> 2;
+    for (int i = threadIdx.x; i < B * n4; i += blockDim.x) {
+        const int b = i / n4, j = 4 * (i - b * n4);
+        f(b, j, __builtin_bit_cast(dq_f4, __builtin_amdgcn_raw_buffer_load_b128(r, (b * ds + j) * 4, 0, 16)));
+    }
+}
+
 // The learner's dot products as micro-tiles: z[b][j] = sum over k < n of
 // X[b * xs + k * xk] * W[j * wr + k * wk] for b < B, j < J.  A group of four
 // lanes takes two rows b by two outputs j; lane c of the group accumulates
@@ -291,18 +318,18 @@ __device__ __forceinline__ void dq_mm(const float* X, int xs, int xk, const floa
 // prefetched (or staged) weights; returns the buffer holding Q [B][A].  The
 // online net also hands its hidden activations over (write-through: the
 // update phase reads them) and keeps its ReLU masks in LDS.
-__device__ float* dq_forward(const LearnArgs& a, int n, float* Pa, float* Qa, float* Ws, uint8_t* M, const float* T) {
+__device__ __forceinline__ float* dq_forward(const LearnArgs& a, int n, float* Pa, float* Qa, float* Ws, uint8_t* M, const float* T) {
     const int B = a.batch, L = a.n_layers, mw = a.maxw, out0 = a.out[0];
     const float* Pn = n ? a.target : a.online;
-    dq_stage(B * out0, [&](int i) { return dq_load_sc1(a.sz0 + (int64_t)n * B * out0 + i); }, [&](int i, float z) {
-        const int b = i / out0, j = i - b * out0;
-        const float h = z > 0.0f ? z : 0.0f;
-        Pa[b * mw + j] = h;
-        if (n == 0) {
-            dq_store_sc1(a.sh[0] + i, h);
-            M[b * mw + j] = z > 0.0f;
+    dq_fetch(a.sz0 + (int64_t)n * B * out0, out0, B, out0, [&](int b, int j, dq_f4 z) {
+        for (int e = 0; e < 4; ++e) {
+            Pa[b * mw + j + e] = z[e] > 0.0f ? z[e] : 0.0f;
+            if (n == 0) M[b * mw + j + e] = z[e] > 0.0f;
         }
     });
+    __syncthreads();
+    DQ_STAMP(8);
+    if (n == 0) dq_publish(Pa, mw, a.sh[0], out0, B, out0);
     for (int l = 1; l < L; ++l) {
         const int li = a.out[l - 1], lo = a.out[l], ls = li + 4;
         const bool hidden = l < L - 1;
@@ -313,17 +340,15 @@ __device__ float* dq_forward(const LearnArgs& a, int n, float* Pa, float* Qa, fl
         dq_mm(Pa, mw, 1, W, ls, 1, li, B, lo, [&](int b, int j, float d) {
             const float z = d + bias[j];
             if (hidden) {
-                const float h = z > 0.0f ? z : 0.0f;
-                Qa[b * mw + j] = h;
-                if (n == 0) {
-                    dq_store_sc1(a.sh[l] + b * lo + j, h);
-                    M[(l * B + b) * mw + j] = z > 0.0f;
-                }
+                Qa[b * mw + j] = z > 0.0f ? z : 0.0f;
+                if (n == 0) M[(l * B + b) * mw + j] = z > 0.0f;
             } else {
                 Qa[b * mw + j] = z;
             }
         });
         __syncthreads();
+        DQ_STAMP(8 + l);
+        if (n == 0 && hidden) dq_publish(Qa, mw, a.sh[l], lo, B, lo);
         float* t = Pa;
         Pa = Qa;
         Qa = t;
@@ -394,7 +419,11 @@ __device__ __forceinline__ void dq_update_weights(const LearnArgs& a, const DqW 
 //     the later layers: gradient, Adam, packed image, target blend.
 // The tails are workgroups 0 and 1 so that they are dispatched first: every
 // wait in the kernel is on work that is already running.
-__global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs a) {
+__global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs args) {
+    // the arguments read in place from the kernarg segment (a by-value parameter that inlined code takes
+    // references to can be copied into private memory: 2.4 KB of scratch traffic per workgroup)
+    (void)args;
+    const LearnArgs& a = *(const LearnArgs*)__builtin_amdgcn_kernarg_segment_ptr();
     extern __shared__ float4 dq_lds4[];
     float* lds = reinterpret_cast<float*>(dq_lds4);
     __shared__ dq_tab s_tab;
@@ -413,7 +442,13 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs a)
     ctr.beta1_pow = a.ctr->beta1_pow;
     ctr.beta2_pow = a.ctr->beta2_pow;
     const bool due = ctr.step % a.target_every == 0;
-    DQ_STAMP(8 * blockIdx.x + 0);
+    DQ_STAMP(0);
+#ifdef DRL_DQN_STAMPS
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the shader clock against the 100 MHz wall clock
+        a.stamps[1000] = clock64();
+        a.stamps[1001] = wall_clock64();
+    }
+#endif
     if (!a.trained) {  // buffer.can_sample is false: no train_step this step (loss 0); the target blend when due
         if (due)
             for (int64_t i = tid; i < a.n_params; i += nt) a.target[i] = dq_blend(a, a.online[i], a.target[i]);
@@ -466,10 +501,10 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs a)
         }
         for (int e = tid; e < B * (in4 - in); e += nt) X[(e / (in4 - in)) * in4 + in + e % (in4 - in)] = 0.0f;
         __syncthreads();
-        DQ_STAMP(8 * blockIdx.x + 1);
+        DQ_STAMP(1);
         dq_stage_segs(lds, s_seg, s_start, 3, s_tab);
         __syncthreads();
-        DQ_STAMP(8 * blockIdx.x + 2);
+        DQ_STAMP(2);
         if (a.code_w) {  // one thread per (row, cell): its six channels
             const uint16_t* R = reinterpret_cast<const uint16_t*>(Bt + DQN_TILE);  // [B][rw] words
             const int W = a.code_w, cells = W * W, cpg = lay::code_cpg(W), cpg8 = lay::code_cpg8(W);
@@ -488,44 +523,69 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs a)
             }
             __syncthreads();
         }
-        float* z0 = a.sz0 + (int64_t)net * B * out0 + u0;
-        dq_mm(X, in4, 1, Wt, xs0, 1, in, B, nu, [&](int b, int u, float z) { dq_store_sc1(z0 + b * out0 + u, z + Bt[u]); });
+        // the tile's pre-activations -> LDS Z [B][DQN_TILE] (after a code net's rows), then 16-B write-through
+        float* Z = Bt + DQN_TILE + (a.code_w ? B * rw : 0);
+        dq_mm(X, in4, 1, Wt, xs0, 1, in, B, nu, [&](int b, int u, float z) { Z[b * DQN_TILE + u] = z + Bt[u]; });
+        __syncthreads();
+        dq_publish(Z, DQN_TILE, a.sz0 + (int64_t)net * B * out0 + u0, out0, B, nu);
         // hand-off: every wave drains its write-through stores, the workgroup barrier, one agent-scope ticket
-        DQ_STAMP(8 * blockIdx.x + 3);
+        DQ_STAMP(3);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) __hip_atomic_fetch_add(&a.ctr->arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // ---- 3. the weights, once the online tail has handed the deltas over
+        // ---- 3. the weights: online workgroups their tile's layer-0 rows, target ones a share of the later
+        // layers; the first DQN_PF per thread (weight, moments, target) are loaded into registers before the wait
+        const bool later = net != 0;
+        int64_t lo_i = 0, hi_i = (int64_t)nu * in;
+        if (later) {
+            const int64_t nw = a.wstart[L] - a.wstart[1], share = (nw + a.tiles0 - 1) / a.tiles0;
+            lo_i = (int64_t)(w % a.tiles0) * share;
+            hi_i = min(nw, lo_i + share);
+        }
+        const int64_t cnt = hi_i - lo_i;
+        auto locate = [&](int64_t f, int& l, int& row, int& k) -> int64_t {  // element f -> (layer, row, k, index)
+            if (!later) {
+                const int u = (int)__umulhi((uint32_t)f, a.rm_in);
+                l = 0;
+                row = u0 + u;
+                k = (int)f - u * in;
+                return a.woff[0] + (int64_t)row * in + k;
+            }
+            const int64_t gi = a.wstart[1] + lo_i + f;
+            l = 1;
+            while (l + 1 < L && gi >= a.wstart[l + 1]) ++l;
+            const int r0 = (int)(gi - a.wstart[l]), li = a.in[l];
+            row = r0 / li;
+            k = r0 - row * li;
+            return a.woff[l] + r0;
+        };
+        float pp[DQN_PF], pm[DQN_PF], pv[DQN_PF], pt[DQN_PF];
+#pragma unroll
+        for (int q = 0; q < DQN_PF; ++q) {
+            const int64_t f = tid + (int64_t)q * nt;
+            pp[q] = pm[q] = pv[q] = pt[q] = 0.0f;
+            if (f < cnt) {
+                int l, row, k;
+                const int64_t wi = locate(f, l, row, k);
+                pp[q] = a.online[wi];
+                pm[q] = a.adam_m[wi];
+                pv[q] = a.adam_v[wi];
+                if (due) pt[q] = a.target[wi];
+            }
+        }
         if (tid == 0) s_flag = dq_wait(a, &a.ctr->pad[2], epoch);
         __syncthreads();
-        DQ_STAMP(8 * blockIdx.x + 4);
+        DQ_STAMP(4);
         if (!s_flag) return;
-        if (net == 0) {  // this tile's layer-0 rows: dW0[u][k] = sum_b dz0[b][u0 + u] * X[b][k]
-            float* Dz = Wt;  // [B][DQN_TILE] (the weight tile is dead)
+        // the deltas (and the later layers' activations) the gradients read
+        int* off = s_start;                                          // [2 (L - 1) + 1] prefix offsets
+        const float** src = reinterpret_cast<const float**>(s_seg);  // [2 (L - 1)] sources
+        float* Dz = Wt;   // [B][DQN_TILE] this tile's layer-0 deltas (the weight tile is dead)
+        float* S = lds;   // later: D_l, H_{l-1} of every later layer (X is dead)
+        if (!later) {
             dq_stage(B * nu, [&](int i) { return dq_load_sc1(a.sd[0] + (i / nu) * out0 + u0 + i % nu); },
                      [&](int i, float d) { Dz[(i / nu) * DQN_TILE + i % nu] = d; });
-            __syncthreads();
-            const int n = nu * in;
-            for (int base = tid; base < n; base += DQN_UB * nt) {
-                DqW ws[DQN_UB];
-                int cnt = 0;
-#pragma unroll
-                for (int q = 0; q < DQN_UB; ++q) {
-                    const int e = base + q * nt;
-                    if (e >= n) break;
-                    const int u = (int)__umulhi((uint32_t)e, a.rm_in), k = e - u * in;
-                    float g = 0.0f;
-                    for (int b = 0; b < B; ++b) g = g + Dz[b * DQN_TILE + u] * X[b * in4 + k];
-                    ws[q] = DqW{0, u0 + u, k, a.woff[0] + (int64_t)(u0 + u) * in + k, g};
-                    cnt = q + 1;
-                }
-                if (cnt) dq_update_weights(a, ws, cnt, bc1, bc2, due);
-            }
-        } else {  // a share of the later layers' weights: dW_l[r][k] = sum_b D_l[b][r] * H_{l-1}[b][k]
-            // D_l and H_{l-1} of every later layer -> LDS (after X: the region is dead); segment table in LDS
-            int* off = s_start;                                       // [2 (L - 1) + 1] prefix offsets
-            const float** src = reinterpret_cast<const float**>(s_seg);  // [2 (L - 1)] sources
-            __syncthreads();
+        } else {
             if (tid == 0) {
                 int ns = 0, tot = 0;
                 for (int l = 1; l < L; ++l) {
@@ -539,39 +599,56 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs a)
                 off[ns] = tot;
             }
             __syncthreads();
-            float* S = lds;
-            const int tot = off[2 * (L - 1)];
-            dq_stage(tot, [&](int i) {
+            dq_stage(off[2 * (L - 1)], [&](int i) {
                 int g = 0;
                 while (i >= off[g + 1]) ++g;
                 return dq_load_sc1(src[g] + (i - off[g]));
             }, [&](int i, float v) { S[i] = v; });
-            __syncthreads();
-            const int64_t nw = a.wstart[L] - a.wstart[1], share = (nw + a.tiles0 - 1) / a.tiles0;
-            const int64_t lo_i = (int64_t)(w % a.tiles0) * share, hi_i = min(nw, lo_i + share);
-            for (int64_t base = lo_i + tid; base < hi_i; base += (int64_t)DQN_UB * nt) {
-                DqW ws[DQN_UB];
-                int cnt = 0;
+        }
+        __syncthreads();
+        // dW_l[row][k] = sum_b D_l[b][row] * H_{l-1}[b][k] in row order (layer 0: H = the sampled rows X)
+        auto grad = [&](int l, int row, int k) {
+            float g = 0.0f;
+            if (!later) {
+                for (int b = 0; b < B; ++b) g = g + Dz[b * DQN_TILE + (row - u0)] * X[b * in4 + k];
+            } else {
+                const int li = a.in[l], lo = a.out[l];
+                const float* D = S + off[2 * (l - 1)];
+                const float* H = S + off[2 * (l - 1) + 1];
+                for (int b = 0; b < B; ++b) g = g + D[b * lo + row] * H[b * li + k];
+            }
+            return g;
+        };
 #pragma unroll
-                for (int q = 0; q < DQN_UB; ++q) {
-                    const int64_t f = base + (int64_t)q * nt;
-                    if (f >= hi_i) break;
-                    const int64_t gi = a.wstart[1] + f;
-                    int l = 1;
-                    while (l + 1 < L && gi >= a.wstart[l + 1]) ++l;
-                    const int r0 = (int)(gi - a.wstart[l]), li = a.in[l], lo = a.out[l];
-                    const int row = r0 / li, k = r0 - row * li;
-                    const float* D = S + off[2 * (l - 1)];
-                    const float* H = S + off[2 * (l - 1) + 1];  // (LDS table reads)
-                    float g = 0.0f;
-                    for (int b = 0; b < B; ++b) g = g + D[b * lo + row] * H[b * li + k];
-                    ws[q] = DqW{l, row, k, a.woff[l] + r0, g};
-                    cnt = q + 1;
-                }
-                if (cnt) dq_update_weights(a, ws, cnt, bc1, bc2, due);
+        for (int q = 0; q < DQN_PF; ++q) {
+            const int64_t f = tid + (int64_t)q * nt;
+            if (f < cnt) {
+                int l, row, k;
+                const int64_t wi = locate(f, l, row, k);
+                float m = pm[q], v = pv[q];
+                const float nwt = dq_adam(a, pp[q], grad(l, row, k), &m, &v, bc1, bc2);
+                a.online[wi] = nwt;
+                a.adam_m[wi] = m;
+                a.adam_v[wi] = v;
+                qnet_pack_write(a.pack, l, qnet_pack_elem(l, row, k, a.pack.kt[l], a.pack.code_w), k, nwt);
+                if (due) a.target[wi] = dq_blend(a, nwt, pt[q]);
             }
         }
-        DQ_STAMP(8 * blockIdx.x + 5);
+        for (int64_t base = tid + (int64_t)DQN_PF * nt; base < cnt; base += (int64_t)DQN_UB * nt) {  // (wide tiles)
+            DqW ws[DQN_UB];
+            int c = 0;
+#pragma unroll
+            for (int q = 0; q < DQN_UB; ++q) {
+                const int64_t f = base + (int64_t)q * nt;
+                if (f >= cnt) break;
+                int l, row, k;
+                const int64_t wi = locate(f, l, row, k);
+                ws[q] = DqW{l, row, k, wi, grad(l, row, k)};
+                c = q + 1;
+            }
+            if (c) dq_update_weights(a, ws, c, bc1, bc2, due);
+        }
+        DQ_STAMP(5);
         return;
     }
 
@@ -587,16 +664,16 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs a)
     if (tid < ns) s_seg[tid] = a.tail[g0 + tid];
     if (tid <= ns) s_start[tid] = a.tail_start[g0 + tid] - a.tail_start[g0];
     __syncthreads();
-    DQ_STAMP(8 * blockIdx.x + 1);
+    DQ_STAMP(1);
     dq_stage_segs(lds, s_seg, s_start, ns, s_tab);
-    DQ_STAMP(8 * blockIdx.x + 2);
+    DQ_STAMP(2);
     if (tid == 0) s_flag = dq_wait(a, &a.ctr->arrive, (uint32_t)a.nblk0);  // every layer-0 workgroup's ticket
     __syncthreads();
-    DQ_STAMP(8 * blockIdx.x + 3);
+    DQ_STAMP(3);
     if (!s_flag) return;
     Pa = dq_forward(a, n, Pa, Qa, Ws, M, T);
     Qa = Pa == lds ? lds + B * mw : lds;
-    DQ_STAMP(8 * blockIdx.x + 4);
+    DQ_STAMP(4);
     const int A = a.out[L - 1];
     if (n == 1) {  // max_a Q_target, handed over write-through behind the second ticket
         for (int b = tid; b < B; b += nt) {
@@ -620,7 +697,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs a)
     if (!s_flag) return;
     for (int b = tid; b < B; b += nt) s_mx[b] = dq_load_sc1(a.smx + b);
     __syncthreads();
-    DQ_STAMP(8 * blockIdx.x + 5);
+    DQ_STAMP(5);
     float loss = 0.0f;
     for (int b = tid; b < B; b += nt) {
         const int act = __float_as_int(T[a.tr + b]);
@@ -644,11 +721,54 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs a)
         dq_store_sc1(a.sd[L - 1] + o, dq);
     }
     __syncthreads();
-    for (int l = L - 1; l >= 0; --l) {
+    for (int l = L - 1; l >= 1; --l) {
+        const int lo = a.out[l], li = a.out[l - 1], ls = li + 4;
+        const float* W = a.prefetch ? T + a.tw[0][l] : Ws;
+        if (!a.prefetch && l < L - 1) {  // (W_{L-1} is still staged from the forward pass)
+            __syncthreads();
+            dq_stage_w(a, a.online, l, Ws);  // (this step's weights: the layer-0 workgroups write them after)
+            __syncthreads();
+        }
+        // delta_{l-1}[b][i] = relu'(z) * sum_j D[b][j] W[j][i]: the same micro-tiles over the out index j
+        dq_mm(D, mw, 1, W, 1, ls, lo, B, li, [&](int b, int i, float s) { D2[b * mw + i] = s; });
+        __syncthreads();
+        for (int e = tid; e < B * li; e += nt) {  // relu'(z): the online forward's masks
+            const int b = e / li, i = e - b * li;
+            if (!M[((l - 1) * B + b) * mw + i]) D2[b * mw + i] = 0.0f;
+        }
+        __syncthreads();
+        DQ_STAMP(12 + L - 1 - l);
+        dq_publish(D2, mw, a.sd[l - 1], li, B, li);
+        float* t = D;
+        D = D2;
+        D2 = t;
+    }
+    DQ_STAMP(15);
+    // hand the deltas and activations over: every wave drains, the barrier, the epoch word
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store((gu32*)&a.ctr->pad[2], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    DQ_STAMP(6);
+#ifdef DRL_DQN_STAMPS
+    if (threadIdx.x == 0) {
+        a.stamps[1002] = clock64();
+        a.stamps[1003] = wall_clock64();
+    }
+#endif
+    // the biases, behind the hand-off: the batch sum of each layer's deltas (read back from it), Adam, the
+    // packed image, the target blend
+    for (int l = 0; l < L; ++l) {
         const int lo = a.out[l];
-        for (int j = tid; j < lo; j += nt) {  // the bias: the batch sum of the deltas, Adam, packed, target blend
+        for (int j = tid; j < lo; j += nt) {
+            float dv[DQN_STAGE];
             float g = 0.0f;
-            for (int b = 0; b < B; ++b) g = g + D[b * mw + j];
+            for (int b0 = 0; b0 < B; b0 += DQN_STAGE) {
+#pragma unroll
+                for (int q = 0; q < DQN_STAGE; ++q) dv[q] = b0 + q < B ? dq_load_sc1(a.sd[l] + (b0 + q) * lo + j) : 0.0f;
+#pragma unroll
+                for (int q = 0; q < DQN_STAGE; ++q)
+                    if (b0 + q < B) g = g + dv[q];
+            }
             const int64_t bi = a.boff[l] + j;
             float m = T[a.tm[l] + j], v = T[a.tv[l] + j];
             const float b0 = T[a.tb[0][l] + j], tb = T[a.tb[1][l] + j];
@@ -661,30 +781,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs a)
                 qnet_pack_write(a.pack, 0, qnet_pack_elem(0, j, -1, a.pack.kt[0], a.pack.code_w), -1, nb);
             if (due) a.target[bi] = dq_blend(a, nb, tb);
         }
-        if (l == 0) break;
-        const int li = a.out[l - 1], ls = li + 4;
-        const float* W = a.prefetch ? T + a.tw[0][l] : Ws;
-        if (!a.prefetch && l < L - 1) {  // (W_{L-1} is still staged from the forward pass)
-            __syncthreads();
-            dq_stage_w(a, a.online, l, Ws);  // (this step's weights: the layer-0 workgroups write them after)
-            __syncthreads();
-        }
-        // delta_{l-1}[b][i] = relu'(z) * sum_j D[b][j] W[j][i]: the same micro-tiles over the out index j
-        dq_mm(D, mw, 1, W, 1, ls, lo, B, li, [&](int b, int i, float s) {
-            const float dz = M[((l - 1) * B + b) * mw + i] ? s : 0.0f;
-            D2[b * mw + i] = dz;
-            dq_store_sc1(a.sd[l - 1] + b * li + i, dz);
-        });
-        __syncthreads();
-        float* t = D;
-        D = D2;
-        D2 = t;
     }
-    // hand the deltas and activations over: every wave drains, the barrier, the epoch word
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store((gu32*)&a.ctr->pad[2], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    DQ_STAMP(8 * blockIdx.x + 6);
     dq_finish(a, ctr, 1, loss, bc1, bc2);
 }
 

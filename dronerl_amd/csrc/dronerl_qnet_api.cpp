@@ -198,7 +198,8 @@ static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout
     P->xs0 = L.in[0] + ((2 - L.in[0]) % 32 + 32) % 32;
     const int rw = L.code_w ? drl::lay::code_bytes(L.code_w) / 4 : 0;
     // the layer-0 workgroups: X, the weight tile and its biases, a code net's sampled rows
-    int64_t a0 = (int64_t)batch * P->in4 + (int64_t)drl::DQN_TILE * P->xs0 + drl::DQN_TILE + (int64_t)batch * rw;
+    int64_t a0 = (int64_t)batch * P->in4 + (int64_t)drl::DQN_TILE * P->xs0 + drl::DQN_TILE + (int64_t)batch * rw +
+                 (int64_t)batch * drl::DQN_TILE;  // (+ the tile's pre-activations before they are published)
     int64_t later = 0;  // a target layer-0 workgroup's update phase: D_l and H_{l-1} of the later layers
     for (int l = 1; l < L.n_layers; ++l) later += (int64_t)batch * (L.out[l] + L.in[l]);
     a0 = std::max(a0, later);
@@ -663,7 +664,7 @@ static int dqn_train_impl(const drl_qnet_desc* d, const drl_dqn_hparams* h, void
     }
     fill_pack(L, d_packed, nullptr, nullptr, &a.pack);
 #ifdef DRL_DQN_STAMPS
-    a.stamps = reinterpret_cast<uint64_t*>(base + P.pub.bytes - 8192);
+    a.stamps = reinterpret_cast<uint64_t*>(base + P.pub.bytes - 8192);  // 16 per workgroup (<= 64)
 #endif
     a.wstart[0] = 0;
     for (int l = 0; l < L.n_layers; ++l) a.wstart[l + 1] = a.wstart[l] + (int64_t)L.in[l] * L.out[l];

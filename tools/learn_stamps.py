@@ -28,6 +28,12 @@ def build():
     subprocess.run(cmd, check=True)
 
 
+# the tails' stamp slots (workgroup 0 online, 1 target)
+TAIL = [(0, "start"), (1, "setup"), (2, "prefetched"), (3, "tickets_in"), (8, "z0_in"), (9, "layer1"),
+        (10, "layer2"), (4, "forward_done"), (5, "target_max_in"), (12, "bw_out"), (13, "bw_1"),
+        (14, "bw_2"), (15, "bw_done"), (6, "deltas_handed")]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
@@ -62,24 +68,25 @@ def main():
         lr.train(loop.rb)
         ev[k][1].record()
         torch.cuda.synchronize()
-        s = st.cpu().numpy().astype(np.int64).reshape(-1, 8)
-        on, tg, blk = s[0, :7], s[1, :5], s[2:2 + nblk, :6]
+        s = st.cpu().numpy().astype(np.int64).reshape(-1, 16)
+        on, tg, blk = s[0, :16], s[1, :16], s[2:2 + nblk, :6]
         t0 = min(blk[:, 0].min(), on[0], tg[0])
         f = lambda x: (x - t0) / 100.0  # noqa: E731
-        rows.append({"blocks": f(blk), "on": f(on), "tg": f(tg), "event_us": ev[k][0].elapsed_time(ev[k][1]) * 1e3})
+        flat = st.cpu().numpy().astype(np.int64)
+        mhz = (flat[1002] - flat[1000]) / max(1, flat[1003] - flat[1001]) * 100.0  # shader clock over the online tail
+        rows.append({"blocks": f(blk), "on": f(on), "tg": f(tg), "event_us": ev[k][0].elapsed_time(ev[k][1]) * 1e3,
+                     "mhz": mhz})
     med = lambda xs: float(np.median(xs))  # noqa: E731
     bl = np.stack([r["blocks"] for r in rows])
     on = np.stack([r["on"] for r in rows])
     tg = np.stack([r["tg"] for r in rows])
     out = {"config": args.config, "layer0_workgroups": nblk,
            "kernel_event_us": med([r["event_us"] for r in rows]),
+           "shader_clock_mhz": med([r["mhz"] for r in rows]),
            "layer0_us": {name: med(bl[:, :, i].max(1)) for i, name in
                          enumerate(["start", "setup", "staged", "z0_handed", "deltas_in", "weights_done"])},
-           "target_tail_us": {name: med(tg[:, i]) for i, name in
-                              enumerate(["start", "setup", "prefetched", "tickets_in", "forward_done"])},
-           "online_tail_us": {name: med(on[:, i]) for i, name in
-                              enumerate(["start", "setup", "prefetched", "tickets_in", "forward_done", "target_max_in",
-                                         "deltas_handed"])}}
+           "target_tail_us": {name: med(tg[:, i]) for i, name in TAIL if i < 5 or 8 <= i < 11},
+           "online_tail_us": {name: med(on[:, i]) for i, name in TAIL}}
     print(json.dumps(out, indent=1))
 
 
