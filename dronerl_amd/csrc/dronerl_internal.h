@@ -389,13 +389,13 @@ static_assert(sizeof(DqnCounters) == 64, "drl_dqn_counters is 64 bytes");
 
 constexpr int DQN_MAX_BATCH = 64;
 constexpr int DQN_TILE = 8;       // layer-0 units per workgroup of the learner kernel
-constexpr int DQN_THREADS = 512;  // the gradient kernel's workgroup
+constexpr int DQN_THREADS = 512;  // the learner kernel's workgroup
 constexpr int DQN_STAGE = 8;      // loads each thread keeps in flight when the learner stages data
-constexpr int DQN_MAX_SEGS = 28;  // copy segments of the gradient kernel's prefetch
+constexpr int DQN_MAX_SEGS = 28;  // copy segments of the learner kernel's prefetch
 constexpr int DQN_UB = 4;         // weights whose loads a thread issues together in the update phase
 constexpr int DQN_PF = 8;         // weights per thread whose operands are loaded before the epoch wait
 
-// One segment of the gradient kernel's one-round staging into LDS: element
+// One segment of the learner kernel's one-round staging into LDS: element
 // i < n lands at LDS float dst + (pad ? (i / row) * (row + pad) + i % row :
 // i) (kind 4: in float4 units, dst still in floats).  kind 0: f32 (or raw
 // 32-bit) at src[i]; 4: float4 at src[i]; the sampled rows' data through the
@@ -460,7 +460,7 @@ struct LearnArgs {
     float gamma, b1, b2, c1, c2, adam_eps, neg_lr, tau, one_minus_tau, eps_decay, eps_end, inv_batch;
     double b1d, b2d;
     int target_every, eps_every;
-    // the act kernels' packed image of the online net (drl_dqn_update_kernel refreshes it)
+    // the act kernels' packed image of the online net (the learner refreshes it)
     QnetPack pack;
     int64_t wstart[QN_MAX_LAYERS + 1];  // the weights in set order: index of layer l's first; [L] = their total
     uint64_t* stamps;                   // DRL_DQN_STAMPS builds: [8 per workgroup (<= 64)][512 + last workgroup's]

@@ -511,10 +511,10 @@ class DQNLearner:
                                             ctypes.byref(rb._c), rb.size, _stream(self.block.device)))
 
     def check_errors(self):
-        """Synchronise; raise if a gradient launch gave up waiting for its
-        workgroups (a hardware-scheduling fault, never expected)."""
+        """Synchronise; raise if a learner launch gave up waiting for one of
+        its hand-offs (a hardware-scheduling fault, never expected)."""
         if int(self._ctr_i[13].item()):
-            raise DroneRLError("drl_dqn_train: a tail workgroup timed out waiting for the layer-0 workgroups")
+            raise DroneRLError("drl_dqn_train: a workgroup timed out waiting for another workgroup's hand-off")
 
     def counters(self) -> dict:
         """Host copy of the device counters (synchronises)."""

@@ -507,7 +507,7 @@ typedef struct drl_dqn_layout {
     int64_t weight_off[4], bias_off[4];
     int64_t online_off, target_off, m_off, v_off;  /* bytes */
     int64_t counters_off, scratch_off, bytes;       /* bytes */
-    int32_t grad_workgroups, grad_lds_bytes;        /* the gradient launch (informative) */
+    int32_t grad_workgroups, grad_lds_bytes;        /* the learner launch: workgroups, dynamic LDS (informative) */
 } drl_dqn_layout;
 
 int drl_dqn_layout_query(const drl_qnet_desc* d, int32_t batch, drl_dqn_layout* layout);
