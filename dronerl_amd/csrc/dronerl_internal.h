@@ -401,7 +401,8 @@ constexpr int DQN_PF = 8;         // weights per thread whose operands are loade
 // 32-bit) at src[i]; 4: float4 at src[i]; the sampled rows' data through the
 // per-row pointer table tbl (0 obs row, 1 next_obs row, 2 action, 3 reward,
 // 4 done): kind 1: the 32-bit word at table[i]; 2: the u8 at table[i], as
-// 0.0f / 1.0f; 3: element (b, k) = table[b][k], k < row.  rm: the
+// 0.0f / 1.0f; 3: element (b, k) = table[b][k], k < row; 5: float2 at
+// src[i] (dst and pad in float2 units like kind 4's float4).  rm: the
 // multiply-shift reciprocal of row (i / row == umulhi(i, rm); 0 when row == 1).
 struct DqSeg {
     const void* src;
@@ -427,6 +428,7 @@ struct LearnArgs {
     int tail_start[DQN_MAX_SEGS + 1];
     float* smx;                       // scratch: max_a Q_target [batch] (the target tail's hand-off)
     int tw[2][QN_MAX_LAYERS], tb[2][QN_MAX_LAYERS], tm[QN_MAX_LAYERS], tv[QN_MAX_LAYERS], tr;  // LDS float offsets
+    int twt[QN_MAX_LAYERS];           // (prefetch) W_l^T [in_l][out_l + 2], built by the online tail for the backward
     int64_t woff[QN_MAX_LAYERS], boff[QN_MAX_LAYERS];  // float offsets of W_l / b_l in a parameter set
     int64_t n_params;                 // floats of a parameter set
     float* online;

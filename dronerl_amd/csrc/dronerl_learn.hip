@@ -163,6 +163,8 @@ __device__ __forceinline__ void dq_stage_w(const LearnArgs& a, const float* P, i
 typedef const __attribute__((address_space(1))) float gcf32;
 typedef float dq_f4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) dq_f4 gcf4;
+typedef float dq_f2 __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(1))) dq_f2 gcf2;
 typedef const __attribute__((address_space(1))) uint8_t gcu8;
 
 __device__ __forceinline__ uint32_t dq_div(uint32_t i, const DqSeg& g) { return g.rm ? __umulhi(i, g.rm) : i; }
@@ -178,13 +180,19 @@ __device__ __forceinline__ dq_f4 dq_seg_load(const DqSeg& g, int i, const dq_tab
             const int b = (int)dq_div((uint32_t)i, g);
             return dq_f4{((gcf32*)tab[g.tbl][b])[i - b * g.row], 0.0f, 0.0f, 0.0f};
         }
+        case 5: {
+            const dq_f2 v = ((gcf2*)g.src)[i];
+            return dq_f4{v.x, v.y, 0.0f, 0.0f};
+        }
         default: return ((gcf4*)g.src)[i];
     }
 }
+__device__ __forceinline__ int dq_seg_width(const DqSeg& g) { return g.kind == 4 ? 4 : g.kind == 5 ? 2 : 1; }
 __device__ __forceinline__ int dq_seg_dst(const DqSeg& g, int i) {
-    if (!g.pad) return g.dst + (g.kind == 4 ? 4 * i : i);
+    const int w = dq_seg_width(g);
+    if (!g.pad) return g.dst + w * i;
     const int r = (int)dq_div((uint32_t)i, g), c = i - r * g.row;
-    return g.dst + (g.kind == 4 ? 4 * (r * (g.row + g.pad) + c) : r * (g.row + g.pad) + c);
+    return g.dst + w * (r * (g.row + g.pad) + c);
 }
 
 // The segments seg[0..ns) (start: their prefix sums, start[ns] = total) in
@@ -199,12 +207,12 @@ __device__ __forceinline__ void dq_stage_segs(float* lds, const DqSeg* seg, cons
     for (int base = threadIdx.x; base < n; base += DQN_STAGE * nt) {
         dq_f4 v[DQN_STAGE];
         int d[DQN_STAGE];
-        bool w4[DQN_STAGE];
+        int w4[DQN_STAGE];
 #pragma unroll
         for (int q = 0; q < DQN_STAGE; ++q) {
             const int i = base + q * nt;
             d[q] = -1;
-            w4[q] = false;
+            w4[q] = 1;
             if (i < n) {
                 while (i >= ge) {
                     ++g;
@@ -214,13 +222,14 @@ __device__ __forceinline__ void dq_stage_segs(float* lds, const DqSeg* seg, cons
                 }
                 v[q] = dq_seg_load(cur, i - gs, tab);
                 d[q] = dq_seg_dst(cur, i - gs);
-                w4[q] = cur.kind == 4;
+                w4[q] = dq_seg_width(cur);
             }
         }
 #pragma unroll
         for (int q = 0; q < DQN_STAGE; ++q) {
             if (d[q] < 0) continue;
-            if (w4[q]) *reinterpret_cast<dq_f4*>(lds + d[q]) = v[q];
+            if (w4[q] == 4) *reinterpret_cast<dq_f4*>(lds + d[q]) = v[q];
+            else if (w4[q] == 2) *reinterpret_cast<dq_f2*>(lds + d[q]) = dq_f2{v[q].x, v[q].y};
             else lds[d[q]] = v[q].x;
         }
     }
@@ -331,7 +340,9 @@ __device__ __forceinline__ float* dq_forward(const LearnArgs& a, int n, float* P
     DQ_STAMP(8);
     if (n == 0) dq_publish(Pa, mw, a.sh[0], out0, B, out0);
     for (int l = 1; l < L; ++l) {
-        const int li = a.out[l - 1], lo = a.out[l], ls = li + 4;
+        // (prefetched rows: in + 2 floats, = 2 mod 32 for in a multiple of 32: the micro-tiles' two rows
+        // and four k classes hit 64 different banks; staged rows: in + 4)
+        const int li = a.out[l - 1], lo = a.out[l], ls = li + (a.prefetch ? 2 : 4);
         const bool hidden = l < L - 1;
         const float* W = a.prefetch ? T + a.tw[n][l] : Ws;
         const float* bias = T + a.tb[n][l];
@@ -666,6 +677,18 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
     __syncthreads();
     DQ_STAMP(1);
     dq_stage_segs(lds, s_seg, s_start, ns, s_tab);
+    if (n == 0 && a.prefetch) {  // W_l^T for the backward pass, built while the layer-0 workgroups run
+        __syncthreads();
+        for (int l = 1; l < L; ++l) {
+            const int li = a.in[l], lo = a.out[l];
+            const float* W = T + a.tw[0][l];
+            float* WT = lds + a.region_a + a.twt[l];
+            for (int e = tid; e < lo * li; e += nt) {
+                const int j = e / li, i = e - j * li;
+                WT[i * (lo + 2) + j] = W[j * (li + 2) + i];
+            }
+        }
+    }
     DQ_STAMP(2);
     if (tid == 0) s_flag = dq_wait(a, &a.ctr->arrive, (uint32_t)a.nblk0);  // every layer-0 workgroup's ticket
     __syncthreads();
@@ -723,14 +746,17 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
     __syncthreads();
     for (int l = L - 1; l >= 1; --l) {
         const int lo = a.out[l], li = a.out[l - 1], ls = li + 4;
-        const float* W = a.prefetch ? T + a.tw[0][l] : Ws;
         if (!a.prefetch && l < L - 1) {  // (W_{L-1} is still staged from the forward pass)
             __syncthreads();
             dq_stage_w(a, a.online, l, Ws);  // (this step's weights: the layer-0 workgroups write them after)
             __syncthreads();
         }
         // delta_{l-1}[b][i] = relu'(z) * sum_j D[b][j] W[j][i]: the same micro-tiles over the out index j
-        dq_mm(D, mw, 1, W, 1, ls, lo, B, li, [&](int b, int i, float s) { D2[b * mw + i] = s; });
+        // (prefetched: on W_l^T, rows of lo + 2 floats, the forward's bank pattern)
+        if (a.prefetch)
+            dq_mm(D, mw, 1, T + a.twt[l], lo + 2, 1, lo, B, li, [&](int b, int i, float s) { D2[b * mw + i] = s; });
+        else
+            dq_mm(D, mw, 1, Ws, 1, ls, lo, B, li, [&](int b, int i, float s) { D2[b * mw + i] = s; });
         __syncthreads();
         for (int e = tid; e < B * li; e += nt) {  // relu'(z): the online forward's masks
             const int b = e / li, i = e - b * li;

@@ -139,6 +139,7 @@ struct DqnPlan {
     int64_t sz0, smx, sh[drl::QN_MAX_LAYERS], sd[drl::QN_MAX_LAYERS];  // float offsets within the scratch
     int in4, xs0, maxw, tiles0, ws_floats, region_a, prefetch;
     int tw[2][drl::QN_MAX_LAYERS], tb[2][drl::QN_MAX_LAYERS], tm[drl::QN_MAX_LAYERS], tv[drl::QN_MAX_LAYERS], tr;
+    int twt[drl::QN_MAX_LAYERS];
     size_t lds;
 };
 
@@ -226,7 +227,11 @@ static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout
     const int64_t t_small = t;
     for (int l = 1; l < L.n_layers; ++l) {  // (each tail holds its own net's weights: the same offsets)
         P->tw[0][l] = P->tw[1][l] = (int)t;
-        t += (int64_t)L.out[l] * (L.in[l] + 4);
+        t += (int64_t)L.out[l] * (L.in[l] + 2);  // (rows of in + 2 floats: dq_mm's bank pattern)
+    }
+    for (int l = 1; l < L.n_layers; ++l) {  // the online tail's W_l^T for the backward pass
+        P->twt[l] = (int)t;
+        t += r4((int64_t)L.in[l] * (L.out[l] + 2));
     }
     constexpr int64_t kMaxFloats = 150 * 1024 / 4;  // (+ ~7 KB of the kernel's own LDS arrays)
     P->prefetch = std::max(a0, a1p + t) <= kMaxFloats;
@@ -555,6 +560,7 @@ static int dqn_train_impl(const drl_qnet_desc* d, const drl_dqn_hparams* h, void
     for (int l = 0; l < L.n_layers; ++l) {
         a.tw[0][l] = P.tw[0][l];
         a.tw[1][l] = P.tw[1][l];
+        a.twt[l] = P.twt[l];
         a.tb[0][l] = P.tb[0][l];
         a.tb[1][l] = P.tb[1][l];
         a.tm[l] = P.tm[l];
@@ -639,7 +645,7 @@ static int dqn_train_impl(const drl_qnet_desc* d, const drl_dqn_hparams* h, void
             const int first = ns;
             if (a.prefetch)
                 for (int l = 1; l < L.n_layers; ++l)
-                    seg(sets[n] + P.pub.weight_off[l], L.in[l] * L.out[l] / 4, P.tw[n][l], L.in[l] / 4, 1, 4);
+                    seg(sets[n] + P.pub.weight_off[l], L.in[l] * L.out[l] / 2, P.tw[n][l], L.in[l] / 2, 1, 5);
             if (n == 0) {
                 for (int m = 0; m < 2; ++m)
                     for (int l = 0; l < L.n_layers; ++l) seg(sets[m] + P.pub.bias_off[l], L.out[l], P.tb[m][l], 1, 0, 0);
