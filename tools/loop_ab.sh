@@ -1,23 +1,14 @@
 #!/bin/bash
-# train-loop A/B: one stream vs the replay add and the refill on parallel graph branches
-# (bench.py's train loop; the other measurements trimmed).
+# tools/loop_ab.sh — the bench's train loop (with the learner) serial vs parallel graph branches, C3 and C5
+# (GPU box; run through gpurun).  -> gpurun_out/loop_ab_<cfg>_<mode>.json
+set -u
+cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-L="--steps 20 --warmup 2 --no-cpu-baseline --no-reset-bench --rollout-chunk 0 --no-pmc-traffic --c5-envs 0 --cached-steps 0 --loop-segments 5"
-for r in 1 2; do
-  for mode in "one" "par"; do
-    case $mode in
-      one) A="" ;;
-      par) A="--parallel-loop" ;;
-    esac
-    timeout -k 10 300 python bench.py $L $A > gpurun_out/loop_ab.json 2> gpurun_out/loop_ab.err
-    rc=$?
-    if [ $rc -ne 0 ]; then echo "rc=$rc"; tail -3 gpurun_out/loop_ab.err; exit $rc; fi
-    MODE=$mode python - <<'PY' || exit 1
-import json, os
-t = open("gpurun_out/loop_ab.json").read()
-d = json.loads(t[t.find('{"metric"'):].splitlines()[0])
-print(os.environ["MODE"], round(d["train_loop"]["us_per_step"], 2), "us/step")
-PY
+A="--steps 20 --warmup 5 --no-cpu-baseline --no-reset-bench --rollout-chunk 0 --no-pmc-traffic --cached-steps 0 --c5-envs 0"
+for c in ${LCFGS:-c3 c5}; do
+  for m in serial parallel; do
+    P=""; [ $m = parallel ] && P="--parallel-loop"
+    timeout -k 10 300 python bench.py --config $c $A $P > gpurun_out/loop_ab_${c}_$m.json 2> gpurun_out/loop_ab_${c}_$m.log || exit $?
+    python3 -c "import json,sys; d=json.load(open('gpurun_out/loop_ab_${c}_$m.json')); t=d['train_loop']; print('$c $m', round(t['us_per_step'],2))"
   done
 done
