@@ -496,6 +496,9 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         float* Wt = lds + B * in4;        // [DQN_TILE][xs0] this tile's layer-0 weight rows, then its biases
         float* Bt = Wt + DQN_TILE * xs0;
         const int rw = (int)a.row_words;
+        float* Z = Bt + DQN_TILE + (a.code_w ? B * rw : 0);  // [B][DQN_TILE] the tile's pre-activations
+        float* W1s = Z + B * DQN_TILE;                         // (online, L > 1) [out1][DQN_TILE + 1] W_1's columns
+        float* D1s = W1s + (L > 1 ? a.out[1] * (DQN_TILE + 1) : 0);  // [B][out1] the handed-over layer-1 deltas
         const float* P = net ? a.target : a.online;
         if (tid == 0) {
             // the tile's weight rows are contiguous in the set: one flat copy into rows of xs0
@@ -516,6 +519,18 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         dq_stage_segs(lds, s_seg, s_start, 3, s_tab);
         __syncthreads();
         DQ_STAMP(2);
+        // the online tile's columns of W_1 (it forms its own layer-0 deltas from them, 3. below): loaded into
+        // registers now, stored to LDS after the tile's dot products, and landed before this workgroup's
+        // ticket (the drain below), so no read of them can see the update workgroups' writes
+        constexpr int W1R = 4;  // (out1 <= 128 hidden units x 8 = 2 per thread)
+        float w1r[W1R];
+        const bool w1 = net == 0 && L > 1;
+        const int n1 = w1 ? a.out[1] * nu : 0;
+#pragma unroll
+        for (int q = 0; q < W1R; ++q) {
+            const int e = tid + q * nt, r = e / DQN_TILE;
+            w1r[q] = e < n1 ? a.online[a.woff[1] + (int64_t)r * a.in[1] + u0 + (e - r * DQN_TILE)] : 0.0f;
+        }
         if (a.code_w) {  // one thread per (row, cell): its six channels
             const uint16_t* R = reinterpret_cast<const uint16_t*>(Bt + DQN_TILE);  // [B][rw] words
             const int W = a.code_w, cells = W * W, cpg = lay::code_cpg(W), cpg8 = lay::code_cpg8(W);
@@ -535,8 +550,12 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
             __syncthreads();
         }
         // the tile's pre-activations -> LDS Z [B][DQN_TILE] (after a code net's rows), then 16-B write-through
-        float* Z = Bt + DQN_TILE + (a.code_w ? B * rw : 0);
         dq_mm(X, in4, 1, Wt, xs0, 1, in, B, nu, [&](int b, int u, float z) { Z[b * DQN_TILE + u] = z + Bt[u]; });
+#pragma unroll
+        for (int q = 0; q < W1R; ++q) {
+            const int e = tid + q * nt, r = e / DQN_TILE;
+            if (e < n1) W1s[r * (DQN_TILE + 1) + (e - r * DQN_TILE)] = w1r[q];
+        }
         __syncthreads();
         dq_publish(Z, DQN_TILE, a.sz0 + (int64_t)net * B * out0 + u0, out0, B, nu);
         // hand-off: every wave drains its write-through stores, the workgroup barrier, one agent-scope ticket
@@ -593,9 +612,18 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         const float** src = reinterpret_cast<const float**>(s_seg);  // [2 (L - 1)] sources
         float* Dz = Wt;   // [B][DQN_TILE] this tile's layer-0 deltas (the weight tile is dead)
         float* S = lds;   // later: D_l, H_{l-1} of every later layer (X is dead)
-        if (!later) {
+        if (!later && L == 1) {  // (no hidden layer: the output deltas are layer 0's)
             dq_stage(B * nu, [&](int i) { return dq_load_sc1(a.sd[0] + (i / nu) * out0 + u0 + i % nu); },
                      [&](int i, float d) { Dz[(i / nu) * DQN_TILE + i % nu] = d; });
+        } else if (!later) {
+            // this tile's layer-0 deltas from the handed-over layer-1 deltas: relu'(z0) * sum_j D1[b][j] W1[j][u]
+            // (the oracle's backprop order over j), z0 still in Z
+            const int o1 = a.out[1];
+            dq_stage(B * o1, [&](int i) { return dq_load_sc1(a.sd[1] + i); }, [&](int i, float d) { D1s[i] = d; });
+            __syncthreads();
+            dq_mm(D1s, o1, 1, W1s, 1, DQN_TILE + 1, o1, B, nu, [&](int b, int u, float sum) {
+                Dz[b * DQN_TILE + u] = Z[b * DQN_TILE + u] > 0.0f ? sum : 0.0f;
+            });
         } else {
             if (tid == 0) {
                 int ns = 0, tot = 0;
@@ -617,6 +645,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
             }, [&](int i, float v) { S[i] = v; });
         }
         __syncthreads();
+        DQ_STAMP(6);
         // dW_l[row][k] = sum_b D_l[b][row] * H_{l-1}[b][k] in row order (layer 0: H = the sampled rows X)
         auto grad = [&](int l, int row, int k) {
             float g = 0.0f;
@@ -645,6 +674,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
                 if (due) a.target[wi] = dq_blend(a, nwt, pt[q]);
             }
         }
+        DQ_STAMP(7);
         for (int64_t base = tid + (int64_t)DQN_PF * nt; base < cnt; base += (int64_t)DQN_UB * nt) {  // (wide tiles)
             DqW ws[DQN_UB];
             int c = 0;
@@ -744,15 +774,15 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         dq_store_sc1(a.sd[L - 1] + o, dq);
     }
     __syncthreads();
-    for (int l = L - 1; l >= 1; --l) {
+    // delta_{l-1}[b][i] = relu'(z) * sum_j D[b][j] W[j][i] (the same micro-tiles over the out index j;
+    // prefetched: on W_l^T, rows of lo + 2 floats, the forward's bank pattern), published to sd[l - 1]
+    auto backward = [&](int l) {
         const int lo = a.out[l], li = a.out[l - 1], ls = li + 4;
         if (!a.prefetch && l < L - 1) {  // (W_{L-1} is still staged from the forward pass)
             __syncthreads();
-            dq_stage_w(a, a.online, l, Ws);  // (this step's weights: the layer-0 workgroups write them after)
+            dq_stage_w(a, a.online, l, Ws);  // (this step's weights: the update workgroups write them after)
             __syncthreads();
         }
-        // delta_{l-1}[b][i] = relu'(z) * sum_j D[b][j] W[j][i]: the same micro-tiles over the out index j
-        // (prefetched: on W_l^T, rows of lo + 2 floats, the forward's bank pattern)
         if (a.prefetch)
             dq_mm(D, mw, 1, T + a.twt[l], lo + 2, 1, lo, B, li, [&](int b, int i, float s) { D2[b * mw + i] = s; });
         else
@@ -768,7 +798,10 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         float* t = D;
         D = D2;
         D2 = t;
-    }
+    };
+    // down to layer 1's deltas before the hand-off: the online layer-0 workgroups form their own layer-0
+    // deltas from them (3. above)
+    for (int l = L - 1; l >= 2; --l) backward(l);
     DQ_STAMP(15);
     // hand the deltas and activations over: every wave drains, the barrier, the epoch word
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -781,6 +814,11 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         a.stamps[1003] = wall_clock64();
     }
 #endif
+    if (L > 1) {  // layer 0's deltas for its biases (published, drained: the bias loop reads them back)
+        backward(1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
     // the biases, behind the hand-off: the batch sum of each layer's deltas (read back from it), Adam, the
     // packed image, the target blend
     for (int l = 0; l < L; ++l) {

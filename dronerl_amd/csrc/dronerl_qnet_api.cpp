@@ -199,8 +199,11 @@ static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout
     P->xs0 = L.in[0] + ((2 - L.in[0]) % 32 + 32) % 32;
     const int rw = L.code_w ? drl::lay::code_bytes(L.code_w) / 4 : 0;
     // the layer-0 workgroups: X, the weight tile and its biases, a code net's sampled rows
+    // (+ the tile's pre-activations Z; with a hidden layer, the online tile's slice of W_1 [out1][TILE + 1]
+    // and the handed-over layer-1 deltas [B][out1], from which it forms its own layer-0 deltas)
+    const int64_t w1s = L.n_layers > 1 ? (int64_t)L.out[1] * (drl::DQN_TILE + 1) + (int64_t)batch * L.out[1] : 0;
     int64_t a0 = (int64_t)batch * P->in4 + (int64_t)drl::DQN_TILE * P->xs0 + drl::DQN_TILE + (int64_t)batch * rw +
-                 (int64_t)batch * drl::DQN_TILE;  // (+ the tile's pre-activations before they are published)
+                 (int64_t)batch * drl::DQN_TILE + w1s;
     int64_t later = 0;  // a target layer-0 workgroup's update phase: D_l and H_{l-1} of the later layers
     for (int l = 1; l < L.n_layers; ++l) later += (int64_t)batch * (L.out[l] + L.in[l]);
     a0 = std::max(a0, later);

@@ -69,7 +69,7 @@ def main():
         ev[k][1].record()
         torch.cuda.synchronize()
         s = st.cpu().numpy().astype(np.int64).reshape(-1, 16)
-        on, tg, blk = s[0, :16], s[1, :16], s[2:2 + nblk, :6]
+        on, tg, blk = s[0, :16], s[1, :16], s[2:2 + nblk, :8]
         t0 = min(blk[:, 0].min(), on[0], tg[0])
         f = lambda x: (x - t0) / 100.0  # noqa: E731
         flat = st.cpu().numpy().astype(np.int64)
@@ -84,7 +84,8 @@ def main():
            "kernel_event_us": med([r["event_us"] for r in rows]),
            "shader_clock_mhz": med([r["mhz"] for r in rows]),
            "layer0_us": {name: med(bl[:, :, i].max(1)) for i, name in
-                         enumerate(["start", "setup", "staged", "z0_handed", "deltas_in", "weights_done"])},
+                         [(0, "start"), (1, "setup"), (2, "staged"), (3, "z0_handed"), (4, "deltas_in"),
+                          (6, "deltas_staged"), (7, "registers_written"), (5, "weights_done")]},
            "target_tail_us": {name: med(tg[:, i]) for i, name in TAIL if i < 5 or 8 <= i < 11},
            "online_tail_us": {name: med(on[:, i]) for i, name in TAIL}}
     print(json.dumps(out, indent=1))
