@@ -341,8 +341,9 @@ __host__ __device__ inline int64_t qnet_pack_elem(int l, int row, int k, int kt,
             g = 0;
             sl = 6 * cpg;
         } else {
-            const int cell = k / 6, ch = k - 6 * cell, lc = cell % cpg;
-            g = cell / cpg;
+            const int cell = k / 6, ch = k - 6 * cell;
+            g = (cell >= cpg) + (cell >= 2 * cpg) + (cell >= 3 * cpg);  // (cell < 4 cpg: no division)
+            const int lc = cell - g * cpg;
             sl = lc < (cpg & ~1) ? 12 * (lc / 2) + 2 * ch + (lc & 1) : 6 * (cpg - 1) + ch;
         }
         t = sl / 8;
@@ -415,7 +416,7 @@ struct LearnArgs {
     int n_layers, batch, code_w, trained, nblk0, tiles0, maxw;
     int in[QN_MAX_LAYERS], out[QN_MAX_LAYERS];
     int in4;                          // layer 0's input row stride in LDS / scratch (in[0] rounded up to 4)
-    int xs0;                          // layer 0's weight row stride in LDS (>= in[0], = 2 mod 32: micro-tile banks)
+    int xs0;                          // layer 0's weight row stride in LDS (>= in[0], = 4 mod 32: dq_mm1's banks)
     uint32_t rm_in, rm_rw;            // DqSeg::rm of in[0] and of row_words
     int ws_floats;                    // per-layer weight staging (no prefetch): max over l >= 1 of out_l * (in_l + 4)
     int region_a;                     // the tail workgroup's LDS floats before its prefetched tail (activations, masks)

@@ -322,6 +322,30 @@ __device__ __forceinline__ void dq_mm(const float* X, int xs, int xk, const floa
     }
 }
 
+// The same dot products with one output per lane quad (lane c: k = c mod 4):
+// four times the lanes of dq_mm and a quarter of its per-lane chain, for
+// the layer-0 workgroups' small output tiles (8 units x B rows).
+template <class Out>
+__device__ __forceinline__ void dq_mm1(const float* X, int xs, const float* W, int wr, int wk, int n, int B, int J,
+                                       Out out) {
+    const int items = B * J * 4;
+    for (int base = 0; base < items; base += blockDim.x) {
+        const int it = base + threadIdx.x;
+        const bool live = it < items;
+        const int c = it & 3, pr = it >> 2;
+        const int j = pr % J, b = pr / J;
+        float s = 0.0f;
+        if (live) {
+            const float *x = X + b * xs, *w = W + j * wr;
+#pragma unroll 8
+            for (int k = c; k < n; k += 4) s = s + x[k] * w[k * wk];
+        }
+        s = s + __shfl_xor(s, 1);
+        s = s + __shfl_xor(s, 2);
+        if (live && c == 0) out(b, j, s);
+    }
+}
+
 // The later layers of net n (1 = target, 0 = online) for the B sampled rows,
 // from its layer-0 pre-activations (handed over write-through) and its
 // prefetched (or staged) weights; returns the buffer holding Q [B][A].  The
@@ -550,7 +574,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
             __syncthreads();
         }
         // the tile's pre-activations -> LDS Z [B][DQN_TILE] (after a code net's rows), then 16-B write-through
-        dq_mm(X, in4, 1, Wt, xs0, 1, in, B, nu, [&](int b, int u, float z) { Z[b * DQN_TILE + u] = z + Bt[u]; });
+        dq_mm1(X, in4, Wt, xs0, 1, in, B, nu, [&](int b, int u, float z) { Z[b * DQN_TILE + u] = z + Bt[u]; });
 #pragma unroll
         for (int q = 0; q < W1R; ++q) {
             const int e = tid + q * nt, r = e / DQN_TILE;
@@ -621,7 +645,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
             const int o1 = a.out[1];
             dq_stage(B * o1, [&](int i) { return dq_load_sc1(a.sd[1] + i); }, [&](int i, float d) { D1s[i] = d; });
             __syncthreads();
-            dq_mm(D1s, o1, 1, W1s, 1, DQN_TILE + 1, o1, B, nu, [&](int b, int u, float sum) {
+            dq_mm1(D1s, o1, W1s, 1, DQN_TILE + 1, o1, B, nu, [&](int b, int u, float sum) {
                 Dz[b * DQN_TILE + u] = Z[b * DQN_TILE + u] > 0.0f ? sum : 0.0f;
             });
         } else {
@@ -707,17 +731,20 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
     __syncthreads();
     DQ_STAMP(1);
     dq_stage_segs(lds, s_seg, s_start, ns, s_tab);
-    if (n == 0 && a.prefetch) {  // W_l^T for the backward pass, built while the layer-0 workgroups run
-        __syncthreads();
-        for (int l = 1; l < L; ++l) {
-            const int li = a.in[l], lo = a.out[l];
-            const float* W = T + a.tw[0][l];
-            float* WT = lds + a.region_a + a.twt[l];
-            for (int e = tid; e < lo * li; e += nt) {
-                const int j = e / li, i = e - j * li;
-                WT[i * (lo + 2) + j] = W[j * (li + 2) + i];
-            }
+    // W_l^T for the backward pass: l >= 2 while the layer-0 workgroups run, W_1^T (only layer 0's deltas,
+    // for its biases, read it) after the hand-off
+    auto transpose = [&](int l) {
+        const int li = a.in[l], lo = a.out[l];
+        const float* W = T + a.tw[0][l];
+        float* WT = lds + a.region_a + a.twt[l];
+        for (int e = tid; e < lo * li; e += nt) {
+            const int j = e / li, i = e - j * li;
+            WT[i * (lo + 2) + j] = W[j * (li + 2) + i];
         }
+    };
+    if (n == 0 && a.prefetch) {
+        __syncthreads();
+        for (int l = 2; l < L; ++l) transpose(l);
     }
     DQ_STAMP(2);
     if (tid == 0) s_flag = dq_wait(a, &a.ctr->arrive, (uint32_t)a.nblk0);  // every layer-0 workgroup's ticket
@@ -815,6 +842,10 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
     }
 #endif
     if (L > 1) {  // layer 0's deltas for its biases (published, drained: the bias loop reads them back)
+        if (a.prefetch) {
+            transpose(1);
+            __syncthreads();
+        }
         backward(1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();

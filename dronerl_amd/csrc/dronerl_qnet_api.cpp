@@ -196,7 +196,7 @@ static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout
     int ws = 0;
     for (int l = 1; l < L.n_layers; ++l) ws = std::max(ws, L.out[l] * (L.in[l] + 4));
     P->ws_floats = ws;
-    P->xs0 = L.in[0] + ((2 - L.in[0]) % 32 + 32) % 32;
+    P->xs0 = L.in[0] + ((4 - L.in[0]) % 32 + 32) % 32;  // (= 4 mod 32: dq_mm1's 8 rows x 4 classes, 32 banks)
     const int rw = L.code_w ? drl::lay::code_bytes(L.code_w) / 4 : 0;
     // the layer-0 workgroups: X, the weight tile and its biases, a code net's sampled rows
     // (+ the tile's pre-activations Z; with a hidden layer, the online tile's slice of W_1 [out1][TILE + 1]
