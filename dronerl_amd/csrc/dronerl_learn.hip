@@ -372,7 +372,7 @@ __device__ __forceinline__ float* dq_forward(const LearnArgs& a, int n, float* P
         const float* bias = T + a.tb[n][l];
         if (!a.prefetch) dq_stage_w(a, Pn, l, Ws);
         __syncthreads();
-        dq_mm(Pa, mw, 1, W, ls, 1, li, B, lo, [&](int b, int j, float d) {
+        auto put = [&](int b, int j, float d) {
             const float z = d + bias[j];
             if (hidden) {
                 Qa[b * mw + j] = z > 0.0f ? z : 0.0f;
@@ -380,7 +380,11 @@ __device__ __forceinline__ float* dq_forward(const LearnArgs& a, int n, float* P
             } else {
                 Qa[b * mw + j] = z;
             }
-        });
+        };
+        if (lo <= 8)  // (the 5-action output layer: one output per quad, more lanes, a shorter chain each)
+            dq_mm1(Pa, mw, W, ls, 1, li, B, lo, put);
+        else
+            dq_mm(Pa, mw, 1, W, ls, 1, li, B, lo, put);
         __syncthreads();
         DQ_STAMP(8 + l);
         if (n == 0 && hidden) dq_publish(Qa, mw, a.sh[l], lo, B, lo);
