@@ -1842,15 +1842,17 @@ __global__ void __launch_bounds__(256) drl_replay_add16_kernel(ReplayArgs a, Fas
     const uint32_t r = __umulhi(k, dcols.m), col = k - r * D4;  // D4 >= 2
     const int64_t i = a.first + r;
     const int64_t slot = ring_slot(a, r);
-    const uint4 o = reinterpret_cast<const uint4*>(a.obs + i * a.obs_stride)[col];
-    const uint4 nx = reinterpret_cast<const uint4*>(a.next_obs + i * a.next_obs_stride)[col];
-    reinterpret_cast<uint4*>(a.buf_obs + slot * a.obs_floats)[col] = o;
-    reinterpret_cast<uint4*>(a.buf_next_obs + slot * a.obs_floats)[col] = nx;
-    if (col == 0) {
-        a.buf_actions[slot] = a.actions[i * a.action_stride];
-        a.buf_rewards[slot] = a.rewards[i * a.reward_stride];
-        a.buf_dones[slot] = a.dones[i * a.done_stride];
-    }
+    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+    const u4v o = reinterpret_cast<const u4v*>(a.obs + i * a.obs_stride)[col];
+    const u4v nx = reinterpret_cast<const u4v*>(a.next_obs + i * a.next_obs_stride)[col];
+    // the ring rows are read back only by a later sample: streaming (nt) stores keep them out of the caches the
+    // next act and step read from
+    __builtin_nontemporal_store(o, reinterpret_cast<u4v*>(a.buf_obs + slot * a.obs_floats) + col);
+    __builtin_nontemporal_store(nx, reinterpret_cast<u4v*>(a.buf_next_obs + slot * a.obs_floats) + col);
+    // the row's scalars from three different lanes (their loads are gathers: one each, in parallel)
+    if (col == 1) a.buf_actions[slot] = a.actions[i * a.action_stride];
+    if (col == 2 % D4) a.buf_rewards[slot] = a.rewards[i * a.reward_stride];
+    if (col == 3 % D4) a.buf_dones[slot] = a.dones[i * a.done_stride];
 }
 
 __global__ void drl_replay_add_rows_kernel(ReplayArgs a) {  // fallback for huge batches: block per row
