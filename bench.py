@@ -778,13 +778,27 @@ def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fus
     learner = None
     if lr is not None:
         c = lr.counters()
-        learner = {"batch": lr.hp.batch, "learning_rate": lr.hp.learning_rate, "gamma": lr.hp.gamma,
+        # the learner alone, back to back on the loop's filled replay (HIP events around 50 launches; its
+        # device counters advance, nothing else is touched)
+        torch.cuda.synchronize(dev)
+        l0, l1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        l0.record()
+        for _ in range(50):
+            lr.train(loop.rb)
+        l1.record()
+        torch.cuda.synchronize(dev)
+        lr.check_errors()
+        learner_us = l0.elapsed_time(l1) * 1e3 / 50
+        c = lr.counters()
+        learner = {"us_per_launch_alone": learner_us, "batch": lr.hp.batch, "learning_rate": lr.hp.learning_rate, "gamma": lr.hp.gamma,
                    "tau": lr.hp.tau, "target_update_interval": lr.hp.target_update_interval,
                    "epsilon_decay_every": lr.hp.epsilon_decay_every, "epsilon_decay": lr.hp.decay(),
                    "replay_capacity": loop.rb.capacity, "steps_taken": c["step"], "adam_steps": c["count"],
                    "epsilon_after": c["epsilon"], "last_loss": c["loss"],
                    "note": "drl_dqn_train every step: sample + train_step (TD-MSE backward) + optax Adam, target "
-                           "update and epsilon decay on the device (train_jax.py:68-98)"}
+                           "update and epsilon decay on the device (train_jax.py:68-98); us_per_launch_alone: 50 "
+                           "launches back to back after the loop (latency-bound: DESIGN.md section 4 has the "
+                           "phase times)"}
     branches = (("replay add_many" if fused else "synthetic actions and replay add_many") +
                 " on parallel graph branches, 3 rotating buffers" if parallel else "one stream") + \
         ("; synthetic actions inside the act launch" if fused else "")
