@@ -395,6 +395,7 @@ constexpr int DQN_STAGE = 8;      // loads each thread keeps in flight when the 
 constexpr int DQN_MAX_SEGS = 28;  // copy segments of the learner kernel's prefetch
 constexpr int DQN_UB = 4;         // weights whose loads a thread issues together in the update phase
 constexpr int DQN_PF = 8;         // weights per thread whose operands are loaded before the epoch wait
+constexpr int DQN_W0R = 8;        // layer-0 tile weights per thread loaded into registers at the launch's start
 
 // One segment of the learner kernel's one-round staging into LDS: element
 // i < n lands at LDS float dst + (pad ? (i / row) * (row + pad) + i % row :

@@ -473,6 +473,22 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
     __shared__ int s_flag;
     const int tid = threadIdx.x, nt = blockDim.x;
     const int B = a.batch, L = a.n_layers;
+    // a layer-0 workgroup's weight tile does not depend on the counters: its loads go out first, beside the
+    // counters' (up to DQN_W0R per thread in registers; the rest, for inputs above 512, staged below)
+    const int in = a.in[0], in4 = a.in4, xs0 = a.xs0, out0 = a.out[0];
+    const int w0 = blockIdx.x - 2, net0 = w0 / (a.tiles0 > 0 ? a.tiles0 : 1);
+    const int u00 = (w0 % (a.tiles0 > 0 ? a.tiles0 : 1)) * DQN_TILE, nu0 = min(DQN_TILE, out0 - u00);
+    const bool l0wg = a.trained && blockIdx.x >= 2;
+    const int nw0 = l0wg ? nu0 * in : 0;
+    float w0r[DQN_W0R];
+    {
+        const float* src = (net0 ? a.target : a.online) + a.woff[0] + (int64_t)u00 * in;
+#pragma unroll
+        for (int q = 0; q < DQN_W0R; ++q) {
+            const int e = threadIdx.x + q * DQN_THREADS;
+            w0r[q] = e < nw0 ? ((gcf32*)src)[e] : 0.0f;
+        }
+    }
     // the counters as this step starts (the online tail writes them at the end)
     DqnCounters ctr;
     ctr.step = a.ctr->step;
@@ -514,7 +530,6 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         }
         for (int t = 0; t < 5; ++t) s_tab[t][tid] = p[t];
     }
-    const int in = a.in[0], in4 = a.in4, xs0 = a.xs0, out0 = a.out[0];
     const uint32_t epoch = (uint32_t)ctr.step + 1u;  // the online tail's hand-off word (pad[2]) for this step
     if (blockIdx.x >= 2) {
         // ---- 1. layer 0 of one net for DQN_TILE units
@@ -528,23 +543,28 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         float* W1s = Z + B * DQN_TILE;                         // (online, L > 1) [out1][DQN_TILE + 1] W_1's columns
         float* D1s = W1s + (L > 1 ? a.out[1] * (DQN_TILE + 1) : 0);  // [B][out1] the handed-over layer-1 deltas
         const float* P = net ? a.target : a.online;
-        if (tid == 0) {
-            // the tile's weight rows are contiguous in the set: one flat copy into rows of xs0
-            s_seg[0] = DqSeg{P + a.woff[0] + (int64_t)u0 * in, nu * in, B * in4, in, xs0 - in, 0, a.rm_in, 0};
-            s_seg[1] = DqSeg{P + a.boff[0] + u0, nu, B * in4 + DQN_TILE * xs0, 1, 0, 0, 0u, 0};
+        if (tid == 0) {  // the biases, the rows (the tile's weights are in registers: in <= 512, the plan checks)
+            s_seg[0] = DqSeg{P + a.boff[0] + u0, nu, B * in4 + DQN_TILE * xs0, 1, 0, 0, 0u, 0};
             if (a.code_w)  // the code rows, decoded from LDS below
-                s_seg[2] = DqSeg{nullptr, B * rw, B * in4 + DQN_TILE * xs0 + DQN_TILE, rw, 0, 3, a.rm_rw, net};
+                s_seg[1] = DqSeg{nullptr, B * rw, B * in4 + DQN_TILE * xs0 + DQN_TILE, rw, 0, 3, a.rm_rw, net};
             else
-                s_seg[2] = DqSeg{nullptr, B * in, 0, in, in4 - in, 3, a.rm_in, net};
+                s_seg[1] = DqSeg{nullptr, B * in, 0, in, in4 - in, 3, a.rm_in, net};
             s_start[0] = 0;
-            s_start[1] = nu * in;
-            s_start[2] = nu * in + nu;
-            s_start[3] = nu * in + nu + s_seg[2].n;
+            s_start[1] = nu;
+            s_start[2] = nu + s_seg[1].n;
+        }
+#pragma unroll
+        for (int q = 0; q < DQN_W0R; ++q) {  // the registers' weights -> rows of xs0
+            const int e = tid + q * nt;
+            if (e < nw0) {
+                const int r = (int)__umulhi((uint32_t)e, a.rm_in);
+                Wt[r * xs0 + (e - r * in)] = w0r[q];
+            }
         }
         for (int e = tid; e < B * (in4 - in); e += nt) X[(e / (in4 - in)) * in4 + in + e % (in4 - in)] = 0.0f;
         __syncthreads();
         DQ_STAMP(1);
-        dq_stage_segs(lds, s_seg, s_start, 3, s_tab);
+        dq_stage_segs(lds, s_seg, s_start, 2, s_tab);
         __syncthreads();
         DQ_STAMP(2);
         // the online tile's columns of W_1 (it forms its own layer-0 deltas from them, 3. below): loaded into

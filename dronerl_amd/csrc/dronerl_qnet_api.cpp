@@ -189,6 +189,8 @@ static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout
 #endif
     o.bytes = o.scratch_off + sc * 4;
     P->tiles0 = (L.out[0] + drl::DQN_TILE - 1) / drl::DQN_TILE;
+    if ((int64_t)L.in[0] * drl::DQN_TILE > (int64_t)drl::DQN_W0R * drl::DQN_THREADS)  // (in <= 512 by qnet_layout)
+        return fail("internal: a layer-0 tile does not fit the learner's weight registers");
     o.grad_workgroups = 2 * P->tiles0 + 2;
     // region A: layer 0 (X, the weight tile and its biases, a code net's sampled rows), then the last
     // workgroup's two activation buffers of one net and the online net's ReLU masks (+ one layer's weights
