@@ -391,7 +391,7 @@ static_assert(sizeof(DqnCounters) == 64, "drl_dqn_counters is 64 bytes");
 constexpr int DQN_MAX_BATCH = 64;
 constexpr int DQN_TILE = 8;       // layer-0 units per workgroup of the learner kernel
 constexpr int DQN_THREADS = 512;  // the learner kernel's workgroup
-constexpr int DQN_STAGE = 8;      // loads each thread keeps in flight when the learner stages data
+constexpr int DQN_STAGE = 12;     // loads each thread keeps in flight when the learner stages data
 constexpr int DQN_MAX_SEGS = 28;  // copy segments of the learner kernel's prefetch
 constexpr int DQN_UB = 4;         // weights whose loads a thread issues together in the update phase
 constexpr int DQN_PF = 8;         // weights per thread whose operands are loaded before the epoch wait
