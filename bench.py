@@ -798,7 +798,11 @@ def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fus
                    "note": "drl_dqn_train every step: sample + train_step (TD-MSE backward) + optax Adam, target "
                            "update and epsilon decay on the device (train_jax.py:68-98); us_per_launch_alone: 50 "
                            "launches back to back after the loop (latency-bound: DESIGN.md section 4 has the "
-                           "phase times)"}
+                           "phase times)",
+                   "parallelism": "one learner per rank, on that rank's env shard and replay (replicas): the "
+                                  "reference's sharded jit run trains one global learner, which would need the "
+                                  "sampled rows gathered across ranks every step (SURVEY.md section 8 E2; "
+                                  "DESIGN.md section 6)"}
     branches = (("replay add_many" if fused else "synthetic actions and replay add_many") +
                 " on parallel graph branches, 3 rotating buffers" if parallel else "one stream") + \
         ("; synthetic actions inside the act launch" if fused else "")
