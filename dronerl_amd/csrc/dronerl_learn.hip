@@ -15,13 +15,14 @@
 //
 // One launch (drl_dqn_train_kernel) per learner step: workgroups split
 // layer 0 of both nets (online on the sampled obs, target on next_obs) in
-// 16-unit tiles and hand their pre-activations over with write-through
+// 8-unit tiles and hand their pre-activations over with write-through
 // stores and a ticket counter; two more workgroups (the tails, one per net)
 // prefetch everything else into LDS meanwhile, wait for the tickets, and run
-// their net's later layers; the online tail then runs the TD error, the loss,
-// the backward pass and the bias updates, and hands the deltas over behind an
-// epoch word, on which the layer-0 workgroups update the weights (gradient,
-// Adam, the act kernels' packed fp16 hi/lo or bf16 image, the target blend).
+// their net's later layers; the online tail then runs the TD error, the loss
+// and the backward pass down to layer 1's deltas and hands them over behind
+// an epoch word, on which the layer-0 workgroups update the weights (their
+// own layer-0 deltas, gradient, Adam, the act kernels' packed fp16 hi/lo or
+// bf16 image, the target blend) while the online tail updates the biases.
 //
 // Arithmetic order is fixed and contraction-free (each product rounded, then
 // each sum), so oracle/dqn_learner.py reproduces the result bit for bit:
@@ -451,11 +452,13 @@ __device__ __forceinline__ void dq_update_weights(const LearnArgs& a, const DqW 
 //     biases, their moments and the rows' action / reward / done) meanwhile;
 //  2. the target tail: the target net's later layers, max_a Q_target handed
 //     over; the online tail: the online net's later layers, the TD error, the
-//     loss, the backward pass, the bias updates (Adam, packed image, target
-//     blend), the deltas and activations handed over behind an epoch word;
-//  3. the layer-0 workgroups take the weights: the online ones their own
-//     units' layer-0 rows (inputs still in LDS), the target ones a share of
-//     the later layers: gradient, Adam, packed image, target blend.
+//     loss, the backward pass to layer 1's deltas, handed over with the hidden
+//     activations behind an epoch word; then layer 0's deltas and the bias
+//     updates (Adam, packed image, target blend), the counters;
+//  3. the layer-0 workgroups take the weights: the online ones form their
+//     units' layer-0 deltas and update their layer-0 rows (inputs still in
+//     LDS), the target ones a share of the later layers: gradient, Adam,
+//     packed image, target blend.
 // The tails are workgroups 0 and 1 so that they are dispatched first: every
 // wait in the kernel is on work that is already running.
 __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs args) {
