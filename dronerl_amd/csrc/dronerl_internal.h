@@ -428,7 +428,7 @@ struct LearnArgs {
     int ntail_of[2];                  // the online tail's segments, then the target tail's (tail[ntail_of[0]..])
     DqSeg tail[DQN_MAX_SEGS];
     int tail_start[DQN_MAX_SEGS + 1];
-    float* smx;                       // scratch: max_a Q_target [batch] (the target tail's hand-off)
+    uint64_t* gmx;                    // scratch: max_a Q_target granules [batch] (the target tail's hand-off)
     int tw[2][QN_MAX_LAYERS], tb[2][QN_MAX_LAYERS], tm[QN_MAX_LAYERS], tv[QN_MAX_LAYERS], tr;  // LDS float offsets
     int twt[QN_MAX_LAYERS];           // (prefetch) W_l^T [in_l][out_l + 2], built by the online tail for the backward
     int64_t woff[QN_MAX_LAYERS], boff[QN_MAX_LAYERS];  // float offsets of W_l / b_l in a parameter set
@@ -438,7 +438,7 @@ struct LearnArgs {
     float* adam_m;
     float* adam_v;
     DqnCounters* ctr;
-    float* sz0;                       // scratch: layer-0 pre-activations [2 nets][batch][out0]
+    uint64_t* gz0;                    // scratch: layer-0 pre-activation granules [2 nets][batch][out0]
     float* sh[QN_MAX_LAYERS];         // scratch: online hidden activations h_l [batch][out_l]
     float* sd[QN_MAX_LAYERS];         // scratch: deltas dL/dz_l [batch][out_l]
     // replay rows (buffers.py:79-93 sample)

@@ -247,6 +247,30 @@ __device__ __forceinline__ float dq_load_sc1(const float* p) {
     return __uint_as_float(__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
+// Granule hand-off (MI355X_MICROARCH.md / cdna_hip_programming.md Guideline 16, R2: the data is the flag):
+// one naturally aligned 8-byte {tag = epoch, value} written by one sc1 store; the reader polls it with sc1
+// loads until the tag is this step's epoch (never 0; the scratch starts zeroed).  No ticket, no drain.
+typedef __attribute__((address_space(1))) uint64_t gu64;
+__device__ __forceinline__ void dq_granule_put(uint64_t* g, uint32_t epoch, float v) {
+    __hip_atomic_store((gu64*)g, ((uint64_t)epoch << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+// false after a bounded wait (DqnCounters::pad[0] = 1)
+__device__ __forceinline__ bool dq_granule_get(const LearnArgs& a, const uint64_t* g, uint32_t epoch, float* v) {
+    for (uint32_t spins = 0;; ++spins) {
+        const uint64_t x = __hip_atomic_load((gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(x >> 32) == epoch) {
+            *v = __uint_as_float((uint32_t)x);
+            return true;
+        }
+        if (spins > (1u << 22)) {
+            a.ctr->pad[0] = 1;
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 // 16-B write-through stores and loads (buffer ops, aux 16 = sc1: the same hand-off form as the 4-B ones, at
 // one fabric write per 16 B instead of per 4 B: MI355X_MICROARCH.md § visibility, stores of each flavour).
 typedef unsigned dq_u4 __attribute__((ext_vector_type(4)));
@@ -261,16 +285,6 @@ __device__ __forceinline__ void dq_publish(const float* src, int ss, float* dst,
         const int b = i / n4, j = 4 * (i - b * n4);
         const dq_f4 v = *reinterpret_cast<const dq_f4*>(src + b * ss + j);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dq_u4, v), r, (b * ds + j) * 4, 0, 16);
-    }
-}
-// global rows (stride ds, the first n floats, n % 4 == 0) -> f(b, j, four values), one 16-B load per lane
-template <class F>
-__device__ __forceinline__ void dq_fetch(const float* src, int ds, int B, int n, F f) {
-    const __amdgpu_buffer_rsrc_t r = dq_rsrc(src, (B - 1) * ds + n);
-    const int n4 = n >> 2;
-    for (int i = threadIdx.x; i < B * n4; i += blockDim.x) {
-        const int b = i / n4, j = 4 * (i - b * n4);
-        f(b, j, __builtin_bit_cast(dq_f4, __builtin_amdgcn_raw_buffer_load_b128(r, (b * ds + j) * 4, 0, 16)));
     }
 }
 
@@ -352,16 +366,24 @@ __device__ __forceinline__ void dq_mm1(const float* X, int xs, const float* W, i
 // prefetched (or staged) weights; returns the buffer holding Q [B][A].  The
 // online net also hands its hidden activations over (write-through: the
 // update phase reads them) and keeps its ReLU masks in LDS.
-__device__ __forceinline__ float* dq_forward(const LearnArgs& a, int n, float* Pa, float* Qa, float* Ws, uint8_t* M, const float* T) {
+__device__ __forceinline__ float* dq_forward(const LearnArgs& a, int n, float* Pa, float* Qa, float* Ws, uint8_t* M,
+                                             const float* T, uint32_t epoch, int* ok) {
     const int B = a.batch, L = a.n_layers, mw = a.maxw, out0 = a.out[0];
     const float* Pn = n ? a.target : a.online;
-    dq_fetch(a.sz0 + (int64_t)n * B * out0, out0, B, out0, [&](int b, int j, dq_f4 z) {
-        for (int e = 0; e < 4; ++e) {
-            Pa[b * mw + j + e] = z[e] > 0.0f ? z[e] : 0.0f;
-            if (n == 0) M[b * mw + j + e] = z[e] > 0.0f;
+    // the layer-0 workgroups' pre-activations: each thread polls its granules until they carry this epoch
+    const uint64_t* g = a.gz0 + (int64_t)n * B * out0;
+    for (int e = threadIdx.x; e < B * out0; e += blockDim.x) {
+        float z;
+        if (!dq_granule_get(a, g + e, epoch, &z)) {
+            *ok = 0;
+            break;
         }
-    });
+        const int b = e / out0, j = e - b * out0;
+        Pa[b * mw + j] = z > 0.0f ? z : 0.0f;
+        if (n == 0) M[b * mw + j] = z > 0.0f;
+    }
     __syncthreads();
+    if (!*ok) return nullptr;
     DQ_STAMP(8);
     if (n == 0) dq_publish(Pa, mw, a.sh[0], out0, B, out0);
     for (int l = 1; l < L; ++l) {
@@ -608,7 +630,10 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
             if (e < n1) W1s[r * (DQN_TILE + 1) + (e - r * DQN_TILE)] = w1r[q];
         }
         __syncthreads();
-        dq_publish(Z, DQN_TILE, a.sz0 + (int64_t)net * B * out0 + u0, out0, B, nu);
+        for (int e = tid; e < B * nu; e += nt) {  // the pre-activations as granules (the tails poll them)
+            const int b = e / nu, u = e - b * nu;
+            dq_granule_put(a.gz0 + ((int64_t)net * B + b) * out0 + u0 + u, epoch, Z[b * DQN_TILE + u]);
+        }
         // hand-off: every wave drains its write-through stores, the workgroup barrier, one agent-scope ticket
         DQ_STAMP(3);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -774,36 +799,28 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         for (int l = 2; l < L; ++l) transpose(l);
     }
     DQ_STAMP(2);
-    if (tid == 0) s_flag = dq_wait(a, &a.ctr->arrive, (uint32_t)a.nblk0);  // every layer-0 workgroup's ticket
+    if (tid == 0) s_flag = 1;
     __syncthreads();
     DQ_STAMP(3);
-    if (!s_flag) return;
-    Pa = dq_forward(a, n, Pa, Qa, Ws, M, T);
+    Pa = dq_forward(a, n, Pa, Qa, Ws, M, T, epoch, &s_flag);
+    if (!Pa) return;
     Qa = Pa == lds ? lds + B * mw : lds;
     DQ_STAMP(4);
     const int A = a.out[L - 1];
-    if (n == 1) {  // max_a Q_target, handed over write-through behind the second ticket
+    if (n == 1) {  // max_a Q_target, handed over as granules
         for (int b = tid; b < B; b += nt) {
             float mx = Pa[b * mw];
             for (int j = 1; j < A; ++j) mx = Pa[b * mw + j] > mx ? Pa[b * mw + j] : mx;  // jnp.max
-            dq_store_sc1(a.smx + b, mx);
+            dq_granule_put(a.gmx + b, epoch, mx);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) __hip_atomic_fetch_add(&a.ctr->pad[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
     for (int b = tid; b < B; b += nt)
         for (int j = 0; j < A; ++j) s_q[b * 8 + j] = Pa[b * mw + j];
-    if (tid == 0) {  // the target tail's ticket; then both tickets are free for the next step
-        s_flag = dq_wait(a, &a.ctr->pad[1], 1u);
-        __hip_atomic_store((gu32*)&a.ctr->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((gu32*)&a.ctr->pad[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    for (int b = tid; b < B; b += nt)
+        if (!dq_granule_get(a, a.gmx + b, epoch, &s_mx[b])) s_flag = 0;
     __syncthreads();
     if (!s_flag) return;
-    for (int b = tid; b < B; b += nt) s_mx[b] = dq_load_sc1(a.smx + b);
-    __syncthreads();
     DQ_STAMP(5);
     float loss = 0.0f;
     for (int b = tid; b < B; b += nt) {
@@ -904,7 +921,12 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
             if (due) a.target[bi] = dq_blend(a, nb, tb);
         }
     }
-    dq_finish(a, ctr, 1, loss, bc1, bc2);
+    if (tid == 0) {  // every layer-0 workgroup has read this step's counters (its ticket): then write them
+        s_flag = dq_wait(a, &a.ctr->arrive, (uint32_t)a.nblk0);
+        __hip_atomic_store((gu32*)&a.ctr->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (s_flag) dq_finish(a, ctr, 1, loss, bc1, bc2);
 }
 
 __global__ void drl_dqn_init_kernel(DqnCounters* c, float epsilon) {

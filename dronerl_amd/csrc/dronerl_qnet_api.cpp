@@ -172,10 +172,10 @@ static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout
     for (int l = 0; l < L.n_layers; ++l) maxw = L.out[l] > maxw ? L.out[l] : maxw;
     P->maxw = (int)r4(maxw);
     int64_t sc = 0;
-    P->sz0 = sc;
-    sc += r4(2ll * batch * L.out[0]);
+    P->sz0 = sc;  // granules: 8 B each
+    sc += r4(2 * 2ll * batch * L.out[0]);
     P->smx = sc;
-    sc += r4(batch);
+    sc += r4(2ll * batch);
     for (int l = 0; l + 1 < L.n_layers; ++l) {
         P->sh[l] = sc;
         sc += r4((int64_t)batch * L.out[l]);
@@ -584,8 +584,8 @@ static int dqn_train_impl(const drl_qnet_desc* d, const drl_dqn_hparams* h, void
     a.adam_v = reinterpret_cast<float*>(base + P.pub.v_off);
     a.ctr = reinterpret_cast<drl::DqnCounters*>(base + P.pub.counters_off);
     float* sc = reinterpret_cast<float*>(base + P.pub.scratch_off);
-    a.sz0 = sc + P.sz0;
-    a.smx = sc + P.smx;
+    a.gz0 = reinterpret_cast<uint64_t*>(sc + P.sz0);
+    a.gmx = reinterpret_cast<uint64_t*>(sc + P.smx);
     for (int l = 0; l < L.n_layers; ++l) {
         a.sh[l] = l + 1 < L.n_layers ? sc + P.sh[l] : nullptr;
         a.sd[l] = sc + P.sd[l];
