@@ -426,6 +426,7 @@ struct LearnArgs {
     // region A in its first load round (tail[]); otherwise the last workgroup stages layer by layer
     int prefetch, ntail;
     int ntail_of[2];                  // the online tail's segments, then the target tail's (tail[ntail_of[0]..])
+    int ntail_a, ntail_b;             // the online tail's: A before the forward pass, B behind it, C the rest
     DqSeg tail[DQN_MAX_SEGS];
     int tail_start[DQN_MAX_SEGS + 1];
     uint64_t* gmx;                    // scratch: max_a Q_target granules [batch] (the target tail's hand-off)

@@ -202,10 +202,10 @@ __device__ __forceinline__ int dq_seg_dst(const DqSeg& g, int i) {
 // registers and re-read from LDS only when it crosses into the next one.
 __device__ __forceinline__ void dq_stage_segs(float* lds, const DqSeg* seg, const int* start, int ns,
                                               const dq_tab& tab) {
-    const int n = start[ns], nt = blockDim.x;
-    int g = 0, ge = start[1], gs = 0;
+    const int n = start[ns], nt = blockDim.x;  // (start[0] may be > 0: a later part of a list)
+    int g = 0, ge = start[1], gs = start[0];
     DqSeg cur = seg[0];
-    for (int base = threadIdx.x; base < n; base += DQN_STAGE * nt) {
+    for (int base = start[0] + threadIdx.x; base < n; base += DQN_STAGE * nt) {
         dq_f4 v[DQN_STAGE];
         int d[DQN_STAGE];
         int w4[DQN_STAGE];
@@ -492,6 +492,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
     float* lds = reinterpret_cast<float*>(dq_lds4);
     __shared__ dq_tab s_tab;
     __shared__ float s_d[DQN_MAX_BATCH], s_mx[DQN_MAX_BATCH], s_q[DQN_MAX_BATCH * 8];
+    __shared__ float s_gb[QN_MAX_LAYERS][128];  // (online tail) the biases' gradients, formed with the deltas
     __shared__ int s_act[DQN_MAX_BATCH];
     __shared__ DqSeg s_seg[DQN_MAX_SEGS];
     __shared__ int s_start[DQN_MAX_SEGS + 1];
@@ -679,6 +680,14 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
                 if (due) pt[q] = a.target[wi];
             }
         }
+        // (online side, with a hidden layer) its units' layer-0 biases: moments and target loaded ahead too
+        const bool b0up = net == 0 && L > 1 && tid < nu;
+        float bm = 0.0f, bv = 0.0f, bt = 0.0f;
+        if (b0up) {
+            bm = a.adam_m[a.boff[0] + u0 + tid];
+            bv = a.adam_v[a.boff[0] + u0 + tid];
+            if (due) bt = a.target[a.boff[0] + u0 + tid];
+        }
         if (tid == 0) s_flag = dq_wait(a, &a.ctr->pad[2], epoch);
         __syncthreads();
         DQ_STAMP(4);
@@ -722,6 +731,20 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         }
         __syncthreads();
         DQ_STAMP(6);
+        if (b0up) {  // the layer-0 bias of unit u0 + tid: the batch sum of its deltas, Adam, packed, target blend
+            const int u = tid;
+            float g = 0.0f;
+            for (int b = 0; b < B; ++b) g = g + Dz[b * DQN_TILE + u];
+            const int64_t bi = a.boff[0] + u0 + u;
+            const float nb = dq_adam(a, Bt[u], g, &bm, &bv, bc1, bc2);
+            a.online[bi] = nb;
+            a.adam_m[bi] = bm;
+            a.adam_v[bi] = bv;
+            a.pack.packed_b[a.pack.bias_off[0] + u0 + u] = nb;
+            if (a.pack.code_w > 0)
+                qnet_pack_write(a.pack, 0, qnet_pack_elem(0, u0 + u, -1, a.pack.kt[0], a.pack.code_w), -1, nb);
+            if (due) a.target[bi] = dq_blend(a, nb, bt);
+        }
         // dW_l[row][k] = sum_b D_l[b][row] * H_{l-1}[b][k] in row order (layer 0: H = the sampled rows X)
         auto grad = [&](int l, int row, int k) {
             float g = 0.0f;
@@ -782,7 +805,9 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
     if (tid <= ns) s_start[tid] = a.tail_start[g0 + tid] - a.tail_start[g0];
     __syncthreads();
     DQ_STAMP(1);
-    dq_stage_segs(lds, s_seg, s_start, ns, s_tab);
+    const int ka = n == 0 ? a.ntail_a : ns, kb = n == 0 ? a.ntail_b : 0;  // (the online tail's parts A, B, C)
+    dq_stage_segs(lds, s_seg, s_start, ka, s_tab);
+    DQ_STAMP(7);
     // W_l^T for the backward pass: l >= 2 while the layer-0 workgroups run, W_1^T (only layer 0's deltas,
     // for its biases, read it) after the hand-off
     auto transpose = [&](int l) {
@@ -817,6 +842,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
     }
     for (int b = tid; b < B; b += nt)
         for (int j = 0; j < A; ++j) s_q[b * 8 + j] = Pa[b * mw + j];
+    dq_stage_segs(lds, s_seg + ka, s_start + ka, kb, s_tab);  // B: the rows' action, reward, done
     for (int b = tid; b < B; b += nt)
         if (!dq_granule_get(a, a.gmx + b, epoch, &s_mx[b])) s_flag = 0;
     __syncthreads();
@@ -845,6 +871,16 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         dq_store_sc1(a.sd[L - 1] + o, dq);
     }
     __syncthreads();
+    // each layer's bias gradient, the batch sum of its deltas in row order, as its deltas appear (the bias
+    // updates run behind the hand-off; layer 0's: the online layer-0 workgroups, which form its deltas)
+    auto bias_grad = [&](int l, const float* Dl) {
+        for (int j = tid; j < a.out[l]; j += nt) {
+            float g = 0.0f;
+            for (int b = 0; b < B; ++b) g = g + Dl[b * mw + j];
+            s_gb[l][j] = g;
+        }
+    };
+    bias_grad(L - 1, D);
     // delta_{l-1}[b][i] = relu'(z) * sum_j D[b][j] W[j][i] (the same micro-tiles over the out index j;
     // prefetched: on W_l^T, rows of lo + 2 floats, the forward's bank pattern), published to sd[l - 1]
     auto backward = [&](int l) {
@@ -866,6 +902,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         __syncthreads();
         DQ_STAMP(12 + L - 1 - l);
         dq_publish(D2, mw, a.sd[l - 1], li, B, li);
+        bias_grad(l - 1, D2);
         float* t = D;
         D = D2;
         D2 = t;
@@ -885,29 +922,14 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         a.stamps[1003] = wall_clock64();
     }
 #endif
-    if (L > 1) {  // layer 0's deltas for its biases (published, drained: the bias loop reads them back)
-        if (a.prefetch) {
-            transpose(1);
-            __syncthreads();
-        }
-        backward(1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-    // the biases, behind the hand-off: the batch sum of each layer's deltas (read back from it), Adam, the
-    // packed image, the target blend
-    for (int l = 0; l < L; ++l) {
+    dq_stage_segs(lds, s_seg + ka + kb, s_start + ka + kb, ns - ka - kb, s_tab);  // C: for the bias updates
+    __syncthreads();
+    // the biases of layers >= 1 (layer 0's too without a hidden layer): Adam on the gradients formed above,
+    // the packed image, the target blend
+    for (int l = L > 1 ? 1 : 0; l < L; ++l) {
         const int lo = a.out[l];
         for (int j = tid; j < lo; j += nt) {
-            float dv[DQN_STAGE];
-            float g = 0.0f;
-            for (int b0 = 0; b0 < B; b0 += DQN_STAGE) {
-#pragma unroll
-                for (int q = 0; q < DQN_STAGE; ++q) dv[q] = b0 + q < B ? dq_load_sc1(a.sd[l] + (b0 + q) * lo + j) : 0.0f;
-#pragma unroll
-                for (int q = 0; q < DQN_STAGE; ++q)
-                    if (b0 + q < B) g = g + dv[q];
-            }
+            const float g = s_gb[l][j];
             const int64_t bi = a.boff[l] + j;
             float m = T[a.tm[l] + j], v = T[a.tv[l] + j];
             const float b0 = T[a.tb[0][l] + j], tb = T[a.tb[1][l] + j];
@@ -921,6 +943,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
             if (due) a.target[bi] = dq_blend(a, nb, tb);
         }
     }
+    DQ_STAMP(14);
     if (tid == 0) {  // every layer-0 workgroup has read this step's counters (its ticket): then write them
         s_flag = dq_wait(a, &a.ctr->arrive, (uint32_t)a.nblk0);
         __hip_atomic_store((gu32*)&a.ctr->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

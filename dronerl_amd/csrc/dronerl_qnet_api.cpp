@@ -234,8 +234,8 @@ static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout
         P->tw[0][l] = P->tw[1][l] = (int)t;
         t += (int64_t)L.out[l] * (L.in[l] + 2);  // (rows of in + 2 floats: dq_mm's bank pattern)
     }
-    for (int l = 1; l < L.n_layers; ++l) {  // the online tail's W_l^T for the backward pass
-        P->twt[l] = (int)t;
+    for (int l = 2; l < L.n_layers; ++l) {  // the online tail's W_l^T for the backward pass (layer 0's deltas:
+        P->twt[l] = (int)t;                    // the layer-0 workgroups, from W_1's columns)
         t += r4((int64_t)L.in[l] * (L.out[l] + 2));
     }
     constexpr int64_t kMaxFloats = 150 * 1024 / 4;  // (+ ~7 KB of the kernel's own LDS arrays)
@@ -652,18 +652,25 @@ static int dqn_train_impl(const drl_qnet_desc* d, const drl_dqn_hparams* h, void
                 for (int l = 1; l < L.n_layers; ++l)
                     seg(sets[n] + P.pub.weight_off[l], L.in[l] * L.out[l] / 2, P.tw[n][l], L.in[l] / 2, 1, 5);
             if (n == 0) {
-                for (int m = 0; m < 2; ++m)
-                    for (int l = 0; l < L.n_layers; ++l) seg(sets[m] + P.pub.bias_off[l], L.out[l], P.tb[m][l], 1, 0, 0);
-                for (int l = 0; l < L.n_layers; ++l) {
-                    seg(a.adam_m + P.pub.bias_off[l], L.out[l], P.tm[l], 1, 0, 0);
-                    seg(a.adam_v + P.pub.bias_off[l], L.out[l], P.tv[l], 1, 0, 0);
-                }
-                seg(nullptr, h->batch, P.tr, 1, 0, 1);  // (the sampled rows' action, reward, done: tables 2-4)
+                // A (before the forward pass): the weights, the online biases of the later layers, the sampled
+                // rows' action, reward, done (tables 2-4); C (behind the hand-off, for the bias updates): layer
+                // 0's bias, the target biases, the moments.  (B, the rows behind the forward pass, measured
+                // slower: their round trip then lands between the forward pass and the TD error)
+                for (int l = 1; l < L.n_layers; ++l) seg(sets[0] + P.pub.bias_off[l], L.out[l], P.tb[0][l], 1, 0, 0);
+                seg(nullptr, h->batch, P.tr, 1, 0, 1);
                 a.tail[ns - 1].tbl = 2;
                 seg(nullptr, h->batch, P.tr + h->batch, 1, 0, 1);
                 a.tail[ns - 1].tbl = 3;
                 seg(nullptr, h->batch, P.tr + 2 * h->batch, 1, 0, 2);
                 a.tail[ns - 1].tbl = 4;
+                a.ntail_a = ns - first;
+                a.ntail_b = 0;
+                seg(sets[0] + P.pub.bias_off[0], L.out[0], P.tb[0][0], 1, 0, 0);
+                for (int l = 0; l < L.n_layers; ++l) seg(sets[1] + P.pub.bias_off[l], L.out[l], P.tb[1][l], 1, 0, 0);
+                for (int l = 0; l < L.n_layers; ++l) {
+                    seg(a.adam_m + P.pub.bias_off[l], L.out[l], P.tm[l], 1, 0, 0);
+                    seg(a.adam_v + P.pub.bias_off[l], L.out[l], P.tv[l], 1, 0, 0);
+                }
             } else {
                 for (int l = 1; l < L.n_layers; ++l) seg(sets[1] + P.pub.bias_off[l], L.out[l], P.tb[1][l], 1, 0, 0);
             }

@@ -29,9 +29,9 @@ def build():
 
 
 # the tails' stamp slots (workgroup 0 online, 1 target)
-TAIL = [(0, "start"), (1, "setup"), (2, "prefetched"), (3, "tickets_in"), (8, "z0_in"), (9, "layer1"),
+TAIL = [(0, "start"), (1, "setup"), (7, "staged"), (2, "prefetched"), (3, "tickets_in"), (8, "z0_in"), (9, "layer1"),
         (10, "layer2"), (4, "forward_done"), (5, "target_max_in"), (12, "bw_out"), (13, "bw_1"),
-        (14, "bw_2"), (15, "bw_done"), (6, "deltas_handed")]
+        (15, "bw_done"), (6, "deltas_handed"), (14, "biases_done")]
 
 
 def main():
@@ -86,7 +86,7 @@ def main():
            "layer0_us": {name: med(bl[:, :, i].max(1)) for i, name in
                          [(0, "start"), (1, "setup"), (2, "staged"), (3, "z0_handed"), (4, "deltas_in"),
                           (6, "deltas_staged"), (7, "registers_written"), (5, "weights_done")]},
-           "target_tail_us": {name: med(tg[:, i]) for i, name in TAIL if i < 5 or 8 <= i < 11},
+           "target_tail_us": {name: med(tg[:, i]) for i, name in TAIL if i < 5 or 7 <= i < 11},
            "online_tail_us": {name: med(on[:, i]) for i, name in TAIL}}
     print(json.dumps(out, indent=1))
 
