@@ -731,20 +731,6 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         }
         __syncthreads();
         DQ_STAMP(6);
-        if (b0up) {  // the layer-0 bias of unit u0 + tid: the batch sum of its deltas, Adam, packed, target blend
-            const int u = tid;
-            float g = 0.0f;
-            for (int b = 0; b < B; ++b) g = g + Dz[b * DQN_TILE + u];
-            const int64_t bi = a.boff[0] + u0 + u;
-            const float nb = dq_adam(a, Bt[u], g, &bm, &bv, bc1, bc2);
-            a.online[bi] = nb;
-            a.adam_m[bi] = bm;
-            a.adam_v[bi] = bv;
-            a.pack.packed_b[a.pack.bias_off[0] + u0 + u] = nb;
-            if (a.pack.code_w > 0)
-                qnet_pack_write(a.pack, 0, qnet_pack_elem(0, u0 + u, -1, a.pack.kt[0], a.pack.code_w), -1, nb);
-            if (due) a.target[bi] = dq_blend(a, nb, bt);
-        }
         // dW_l[row][k] = sum_b D_l[b][row] * H_{l-1}[b][k] in row order (layer 0: H = the sampled rows X)
         auto grad = [&](int l, int row, int k) {
             float g = 0.0f;
@@ -772,6 +758,20 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
                 qnet_pack_write(a.pack, l, qnet_pack_elem(l, row, k, a.pack.kt[l], a.pack.code_w), k, nwt);
                 if (due) a.target[wi] = dq_blend(a, nwt, pt[q]);
             }
+        }
+        if (b0up) {  // (after the weights: the wave holding these threads is not held up) the layer-0 bias of unit u0 + tid: the batch sum of its deltas, Adam, packed, target blend
+            const int u = tid;
+            float g = 0.0f;
+            for (int b = 0; b < B; ++b) g = g + Dz[b * DQN_TILE + u];
+            const int64_t bi = a.boff[0] + u0 + u;
+            const float nb = dq_adam(a, Bt[u], g, &bm, &bv, bc1, bc2);
+            a.online[bi] = nb;
+            a.adam_m[bi] = bm;
+            a.adam_v[bi] = bv;
+            a.pack.packed_b[a.pack.bias_off[0] + u0 + u] = nb;
+            if (a.pack.code_w > 0)
+                qnet_pack_write(a.pack, 0, qnet_pack_elem(0, u0 + u, -1, a.pack.kt[0], a.pack.code_w), -1, nb);
+            if (due) a.target[bi] = dq_blend(a, nb, bt);
         }
         DQ_STAMP(7);
         for (int64_t base = tid + (int64_t)DQN_PF * nt; base < cnt; base += (int64_t)DQN_UB * nt) {  // (wide tiles)
