@@ -440,6 +440,7 @@ struct LearnArgs {
     float* adam_v;
     DqnCounters* ctr;
     uint64_t* gz0;                    // scratch: layer-0 pre-activation granules [2 nets][batch][out0]
+    uint64_t* gd1;                    // scratch: layer-1 delta granules [batch][out1] (the online layer-0 side)
     float* sh[QN_MAX_LAYERS];         // scratch: online hidden activations h_l [batch][out_l]
     float* sd[QN_MAX_LAYERS];         // scratch: deltas dL/dz_l [batch][out_l]
     // replay rows (buffers.py:79-93 sample)

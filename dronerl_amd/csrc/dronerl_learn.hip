@@ -688,7 +688,9 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
             bv = a.adam_v[a.boff[0] + u0 + tid];
             if (due) bt = a.target[a.boff[0] + u0 + tid];
         }
-        if (tid == 0) s_flag = dq_wait(a, &a.ctr->pad[2], epoch);
+        // the online side (with a hidden layer) polls the layer-1 delta granules below instead of the epoch word
+        const bool d1g = !later && L > 1;
+        if (tid == 0) s_flag = d1g ? 1 : dq_wait(a, &a.ctr->pad[2], epoch);
         __syncthreads();
         DQ_STAMP(4);
         if (!s_flag) return;
@@ -704,8 +706,11 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
             // this tile's layer-0 deltas from the handed-over layer-1 deltas: relu'(z0) * sum_j D1[b][j] W1[j][u]
             // (the oracle's backprop order over j), z0 still in Z
             const int o1 = a.out[1];
-            dq_stage(B * o1, [&](int i) { return dq_load_sc1(a.sd[1] + i); }, [&](int i, float d) { D1s[i] = d; });
+            for (int i = tid; i < B * o1; i += nt)  // the granules: polled in place (Guideline 16, R2)
+                if (!dq_granule_get(a, a.gd1 + i, epoch, &D1s[i])) s_flag = 0;
             __syncthreads();
+            if (!s_flag) return;
+            DQ_STAMP(4);
             dq_mm1(D1s, o1, W1s, 1, DQN_TILE + 1, o1, B, nu, [&](int b, int u, float sum) {
                 Dz[b * DQN_TILE + u] = Z[b * DQN_TILE + u] > 0.0f ? sum : 0.0f;
             });
@@ -869,6 +874,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         const float dq = (s_act[b] == j) ? (s_d[b] + s_d[b]) / (float)B : 0.0f;
         D[b * mw + j] = dq;
         dq_store_sc1(a.sd[L - 1] + o, dq);
+        if (L == 2) dq_granule_put(a.gd1 + o, epoch, dq);  // (layer 1's deltas: the online layer-0 workgroups)
     }
     __syncthreads();
     // each layer's bias gradient, the batch sum of its deltas in row order, as its deltas appear (the bias
@@ -901,6 +907,11 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         }
         __syncthreads();
         DQ_STAMP(12 + L - 1 - l);
+        if (l == 2)  // layer 1's deltas, also as granules: the online layer-0 workgroups poll them
+            for (int e = tid; e < B * li; e += nt) {
+                const int b = e / li, i = e - b * li;
+                dq_granule_put(a.gd1 + e, epoch, D2[b * mw + i]);
+            }
         dq_publish(D2, mw, a.sd[l - 1], li, B, li);
         bias_grad(l - 1, D2);
         float* t = D;

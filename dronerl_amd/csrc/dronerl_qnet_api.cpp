@@ -136,7 +136,7 @@ int num_cus() {
 // regions of drl::LearnArgs, and the gradient launch's LDS.
 struct DqnPlan {
     drl_dqn_layout pub;
-    int64_t sz0, smx, sh[drl::QN_MAX_LAYERS], sd[drl::QN_MAX_LAYERS];  // float offsets within the scratch
+    int64_t sz0, smx, sd1, sh[drl::QN_MAX_LAYERS], sd[drl::QN_MAX_LAYERS];  // float offsets within the scratch
     int in4, xs0, maxw, tiles0, ws_floats, region_a, prefetch;
     int tw[2][drl::QN_MAX_LAYERS], tb[2][drl::QN_MAX_LAYERS], tm[drl::QN_MAX_LAYERS], tv[drl::QN_MAX_LAYERS], tr;
     int twt[drl::QN_MAX_LAYERS];
@@ -176,6 +176,8 @@ static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout
     sc += r4(2 * 2ll * batch * L.out[0]);
     P->smx = sc;
     sc += r4(2ll * batch);
+    P->sd1 = sc;  // layer-1 delta granules
+    sc += L.n_layers > 1 ? r4(2ll * batch * L.out[1]) : 0;
     for (int l = 0; l + 1 < L.n_layers; ++l) {
         P->sh[l] = sc;
         sc += r4((int64_t)batch * L.out[l]);
@@ -586,6 +588,7 @@ static int dqn_train_impl(const drl_qnet_desc* d, const drl_dqn_hparams* h, void
     float* sc = reinterpret_cast<float*>(base + P.pub.scratch_off);
     a.gz0 = reinterpret_cast<uint64_t*>(sc + P.sz0);
     a.gmx = reinterpret_cast<uint64_t*>(sc + P.smx);
+    a.gd1 = reinterpret_cast<uint64_t*>(sc + P.sd1);
     for (int l = 0; l < L.n_layers; ++l) {
         a.sh[l] = l + 1 < L.n_layers ? sc + P.sh[l] : nullptr;
         a.sd[l] = sc + P.sd[l];
