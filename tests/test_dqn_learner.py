@@ -309,6 +309,9 @@ def assert_same(learner, st, where):
     ((294, 64, 5), "code", dict(batch=1, epsilon_decay=0.9, epsilon_decay_every=1), 16, 100),
     ((294, 96, 32, 32, 5), "code", dict(batch=32, learning_rate=3e-3, gamma=0.95), 40, 500),
     ((294, 128, 64, 5), "code", dict(batch=64, target_update_interval=7, sample_seed=99), 24, 96),
+    # narrow layer 0, wide later layers: the tails stage those weights layer by layer (no prefetch) and the
+    # target-side shares exceed the registers' 8 per thread (the batched fallback update)
+    ((294, 32, 128, 128, 5), "code", dict(batch=8, tau=0.5, target_update_interval=2), 32, 200),
 ])
 def test_learner_matches_oracle_bit_exact(sizes, inp, hp_kw, E, cap):
     """The train_jax.py loop shape with the learner on: act (device epsilon)
