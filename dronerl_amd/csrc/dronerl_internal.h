@@ -363,8 +363,7 @@ __host__ __device__ inline int64_t qnet_pack_elem(int l, int row, int k, int kt,
 // weights carry the input's 1/100; DRL_QNET_F32 writes fp16 hi and lo =
 // fp16((w - hi) * 2^11) (|w| >= 65504 or NaN raises DRL_ERR_QNET_RANGE in the
 // packed net's status word), DRL_QNET_BF16 a bf16.
-__device__ __forceinline__ void qnet_pack_write(const QnetPack& p, int l, int64_t e, int k, float w) {
-    if (l == 0 && p.code_w > 0 && k >= 0 && k < p.in[l] && k % 6 == 4) w /= 100.0f;
+__device__ __forceinline__ void qnet_pack_store(const QnetPack& p, int l, int64_t e, float w) {
     if (p.precision == DRL_QNET_F32) {
         if (!(__builtin_fabsf(w) < 65504.0f)) atomicOr(p.status, DRL_ERR_QNET_RANGE);
         const _Float16 hi = (_Float16)w;
@@ -373,6 +372,16 @@ __device__ __forceinline__ void qnet_pack_write(const QnetPack& p, int l, int64_
     } else {
         reinterpret_cast<__bf16*>(p.packed_w)[(int64_t)p.frag_off[l] * 8 + e] = (__bf16)w;
     }
+}
+__device__ __forceinline__ void qnet_pack_write(const QnetPack& p, int l, int64_t e, int k, float w) {
+    if (l == 0 && p.code_w > 0 && k >= 0 && k < p.in[l] && k % 6 == 4) w /= 100.0f;
+    qnet_pack_store(p, l, e, w);
+}
+// The learner's table form (drl_dqn_init writes it): a weight's element in its layer's fragments in bits
+// 0-30, bit 31 set where a code net's charge channel carries the input's 1/100.
+__device__ __forceinline__ void qnet_pack_write_idx(const QnetPack& p, int l, uint32_t pe, float w) {
+    if (pe >> 31) w /= 100.0f;
+    qnet_pack_store(p, l, (int64_t)(pe & 0x7fffffffu), w);
 }
 
 // ----------------------------------------------------------- DQN learner ---
@@ -441,6 +450,7 @@ struct LearnArgs {
     DqnCounters* ctr;
     uint64_t* gz0;                    // scratch: layer-0 pre-activation granules [2 nets][batch][out0]
     uint64_t* gd1;                    // scratch: layer-1 delta granules [batch][out1] (the online layer-0 side)
+    const uint32_t* pidx;             // scratch: each weight's packed-image element (qnet_pack_write_idx) [n_params]
     float* sh[QN_MAX_LAYERS];         // scratch: online hidden activations h_l [batch][out_l]
     float* sd[QN_MAX_LAYERS];         // scratch: deltas dL/dz_l [batch][out_l]
     // replay rows (buffers.py:79-93 sample)

@@ -443,12 +443,14 @@ struct DqW {
 __device__ __forceinline__ void dq_update_weights(const LearnArgs& a, const DqW (&w)[DQN_UB], int cnt, float bc1,
                                                   float bc2, bool due) {
     float p[DQN_UB], m[DQN_UB], v[DQN_UB], t[DQN_UB];
+    uint32_t px[DQN_UB];
 #pragma unroll
     for (int q = 0; q < DQN_UB; ++q) {
         const int64_t wi = q < cnt ? w[q].wi : w[0].wi;
         p[q] = a.online[wi];
         m[q] = a.adam_m[wi];
         v[q] = a.adam_v[wi];
+        px[q] = a.pidx[wi];
         t[q] = due ? a.target[wi] : 0.0f;
     }
 #pragma unroll
@@ -458,8 +460,7 @@ __device__ __forceinline__ void dq_update_weights(const LearnArgs& a, const DqW 
         a.online[w[q].wi] = nw;
         a.adam_m[w[q].wi] = m[q];
         a.adam_v[w[q].wi] = v[q];
-        qnet_pack_write(a.pack, w[q].l, qnet_pack_elem(w[q].l, w[q].row, w[q].k, a.pack.kt[w[q].l], a.pack.code_w),
-                        w[q].k, nw);
+        qnet_pack_write_idx(a.pack, w[q].l, px[q], nw);
         if (due) a.target[w[q].wi] = dq_blend(a, nw, t[q]);
     }
 }
@@ -667,16 +668,19 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
             return a.woff[l] + r0;
         };
         float pp[DQN_PF], pm[DQN_PF], pv[DQN_PF], pt[DQN_PF];
+        uint32_t px[DQN_PF];
 #pragma unroll
         for (int q = 0; q < DQN_PF; ++q) {
             const int64_t f = tid + (int64_t)q * nt;
             pp[q] = pm[q] = pv[q] = pt[q] = 0.0f;
+            px[q] = 0u;
             if (f < cnt) {
                 int l, row, k;
                 const int64_t wi = locate(f, l, row, k);
                 pp[q] = a.online[wi];
                 pm[q] = a.adam_m[wi];
                 pv[q] = a.adam_v[wi];
+                px[q] = a.pidx[wi];
                 if (due) pt[q] = a.target[wi];
             }
         }
@@ -760,7 +764,9 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
                 a.online[wi] = nwt;
                 a.adam_m[wi] = m;
                 a.adam_v[wi] = v;
-                qnet_pack_write(a.pack, l, qnet_pack_elem(l, row, k, a.pack.kt[l], a.pack.code_w), k, nwt);
+#ifndef DRL_DIAG_NO_PACKW  // (diagnostic: timing without the packed image's writes; wrong results)
+                qnet_pack_write_idx(a.pack, l, px[q], nwt);
+#endif
                 if (due) a.target[wi] = dq_blend(a, nwt, pt[q]);
             }
         }

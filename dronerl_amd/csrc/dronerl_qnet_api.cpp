@@ -136,7 +136,7 @@ int num_cus() {
 // regions of drl::LearnArgs, and the gradient launch's LDS.
 struct DqnPlan {
     drl_dqn_layout pub;
-    int64_t sz0, smx, sd1, sh[drl::QN_MAX_LAYERS], sd[drl::QN_MAX_LAYERS];  // float offsets within the scratch
+    int64_t sz0, smx, sd1, spx, sh[drl::QN_MAX_LAYERS], sd[drl::QN_MAX_LAYERS];  // float offsets in the scratch
     int in4, xs0, maxw, tiles0, ws_floats, region_a, prefetch;
     int tw[2][drl::QN_MAX_LAYERS], tb[2][drl::QN_MAX_LAYERS], tm[drl::QN_MAX_LAYERS], tv[drl::QN_MAX_LAYERS], tr;
     int twt[drl::QN_MAX_LAYERS];
@@ -178,6 +178,8 @@ static int dqn_plan(const drl_qnet_desc* d, int32_t batch, const drl::QnetLayout
     sc += r4(2ll * batch);
     P->sd1 = sc;  // layer-1 delta granules
     sc += L.n_layers > 1 ? r4(2ll * batch * L.out[1]) : 0;
+    P->spx = sc;  // the weights' packed-image elements (drl_dqn_init)
+    sc += r4(f);
     for (int l = 0; l + 1 < L.n_layers; ++l) {
         P->sh[l] = sc;
         sc += r4((int64_t)batch * L.out[l]);
@@ -519,6 +521,20 @@ int drl_dqn_init(const drl_qnet_desc* d, int32_t batch, void* d_agent, float eps
     const size_t set = (size_t)P.pub.n_params * 4;
     if (hipError_t e = hipMemsetAsync(base + P.pub.m_off, 0, 2 * set, stream); e != hipSuccess)
         return hip_fail(e, "drl_dqn_init moments");
+    // each weight's element in the act kernels' packed image (qnet_pack_elem, once: the learner reads it)
+    std::vector<uint32_t> px((size_t)P.pub.n_params, 0u);
+    for (int l = 0; l < L.n_layers; ++l)
+        for (int row = 0; row < L.out[l]; ++row)
+            for (int k = 0; k < L.in[l]; ++k) {
+                const int64_t pe = drl::qnet_pack_elem(l, row, k, L.kt[l], L.code_w);
+                const bool scale = l == 0 && L.code_w > 0 && k % 6 == 4;
+                px[(size_t)(P.pub.weight_off[l] + (int64_t)row * L.in[l] + k)] = (uint32_t)pe | (scale ? 0x80000000u : 0u);
+            }
+    if (hipError_t e = hipMemcpyAsync(base + P.pub.scratch_off + P.spx * 4, px.data(), px.size() * 4,
+                                      hipMemcpyHostToDevice, stream); e != hipSuccess)
+        return hip_fail(e, "drl_dqn_init pack index");
+    if (hipError_t e = hipStreamSynchronize(stream); e != hipSuccess)  // (px is a host temporary)
+        return hip_fail(e, "drl_dqn_init pack index");
     hipError_t e = drl::launch_dqn_init(base + P.pub.counters_off, epsilon_start, stream);
     return e == hipSuccess ? 0 : hip_fail(e, "drl_dqn_init launch");
 }
@@ -589,6 +605,7 @@ static int dqn_train_impl(const drl_qnet_desc* d, const drl_dqn_hparams* h, void
     a.gz0 = reinterpret_cast<uint64_t*>(sc + P.sz0);
     a.gmx = reinterpret_cast<uint64_t*>(sc + P.smx);
     a.gd1 = reinterpret_cast<uint64_t*>(sc + P.sd1);
+    a.pidx = reinterpret_cast<const uint32_t*>(sc + P.spx);
     for (int l = 0; l < L.n_layers; ++l) {
         a.sh[l] = l + 1 < L.n_layers ? sc + P.sh[l] : nullptr;
         a.sd[l] = sc + P.sd[l];

@@ -4,7 +4,7 @@ stamps (100 MHz) of a -DDRL_DQN_STAMPS build (tools/var_dqnstamps.so, never
 the product library).  Every figure is the latest workgroup's, in us from the
 earliest workgroup start (median over steps).
 
-python tools/learn_stamps.py [--config c3] [--steps 20] [--build]
+python tools/learn_stamps.py [--config c3] [--steps 20] [--build]   (DQN_FLAGS="-D..." adds build macros)
 Per workgroup: setup (segment table + sample), stage (the prefetch round),
 compute (layer-0 tile + its write-through stores), drain (vmcnt + barrier),
 ticket; the last workgroup: target forward, online forward, TD, backward +
@@ -24,7 +24,7 @@ LIB = os.path.join(REPO, "tools", "var_dqnstamps.so")
 def build():
     from dronerl_amd import build as b
     cmd = [b.hipcc(), f"--offload-arch={b.ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DDRL_DQN_STAMPS",
-           "-I", os.path.join(REPO, "include"), "-o", LIB] + b.SOURCES
+           "-I", os.path.join(REPO, "include"), "-o", LIB] + os.environ.get("DQN_FLAGS", "").split() + b.SOURCES
     subprocess.run(cmd, check=True)
 
 
