@@ -617,7 +617,7 @@ class TrainSegment:
 
     def __init__(self, env, seg: int, parallel: bool = False, net=None, rb=None, fused: bool = True,
                  precision: str = "f32", input: str = "obs", learn: bool = True, capacity: int = MEMORY_SIZE,
-                 hp=None):
+                 hp=None, fuse_replay=None):
         from dronerl_amd.dqn import DQNHParams, DQNLearner, QNetwork, ReplayBuffer
         E, N, dev = env.num_envs, env.n_drones, env.device
         W = env.layout.obs_window
@@ -629,6 +629,13 @@ class TrainSegment:
         # stores code rows, decoding the rows it samples to the observation
         self.input = input
         self.fused = fused
+        # fuse_replay (code input, one stream; the default there): the step lands its drone-0 transitions in
+        # the ring itself (drl_step_code_replay) -- no replay-add launch, and the code rows are not read back
+        if fuse_replay is None:
+            fuse_replay = input == "code" and not parallel
+        if fuse_replay and (input != "code" or parallel):
+            raise ValueError("fuse_replay needs input='code' and parallel=False")
+        self.fuse_replay = fuse_replay
         # parallel branches need 3 rotating buffers (see above); on one stream 2
         # suffice, and the third 77 MB observation buffer costs MALL hits (C3
         # loop 79.4 vs 74.4 us per step)
@@ -665,7 +672,10 @@ class TrainSegment:
                      actions=self.acts[b], synth=(2024, t) if self.fused else None)
         if before_step is not None:  # (parallel: the refill branch joins here)
             before_step()
-        if self.input == "code":
+        if self.fuse_replay:
+            self.env.step(self.acts[b], rewards=self.rewards[b], dones=self.dones[b], code=self.code[nb],
+                          replay=self.rb, replay_obs=self.code[b])
+        elif self.input == "code":
             self.env.step(self.acts[b], rewards=self.rewards[b], dones=self.dones[b], code=self.code[nb])
         else:
             self.env.step(self.acts[b], obs_k=1, rewards=self.rewards[b], dones=self.dones[b], obs=self.obs[nb],
@@ -686,7 +696,8 @@ class TrainSegment:
                 if not self.fused:
                     self._synth(t)
                 self._act_step(t)
-                self._replay(t)
+                if not self.fuse_replay:
+                    self._replay(t)
                 self._learn()
         else:
             ev_syn = [torch.cuda.Event() for _ in range(self.seg)]
@@ -805,7 +816,8 @@ def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fus
                                   "DESIGN.md section 6)"}
     branches = (("replay add_many" if fused else "synthetic actions and replay add_many") +
                 " on parallel graph branches, 3 rotating buffers" if parallel else "one stream") + \
-        ("; synthetic actions inside the act launch" if fused else "")
+        ("; synthetic actions inside the act launch" if fused else "") + \
+        ("; the replay add inside the step launch (drl_step_code_replay)" if loop.fuse_replay else "")
     return {"env_steps_per_s": E * seg * reps / dt, "us_per_step": dt / (seg * reps) * 1e6,
             "segments": reps, "steps_per_segment": seg, "precision": precision, "input": input,
             "learner": learner,

@@ -376,9 +376,48 @@ int32_t drl_policy_code_bytes(int32_t window_radius) {
     return drl::lay::code_bytes(2 * window_radius + 1);
 }
 
+static int step_code_impl(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
+                          uint8_t* d_dones, float* d_obs, int32_t obs_k, void* d_code, int32_t* d_err, uint32_t flags,
+                          hipStream_t stream, const drl::StepArgs* ring);
+
 int drl_step_code(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
                   uint8_t* d_dones, float* d_obs, int32_t obs_k, void* d_code, int32_t* d_err, uint32_t flags,
                   hipStream_t stream) {
+    return step_code_impl(p, s, d_actions, d_rewards, d_dones, d_obs, obs_k, d_code, d_err, flags, stream, nullptr);
+}
+
+int drl_step_code_replay(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
+                         uint8_t* d_dones, void* d_code, const void* d_code_prev, const drl_replay* r, int64_t cursor,
+                         int32_t* d_err, uint32_t flags, hipStream_t stream) {
+    if (!d_code || !d_code_prev) return fail("code and code_prev must be non-NULL");
+    if (d_code == d_code_prev) return fail("code_prev must be another buffer than code (the act's input rows)");
+    if ((uintptr_t)d_code_prev % 16) return fail("code_prev must be 16-byte aligned");
+    if (!r) return fail("replay is NULL");
+    if (!r->obs || !r->next_obs || !r->actions || !r->rewards || !r->dones) return fail("replay buffers are NULL");
+    if ((uintptr_t)r->obs % 16 || (uintptr_t)r->next_obs % 16) return fail("replay rows must be 16-byte aligned");
+    if (r->capacity < 1 || cursor < 0) return fail("replay capacity must be >= 1 and cursor >= 0");
+    if (!p) return fail("params is NULL");
+    const int32_t cb = drl_policy_code_bytes(p->window_radius);
+    if (cb < 0 || r->obs_floats * 4 != cb)
+        return fail("replay obs_floats %d must hold one policy code row (%d bytes)", r->obs_floats, cb);
+    drl::StepArgs ring;
+    memset(&ring, 0, sizeof ring);
+    const int64_t n = s ? s->num_envs : 0;
+    ring.ring_first = n > r->capacity ? n - r->capacity : 0;  // as drl_replay_add: earlier rows would be overwritten
+    ring.ring_cap = r->capacity;
+    ring.ring_base = (cursor % r->capacity + ring.ring_first % r->capacity) % r->capacity;
+    ring.ring_obs = reinterpret_cast<uint4*>(r->obs);
+    ring.ring_next = reinterpret_cast<uint4*>(r->next_obs);
+    ring.ring_act = r->actions;
+    ring.ring_rew = r->rewards;
+    ring.ring_done = r->dones;
+    ring.code_prev = static_cast<const uint4*>(d_code_prev);
+    return step_code_impl(p, s, d_actions, d_rewards, d_dones, nullptr, 0, d_code, d_err, flags, stream, &ring);
+}
+
+static int step_code_impl(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
+                          uint8_t* d_dones, float* d_obs, int32_t obs_k, void* d_code, int32_t* d_err, uint32_t flags,
+                          hipStream_t stream, const drl::StepArgs* ring) {
     drl_layout L;
     if (flags & ~(DRL_STEP_OBS_STREAM | DRL_STEP_REFILL)) return fail("unknown drl_step flags 0x%x", flags);
     if (validate(p, &L) || check_state(s, L)) return -1;
@@ -399,6 +438,17 @@ int drl_step_code(const drl_params* p, const drl_state* s, const int32_t* d_acti
     a.obs_nt = (flags & DRL_STEP_OBS_STREAM) ? 1 : 0;
     a.dones_packed = dones_packed(p, d_dones, 0, a);
     if (d_code && set_code(p, &a, d_code, L, d_obs != nullptr)) return -1;
+    if (ring) {
+        a.ring_obs = ring->ring_obs;
+        a.ring_next = ring->ring_next;
+        a.ring_act = ring->ring_act;
+        a.ring_rew = ring->ring_rew;
+        a.ring_done = ring->ring_done;
+        a.code_prev = ring->code_prev;
+        a.ring_first = ring->ring_first;
+        a.ring_base = ring->ring_base;
+        a.ring_cap = ring->ring_cap;
+    }
     hipError_t e = drl::launch_step(a, L.step_group_lanes, stream, drl::kStepMode);
     if (e != hipSuccess) return hip_fail(e, "drl_step launch");
     return (flags & DRL_STEP_REFILL) ? launch_refill(p, s, stream) : 0;

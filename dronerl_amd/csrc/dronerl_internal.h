@@ -181,6 +181,15 @@ struct StepArgs {
     int dones_packed; // 1: dones written as dwords (n_drones % 4 == 0, 4-B aligned rows and step strides)
     uint4* code;      // nullable: drone 0's policy code (lay::code_bytes(W) per env), written with the observation
     int code_lds;     // byte offset of the wave's code-row staging in its LDS (code non-NULL)
+    // drl_step_code_replay: the step's drone-0 transitions land in a replay ring (a fused drl_replay_add; code
+    // rows): env e (e >= ring_first) -> slot ring_base + e - ring_first (mod ring_cap); ring_next NULL: no ring
+    uint4* ring_obs;
+    uint4* ring_next;
+    int32_t* ring_act;
+    float* ring_rew;
+    uint8_t* ring_done;
+    const uint4* code_prev;  // the transitions' obs: the code rows the act read (not `code`)
+    int64_t ring_first, ring_base, ring_cap;
     uint32_t max_rounds;
     FastDiv div_side;
     ObsGeom og;

@@ -557,6 +557,86 @@ __device__ __forceinline__ uint16_t* code_row(const StepArgs& a, int64_t wenv0, 
     return reinterpret_cast<uint16_t*>(a.code) + wenv0 * (int64_t)(4 * lay::code_cpg8((int)g.W()));
 }
 
+// drl_step_code_replay: the ring slot of env e's transition (e >= ring_first;
+// e - ring_first < ring_cap, so one wrap at most) -- drl_replay_add's ring_slot
+template <class A>
+__device__ __forceinline__ int64_t step_ring_slot(const A& a, int64_t e) {
+    const int64_t s = a.ring_base + (e - a.ring_first);
+    return s >= a.ring_cap ? s - a.ring_cap : s;
+}
+
+// ... and its code rows: obs = the row the act read (code_prev), next_obs = the
+// row this step wrote (still in the wave's LDS staging, `cst`).  Streaming
+// stores, as drl_replay_add16_kernel: the ring is read back only by a later
+// sample.  VR = 16-B vectors per row; vector v = lane + 64 q of the wave's
+// rows (q < RQ) is loaded ahead into pre[q] (step_ring_prefetch), any past
+// 64 RQ (runtime windows wider than 9x9) are loaded in the sink.
+template <class A>
+__device__ __forceinline__ bool ring_vec(const A& a, int64_t wenv0, uint32_t v, uint32_t VR, int64_t* e,
+                                         uint32_t* col) {
+    const uint32_t el = v / VR;
+    *col = v - el * VR;
+    *e = wenv0 + el;
+    return *e >= a.ring_first;
+}
+
+template <int RQ, class A>
+__device__ __forceinline__ void step_ring_prefetch(const A& a, int64_t wenv0, int nenv_w, int lane, uint32_t VR,
+                                                   u32x4 (&pre)[RQ]) {
+    const uint32_t nv = (uint32_t)nenv_w * VR;
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {
+        const uint32_t v = (uint32_t)(lane + 64 * q);
+        int64_t e;
+        uint32_t col;
+        if (v < nv && ring_vec(a, wenv0, v, VR, &e, &col))
+            pre[q] = reinterpret_cast<const u32x4*>(a.code_prev)[e * VR + col];
+    }
+}
+
+// ... and the rows' scalars: drone index 0's action, reward and done, read
+// back from this wave's own rewards / dones stores (a one-wave workgroup: the
+// workgroup-scope fence orders them before the loads) -- the values held in
+// registers to here cost the step kernel spills.
+template <int RQ, class A>
+__device__ __forceinline__ void step_ring_sink(const A& a, int64_t wenv0, int nenv_w, int N, const l_u16* cst,
+                                               int lane, uint32_t VR, const u32x4 (&pre)[RQ]) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    if (lane < nenv_w) {
+        const int64_t e = wenv0 + lane;
+        if (e >= a.ring_first) {
+            const int64_t slot = step_ring_slot(a, e);
+            a.ring_act[slot] = a.actions[e * N];
+            a.ring_rew[slot] = a.rewards[e * N];
+            a.ring_done[slot] = a.dones[e * N];
+        }
+    }
+    const l_u4* cv = reinterpret_cast<const l_u4*>(cst);
+    const uint32_t nv = (uint32_t)nenv_w * VR;
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {
+        const uint32_t v = (uint32_t)(lane + 64 * q);
+        int64_t e;
+        uint32_t col;
+        if (v < nv && ring_vec(a, wenv0, v, VR, &e, &col)) {
+            const int64_t slot = step_ring_slot(a, e);
+            const u32x4 next = cv[v];
+            __builtin_nontemporal_store(next, reinterpret_cast<u32x4*>(a.ring_next) + slot * VR + col);
+            __builtin_nontemporal_store(pre[q], reinterpret_cast<u32x4*>(a.ring_obs) + slot * VR + col);
+        }
+    }
+    for (uint32_t v = (uint32_t)(lane + 64 * RQ); v < nv; v += 64) {
+        int64_t e;
+        uint32_t col;
+        if (!ring_vec(a, wenv0, v, VR, &e, &col)) continue;
+        const int64_t slot = step_ring_slot(a, e);
+        const u32x4 prev = reinterpret_cast<const u32x4*>(a.code_prev)[e * VR + col];
+        const u32x4 next = cv[v];
+        __builtin_nontemporal_store(next, reinterpret_cast<u32x4*>(a.ring_next) + slot * VR + col);
+        __builtin_nontemporal_store(prev, reinterpret_cast<u32x4*>(a.ring_obs) + slot * VR + col);
+    }
+}
+
 // Each drone paints its air byte into every observed window (drone indices
 // 0..K-1) that contains it.  posidx must be final.
 template <class GEO>
@@ -649,7 +729,9 @@ __device__ __forceinline__ void for_other_lanes(int v, F&& f) {
 // step t+1 are loaded during step t.  NT: streaming observation stores.
 // CODE: also write drone 0's policy code (a separate instance: the code
 // writer's registers would otherwise spill in the plain step at 64 VGPRs).
-template <int P, class GEO, bool ROLL, bool NT, bool CODE = false>
+// RING (with CODE): also land drone 0's transitions in a replay ring
+// (drl_step_code_replay, step_ring_sink).
+template <int P, class GEO, bool ROLL, bool NT, bool CODE = false, bool RING = false>
 __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     using GMask = typename GMaskT<P>::type;
     constexpr int GPW = 64 / P;
@@ -1246,6 +1328,14 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     }
     DRL_STAMP(5);
     if (GEO::kObs && (a.obs || (CODE && !ROLL))) {
+        // drl_step_code_replay: the arguments read where they are used (the kernarg segment), so the ring's
+        // pointers hold no registers through the step; the transitions' obs rows (code_prev) are loaded
+        // before the code is built, so their latency overlaps it
+        const StepArgs& ka = *(const StepArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+        constexpr int RQ = RING ? (GPW * (GEO::kW > 1 ? lay::code_cpg8((int)GEO::kW) / 2 : 12) + 63) / 64 : 1;
+        const uint32_t VR = (uint32_t)lay::code_cpg8((int)g.W()) / 2u;
+        [[maybe_unused]] u32x4 rpre[RQ];
+        if constexpr (RING) step_ring_prefetch<RQ>(ka, wenv0, nenv_w, lane, VR, rpre);
         if (active) paint_windows(W.paint + grp * g.lds_paint(), posidx, (int)py, (int)px,
                                   (uint8_t)((c + 1) | (carry << 7)), g);
         wave_sync();
@@ -1255,6 +1345,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
             l_u16* cst = reinterpret_cast<l_u16*>((l_u8*)smem + a.code_lds);
             if (a.obs) write_obs_wave<NT, true, true>(obase, nenv_w, g, W, a.obs_wide, lane, crow, cst);
             else write_obs_wave<NT, true, false>(obase, nenv_w, g, W, a.obs_wide, lane, crow, cst);
+            if constexpr (RING) step_ring_sink<RQ>(ka, wenv0, nenv_w, N, cst, lane, VR, rpre);
         } else {
             write_obs_wave<NT>(obase, nenv_w, g, W, a.obs_wide, lane);
         }
@@ -1297,10 +1388,12 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t orig, uint32_t n) {
 // latency hiding than the longer waves gain in balance.)
 // NT: streaming observation stores (DRL_STEP_OBS_STREAM).  CODE: with the
 // policy code (drl_step_code).
-template <int P, class GEO, bool NT, bool CODE = false>
+// RING: drl_step_code_replay (its own instance: the sink costs the plain
+// step's register allocation spills).
+template <int P, class GEO, bool NT, bool CODE = false, bool RING = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : 1, 8)))
 drl_step_kernel(StepArgs a) {
-    step_batch<P, GEO, false, NT, CODE>(a, (int64_t)xcd_block(blockIdx.x, gridDim.x) * (64 / P));
+    step_batch<P, GEO, false, NT, CODE, RING>(a, (int64_t)xcd_block(blockIdx.x, gridDim.x) * (64 / P));
 }
 
 // drl_rollout: a.steps steps per launch, same wave layout (P >= 16).
@@ -2323,6 +2416,8 @@ static hipError_t launch_step_t(const StepArgs& a, hipStream_t s, int mode) {
     } else if (mode == kRolloutMode) {
         if constexpr (P >= kRolloutNoObsMinLanes) hipLaunchKernelGGL((drl_rollout_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
         else return hipErrorInvalidValue;
+    } else if (GEO::kObs && a.code && a.ring_next) {  // drl_step_code_replay (no f32 observation)
+        hipLaunchKernelGGL((drl_step_kernel<P, GEO, false, GEO::kObs, GEO::kObs>), grid, block, a.wave_lds, s, a);
     } else if (GEO::kObs && a.code) {  // (obs NULL: the code alone)
         if (a.obs_nt) hipLaunchKernelGGL((drl_step_kernel<P, GEO, GEO::kObs, GEO::kObs>), grid, block, a.wave_lds, s, a);
         else hipLaunchKernelGGL((drl_step_kernel<P, GEO, false, GEO::kObs>), grid, block, a.wave_lds, s, a);

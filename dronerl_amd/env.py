@@ -158,7 +158,8 @@ class BatchedDeliveryDrones:
 
     def step(self, actions: torch.Tensor, obs_k: int = 0, rewards: Optional[torch.Tensor] = None,
              dones: Optional[torch.Tensor] = None, obs: Optional[torch.Tensor] = None,
-             obs_stream: Optional[bool] = None, code: Optional[torch.Tensor] = None):
+             obs_stream: Optional[bool] = None, code: Optional[torch.Tensor] = None, replay=None,
+             replay_obs: Optional[torch.Tensor] = None):
         """env.py:112-215 for every env.  actions int32 [E, N] by drone index.
 
         Returns (rewards f32 [E,N], dones bool-as-uint8 [E,N]) and, when
@@ -172,6 +173,13 @@ class BatchedDeliveryDrones:
         0's policy code after the step (drl_step_code), the input of a
         QNetwork(input="code"); with obs_k = 0 the code alone (no f32
         observation rows are written).
+        replay: a ReplayBuffer(code_radius=window_radius) and replay_obs the
+        code rows the act read (uint8 [E, policy_code_bytes], another buffer
+        than ``code``): the step also lands its drone-0 transitions
+        (replay_obs, actions[:, 0], rewards[:, 0], code, dones[:, 0]) in the
+        ring, exactly as a following ``replay.add_many`` would, in the same
+        launch (drl_step_code_replay; obs_k must be 0).  The batch
+        description is left in ``replay.last_batch``.
         """
         E, N = self.num_envs, self.n_drones
         actions = self._check(actions, torch.int32, (E, N), "actions")
@@ -197,6 +205,11 @@ class BatchedDeliveryDrones:
             if self._since_refill >= self.refill_every:
                 self._since_refill = 0
                 flags |= DRL_STEP_REFILL
+        if replay is not None:
+            if code is None or obs_k or replay_obs is None:
+                raise ValueError("replay= needs code= and replay_obs=, and obs_k=0")
+            replay._add_from_step(self, actions, rewards, dones, replay_obs, code, flags)
+            return rewards, dones
         check(lib().drl_step_code(ctypes.byref(self._cp), ctypes.byref(s), _ptr(actions), _ptr(rewards), _ptr(dones),
                                   _ptr(obs) if obs_k else None, int(obs_k), None if code is None else _ptr(code),
                                   _ptr(self.err), flags, _stream(self.device)), "drl_step")

@@ -438,6 +438,19 @@ int drl_replay_add(const drl_replay* r, int64_t cursor, int64_t n, const float* 
                    const float* d_next_obs, int64_t next_obs_stride, const int32_t* d_actions, int64_t action_stride,
                    const float* d_rewards, int64_t reward_stride, const uint8_t* d_dones, int64_t done_stride,
                    hipStream_t stream);
+/* drl_step_code (no f32 observation) fused with the drl_replay_add of the
+ * step's drone-0 transitions, code rows (replaces train_jax.py:55-62's
+ * env.step + buffer.add_many pair, jax_impl/buffers.py:57-80): env e lands
+ * in slot (cursor + e) % capacity with obs = d_code_prev row e (the rows the
+ * act read; another buffer than d_code), next_obs = the code this step
+ * writes to d_code, action = d_actions[e * n_drones], reward / done = drone
+ * index 0's.  The ring's contents equal drl_step_code + drl_replay_add(obs =
+ * d_code_prev, next_obs = d_code, action/reward/done column 0) bit for bit;
+ * r->obs_floats * 4 = drl_policy_code_bytes(window_radius), rows 16-byte
+ * aligned.  The caller advances cursor by num_envs. */
+int drl_step_code_replay(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
+                         uint8_t* d_dones, void* d_code, const void* d_code_prev, const drl_replay* r, int64_t cursor,
+                         int32_t* d_err, uint32_t flags, hipStream_t stream);
 
 
 /* drl_qnet_act / drl_qnet_act_code with epsilon read from device memory

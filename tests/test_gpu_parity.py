@@ -731,6 +731,38 @@ def test_train_segment_parallel_matches_serial():
         assert torch.equal(l0.net.packed, l1.net.packed), name
 
 
+def test_train_segment_code_fused_replay_matches_separate_add():
+    """bench.TrainSegment on policy codes: the step that lands its transitions
+    in the ring itself (drl_step_code_replay, the one-stream default) leaves
+    the same env state, ring, learner and packed net as the separate replay
+    add (one stream) and as the parallel branches (learner on fresh rows)."""
+    from bench import TrainSegment
+    p = EnvParams(n_drones=8, grid_size=16)
+    E, seg = 3000, 13
+    runs = []
+    for parallel, fuse in ((False, False), (False, True), (True, False)):
+        env = Env(p, E)
+        env.reset(seed=6)
+        loop = TrainSegment(env, seg, parallel=parallel, input="code", capacity=20000, fuse_replay=fuse)
+        assert loop.fuse_replay == fuse
+        loop.run()
+        loop.run()
+        torch.cuda.synchronize()
+        env.check_errors()
+        runs.append((gpu_state(env), loop))
+    g0, l0 = runs[0]
+    for name, (g1, l1) in zip(("fused replay", "parallel"), runs[1:]):
+        assert_state(g1, g0, f"{name} vs separate add")
+        for k in ("obs", "next_obs", "actions", "rewards", "dones"):
+            assert torch.equal(getattr(l0.rb, k), getattr(l1.rb, k)), (name, k)
+        assert l0.rb.cursor == l1.rb.cursor and l0.rb.size == l1.rb.size
+        for k in ("online", "target", "m", "v"):
+            for (w0, b0), (w1, b1) in zip(l0.learner.params(k), l1.learner.params(k)):
+                assert torch.equal(w0, w1) and torch.equal(b0, b1), (name, k)
+        assert l0.learner.counters() == l1.learner.counters(), name
+        assert torch.equal(l0.net.packed, l1.net.packed), name
+
+
 @pytest.mark.parametrize("kernel", list(RESET_KERNELS))
 @pytest.mark.parametrize("name", ["c1_g8_n4", "c3_g16_n8", "c4_g32_n16", "c5_g64_n32", "t_g5_n1", "t_g7_n2",
                                   "t_g11_n6", "t_g13_n8"])

@@ -297,3 +297,64 @@ def test_code_replay_buffer_samples_decode_to_obs_buffer():
     sc = rb_c.sample(256, generator=torch.Generator(device="cuda").manual_seed(9))
     for k in sf:
         assert torch.equal(sf[k], sc[k]), k
+
+
+@gpu
+@pytest.mark.parametrize("side,n,radius,E,cap,cursor0", [
+    (16, 8, 3, 4096, 10000, 0),      # the C3 geometry (compile-time instance), no wrap in the first steps
+    (16, 8, 3, 3000, 7001, 6000),    # the ring wraps inside a call
+    (16, 8, 3, 2000, 1500, 700),     # num_envs > capacity: only the last `capacity` envs land
+    (24, 5, 3, 777, 2000, 1999),     # runtime geometry, n_drones % 4 != 0 (byte dones)
+    (32, 16, 2, 333, 1000, 10),      # 5x5 window (64-B code rows)
+    (64, 32, 4, 129, 300, 250),      # 9x9 window (192-B rows), C5's grid
+])
+def test_step_code_replay_equals_step_then_add_many(side, n, radius, E, cap, cursor0):
+    """drl_step_code_replay (env.step(..., replay=rb, replay_obs=prev)): the
+    step's outputs and state and the whole ring -- obs, next_obs, actions,
+    rewards, dones, cursor, size -- equal drl_step_code followed by
+    drl_replay_add of the same transitions, bit for bit, over steps that wrap
+    the ring."""
+    from dronerl_amd.dqn import ReplayBuffer
+    D = (2 * radius + 1) ** 2 * 6
+    a, b = _env(side, n, radius, E, seed=11), _env(side, n, radius, E, seed=11)
+    ra_ = ReplayBuffer(cap, D, torch.device("cuda"), code_radius=radius)
+    rb_ = ReplayBuffer(cap, D, torch.device("cuda"), code_radius=radius)
+    for r in (ra_, rb_):
+        r.cursor = cursor0
+        for f in ("obs", "next_obs"):
+            getattr(r, f).fill_(0x5A)  # (stale rows: every landing row must be overwritten)
+    ca, cb = [a.new_code(), a.new_code()], [b.new_code(), b.new_code()]
+    a.get_obs(1, code=ca[0])
+    b.get_obs(1, code=cb[0])
+    for t in range(6):
+        acts = a.synth_actions(seed=8, step=t)
+        rw_a, dn_a = a.step(acts, code=ca[(t + 1) & 1], replay=ra_, replay_obs=ca[t & 1])
+        rw_b, dn_b = b.step(acts, code=cb[(t + 1) & 1])
+        rb_.add_many(cb[t & 1], acts, rw_b, cb[(t + 1) & 1], dn_b)
+        assert torch.equal(rw_a, rw_b) and torch.equal(dn_a, dn_b), t
+        assert torch.equal(ca[(t + 1) & 1], cb[(t + 1) & 1]), t
+        assert ra_.cursor == rb_.cursor and ra_.size == rb_.size, t
+        for f in ("obs", "next_obs", "actions", "rewards", "dones"):
+            assert torch.equal(getattr(ra_, f), getattr(rb_, f)), (t, f)
+        assert ra_.last_batch.n == E and ra_.last_batch.cursor == (cursor0 + t * E) % cap
+    for f in ("ground", "drones", "mt", "mt_index"):
+        assert torch.equal(getattr(a.state, f), getattr(b.state, f)), f
+    a.check_errors()
+
+
+@gpu
+def test_step_code_replay_argument_checks():
+    from dronerl_amd.dqn import ReplayBuffer
+    env = _env(16, 8, 3, 64)
+    rb = ReplayBuffer(100, 294, torch.device("cuda"), code_radius=3)
+    c0, c1 = env.new_code(), env.new_code()
+    acts = env.synth_actions(seed=1, step=0)
+    with pytest.raises(ValueError):  # the act's rows must be another buffer
+        env.step(acts, code=c0, replay=rb, replay_obs=c0)
+    with pytest.raises(ValueError):  # no f32 observation with the ring
+        env.step(acts, obs_k=1, code=c0, replay=rb, replay_obs=c1)
+    with pytest.raises(ValueError):  # a buffer of f32 rows
+        env.step(acts, code=c0, replay=ReplayBuffer(100, 294, torch.device("cuda")), replay_obs=c1)
+    with pytest.raises(ValueError):  # another window radius
+        env.step(acts, code=c0, replay=ReplayBuffer(100, 150, torch.device("cuda"), code_radius=2), replay_obs=c1)
+    assert rb.cursor == 0 and rb.size == 0
