@@ -20,6 +20,7 @@
  *   jax_impl/buffers.py:79-93      sample / can_sample,
  *   train_jax.py:68-98             the scan body's learner block   drl_dqn_train
  *   jax_impl/buffers.py:57-77      ReplayBuffer.add_many  drl_replay_add
+ *   train_jax.py:55-62             env.step + add_many    drl_step_code_replay (one launch)
  *
  * Two layers: stateless calls on caller-owned buffers (drl_reset, drl_step,
  * ...) and library-owned env handles (drl_env_*) that
