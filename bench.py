@@ -682,6 +682,8 @@ class TrainSegment:
                           obs_stream=LOOP_OBS_STREAM)  # None: env.step()'s default
 
     def _replay(self, t):
+        if self.fuse_replay:  # the step of _act_step(t) has added them (drl_step_code_replay)
+            return self.rb.last_batch
         b, nb = t % self.NB, (t + 1) % self.NB
         return self.rb.add_many(self.obs[b], self.acts[b], self.rewards[b], self.obs[nb], self.dones[b])
 
@@ -696,8 +698,7 @@ class TrainSegment:
                 if not self.fused:
                     self._synth(t)
                 self._act_step(t)
-                if not self.fuse_replay:
-                    self._replay(t)
+                self._replay(t)
                 self._learn()
         else:
             ev_syn = [torch.cuda.Event() for _ in range(self.seg)]

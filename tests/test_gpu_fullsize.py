@@ -174,6 +174,7 @@ def test_c3_code_train_loop_matches_oracle():
     loop = bench.TrainSegment(env, seg, precision="f32", input="code")  # the bench's own loop (one stream, fused)
     assert loop.input == "code" and loop.net.precision == "f32" and loop.rb.code_radius == 3
     assert loop.rb.capacity == 100_000 and loop.learner is not None
+    assert loop.fuse_replay  # the ring is written by the step itself (drl_step_code_replay; _replay is a no-op)
     lst, ohp = state_from_learner(loop.learner), oracle_hparams(loop.learner.hp)
     W = env.layout.obs_window
     want0 = o.obs(3, 1)[:, 0]
