@@ -125,6 +125,30 @@ def test_replay_add_rejects_short_rows():
     assert b"strides" in L.drl_last_error()
 
 
+def test_step_code_replay_validates_before_device_work():
+    """drl_step_code_replay (the step + add_many of its drone-0 transitions)
+    checks its ring and buffers before any device work (no GPU needed)."""
+    from dronerl_amd._native import DrlState
+    from dronerl_amd.dqn import DrlReplay, _bind
+    L = _bind(lib())
+    vp = ctypes.c_void_p
+    p = EnvParams(n_drones=8, grid_size=16).to_c()  # radius 3: 128-B code rows = 32 words
+    s = DrlState(vp(64), vp(64), vp(64), vp(64), 10)
+    good = DrlReplay(100, 32, 64, 64, 64, 64, 64)
+
+    def call(r, code=vp(1024), prev=vp(2048), cursor=0):
+        return L.drl_step_code_replay(ctypes.byref(p), ctypes.byref(s), vp(64), vp(64), vp(64), code, prev,
+                                      None if r is None else ctypes.byref(r), cursor, None, 0, None)
+    assert call(good, prev=None) != 0 and b"code_prev" in L.drl_last_error()
+    assert call(good, prev=vp(1024)) != 0 and b"another buffer" in L.drl_last_error()
+    assert call(good, prev=vp(2056)) != 0 and b"16-byte" in L.drl_last_error()
+    assert call(None) != 0 and b"replay is NULL" in L.drl_last_error()
+    assert call(DrlReplay(100, 32, 64, 64, 64, 64, None)) != 0 and b"NULL" in L.drl_last_error()
+    assert call(DrlReplay(100, 32, 72, 64, 64, 64, 64)) != 0 and b"aligned" in L.drl_last_error()
+    assert call(good, cursor=-1) != 0 and b"cursor" in L.drl_last_error()
+    assert call(DrlReplay(100, 294, 64, 64, 64, 64, 64)) != 0 and b"obs_floats" in L.drl_last_error()
+
+
 @pytest.mark.parametrize("val,ok", [("0", False), ("-3", False), ("x", False), ("", False), ("7", True)])
 def test_refill_cadence_override_must_be_positive(monkeypatch, val, ok):
     """DRL_REFILL_EVERY=0 used to mean "after every step" in C but
