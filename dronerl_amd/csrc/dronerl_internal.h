@@ -489,7 +489,15 @@ struct LearnArgs {
     QnetPack pack;
     int64_t wstart[QN_MAX_LAYERS + 1];  // the weights in set order: index of layer l's first; [L] = their total
     uint64_t* stamps;                   // DRL_DQN_STAMPS builds: [8 per workgroup (<= 64)][512 + last workgroup's]
+    // bounded waits: polls of a hand-off word / of a granule before a workgroup gives up (DqnCounters::pad[0])
+    uint32_t spin_word, spin_granule;
+    int drop_handoff;                   // debug knob (DRL_DQN_DEBUG_DROP_HANDOFF): the online tail omits the epoch word
 };
+constexpr uint32_t DQN_SPIN_WORD = 1u << 24, DQN_SPIN_GRANULE = 1u << 22;
+
+// co-residency of the learner's workgroups (they poll each other's hand-offs): how many can be resident at
+// once on this device with `lds` bytes of dynamic LDS each (occupancy x compute units)
+int dqn_train_resident_capacity(size_t lds, int num_cus);
 
 hipError_t launch_qnet_pack(const QnetPack& p, hipStream_t s);
 hipError_t launch_dqn_train(const LearnArgs& a, size_t lds_grad, hipStream_t s);

@@ -249,7 +249,9 @@ __device__ __forceinline__ float dq_load_sc1(const float* p) {
 
 // Granule hand-off (MI355X_MICROARCH.md / cdna_hip_programming.md Guideline 16, R2: the data is the flag):
 // one naturally aligned 8-byte {tag = epoch, value} written by one sc1 store; the reader polls it with sc1
-// loads until the tag is this step's epoch (never 0; the scratch starts zeroed).  No ticket, no drain.
+// loads until the tag is this step's epoch (never 0; drl_dqn_init zeroes the scratch).  No ticket, no drain.
+// A launch that gave up on a hand-off leaves pad[0] set, and every later launch then returns at once (see
+// the kernel's entry), so a stale granule of an aborted step (same epoch: step did not advance) is never read.
 typedef __attribute__((address_space(1))) uint64_t gu64;
 __device__ __forceinline__ void dq_granule_put(uint64_t* g, uint32_t epoch, float v) {
     __hip_atomic_store((gu64*)g, ((uint64_t)epoch << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
@@ -263,7 +265,7 @@ __device__ __forceinline__ bool dq_granule_get(const LearnArgs& a, const uint64_
             *v = __uint_as_float((uint32_t)x);
             return true;
         }
-        if (spins > (1u << 22)) {
+        if (spins > a.spin_granule) {
             a.ctr->pad[0] = 1;
             return false;
         }
@@ -424,7 +426,7 @@ __device__ __forceinline__ bool dq_wait(const LearnArgs& a, int32_t* word, uint3
     uint32_t spins = 0;
     while (__hip_atomic_load((gu32*)word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
         __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1u << 24)) {
+        if (++spins > a.spin_word) {
             a.ctr->pad[0] = 1;
             return false;
         }
@@ -516,6 +518,9 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
             w0r[q] = e < nw0 ? ((gcf32*)src)[e] : 0.0f;
         }
     }
+    // a learner whose block carries the timeout flag does nothing until drl_dqn_init clears it: the aborted
+    // launch left granules tagged with this step's epoch and the arrive ticket part-counted
+    if (__hip_atomic_load((gu32*)&a.ctr->pad[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
     // the counters as this step starts (the online tail writes them at the end)
     DqnCounters ctr;
     ctr.step = a.ctr->step;
@@ -931,7 +936,8 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
     // hand the deltas and activations over: every wave drains, the barrier, the epoch word
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_store((gu32*)&a.ctr->pad[2], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0 && !a.drop_handoff)
+        __hip_atomic_store((gu32*)&a.ctr->pad[2], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     DQ_STAMP(6);
 #ifdef DRL_DQN_STAMPS
     if (threadIdx.x == 0) {
@@ -992,6 +998,13 @@ hipError_t launch_dqn_train(const LearnArgs& a, size_t lds, hipStream_t s) {
     else
         hipLaunchKernelGGL(drl_dqn_train_kernel, dim3(1), dim3(DQN_THREADS), 0, s, a);
     return hipGetLastError();
+}
+
+int dqn_train_resident_capacity(size_t lds, int num_cus) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, drl_dqn_train_kernel, DQN_THREADS, lds) != hipSuccess)
+        return -1;
+    return per_cu * num_cus;
 }
 
 hipError_t launch_dqn_init(void* counters, float epsilon, hipStream_t s) {

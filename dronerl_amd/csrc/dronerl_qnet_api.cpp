@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -131,6 +132,20 @@ int num_cus() {
     return cache[dev];
 }
 
+
+// drl::dqn_train_resident_capacity per (device, LDS bytes), queried once
+static int dqn_resident_capacity(size_t lds) {
+    static std::mutex mu;
+    static std::vector<std::pair<std::pair<int, size_t>, int>> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    std::lock_guard<std::mutex> g(mu);
+    for (const auto& c : cache)
+        if (c.first.first == dev && c.first.second == lds) return c.second;
+    const int cap = drl::dqn_train_resident_capacity(lds, num_cus());
+    if (cap >= 0) cache.push_back({{dev, lds}, cap});
+    return cap;
+}
 
 // The agent block of a learner (include/dronerl.h drl_dqn_layout), the scratch
 // regions of drl::LearnArgs, and the gradient launch's LDS.
@@ -521,6 +536,11 @@ int drl_dqn_init(const drl_qnet_desc* d, int32_t batch, void* d_agent, float eps
     const size_t set = (size_t)P.pub.n_params * 4;
     if (hipError_t e = hipMemsetAsync(base + P.pub.m_off, 0, 2 * set, stream); e != hipSuccess)
         return hip_fail(e, "drl_dqn_init moments");
+    // the whole scratch: the hand-off granules' tags must not match a later epoch (a block from hipMalloc,
+    // or one that has trained already)
+    if (hipError_t e = hipMemsetAsync(base + P.pub.scratch_off, 0, (size_t)(P.pub.bytes - P.pub.scratch_off), stream);
+        e != hipSuccess)
+        return hip_fail(e, "drl_dqn_init scratch");
     // each weight's element in the act kernels' packed image (qnet_pack_elem, once: the learner reads it)
     std::vector<uint32_t> px((size_t)P.pub.n_params, 0u);
     for (int l = 0; l < L.n_layers; ++l)
@@ -562,9 +582,27 @@ static int dqn_train_impl(const drl_qnet_desc* d, const drl_dqn_hparams* h, void
         return fail("replay obs_floats < in_features");
     }
     if ((uintptr_t)r->obs % 4 || (uintptr_t)r->next_obs % 4) return fail("replay rows must be 4-byte aligned");
+    if (size >= h->batch) {  // the workgroups poll each other's hand-offs: all of them must fit at once
+        const int cap = dqn_resident_capacity(P.lds);
+        if (cap < 0) return fail("drl_dqn_train: the occupancy query failed");
+        if (cap < P.pub.grad_workgroups) {
+            char buf[160];
+            snprintf(buf, sizeof buf, "drl_dqn_train needs %d co-resident workgroups (%zu B of LDS each); "
+                     "this device holds %d", P.pub.grad_workgroups, P.lds, cap);
+            return fail(buf);
+        }
+    }
     uint8_t* base = static_cast<uint8_t*>(d_agent);
     drl::LearnArgs a;
     memset(&a, 0, sizeof a);
+    a.spin_word = drl::DQN_SPIN_WORD;
+    a.spin_granule = drl::DQN_SPIN_GRANULE;
+    if (const char* v = getenv("DRL_DQN_DEBUG_DROP_HANDOFF"); v && v[0] == '1') {
+        // (diagnostic, tests only: the target side's layer-0 workgroups then give up after a short wait)
+        a.drop_handoff = 1;
+        a.spin_word = 1u << 12;
+        a.spin_granule = 1u << 12;
+    }
     a.n_layers = L.n_layers;
     a.batch = h->batch;
     a.code_w = L.code_w;

@@ -149,10 +149,8 @@ class QNetwork:
         sizes = [in_features, *self.hidden, n_actions]
         self.weights, self.biases = [], []
         for i in range(len(sizes) - 1):
-            fan_in = sizes[i]
-            # he_normal for the hidden layers (dqn.py:53), lecun-normal-like for the output
-            std = (2.0 / fan_in) ** 0.5 if i < len(sizes) - 2 else (1.0 / fan_in) ** 0.5
-            w = torch.randn((sizes[i + 1], fan_in), generator=generator) * std
+            # he_normal for the hidden layers (dqn.py:53), flax Dense's lecun_normal for the output
+            w = flax_kernel_init((sizes[i + 1], sizes[i]), 2.0 if i < len(sizes) - 2 else 1.0, generator)
             self.weights.append(w.to(self.device))
             self.biases.append(torch.zeros(sizes[i + 1], device=self.device))
         self.desc = DrlQnetDesc(in_features, len(self.hidden), (ctypes.c_int32 * 3)(*self.hidden, *[0] * (3 - len(self.hidden))),
@@ -424,6 +422,15 @@ class ReplayBuffer:
                     next_obs=next_obs, dones=self.dones[idx])
 
 
+def flax_kernel_init(shape, scale: float, generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    """flax's variance_scaling(scale, "fan_in", "truncated_normal") for a torch-layout [out][in] weight:
+    he_normal (scale 2, the hidden layers, jax dqn.py:54) and Dense's default lecun_normal (scale 1, the output
+    layer, :56) -- a normal truncated at +-2 standard deviations, its deviation divided by .87962566103423978
+    (the truncated unit normal's) so the variance is scale / fan_in."""
+    std = (scale / shape[1]) ** 0.5 / .87962566103423978
+    return torch.nn.init.trunc_normal_(torch.empty(shape), 0.0, std, -2.0 * std, 2.0 * std, generator=generator)
+
+
 @dataclass
 class DQNHParams:
     """The learner's hyperparameters: jax_impl/agents/dqn.py DQNAgentParams
@@ -470,7 +477,8 @@ class DQNLearner:
 
     target: the target net's initial (weights, biases) (torch layout); the
     reference initialises it from its own key (dqn.py:119-121), so by default
-    it is a fresh random init from `generator`."""
+    it is a fresh init from `generator` with the reference's initialisers
+    (flax_kernel_init; zero biases)."""
 
     def __init__(self, net: QNetwork, hp: Optional[DQNHParams] = None, target=None,
                  generator: Optional[torch.Generator] = None):
@@ -494,10 +502,7 @@ class DQNLearner:
         shapes = [(w.shape, b.shape) for w, b in zip(net.weights, net.biases)]
         if target is None:
             g = generator if generator is not None else torch.Generator().manual_seed(1)
-            tw = []
-            for ws, _ in shapes:
-                std = (2.0 / ws[1]) ** 0.5 if len(tw) < len(shapes) - 1 else (1.0 / ws[1]) ** 0.5
-                tw.append(torch.randn(ws, generator=g) * std)
+            tw = [flax_kernel_init(ws, 2.0 if l < len(shapes) - 1 else 1.0, g) for l, (ws, _) in enumerate(shapes)]
             target = (tw, [torch.zeros(bs) for _, bs in shapes])
         for l, (ws, bs) in enumerate(shapes):
             self.params("online")[l][0].copy_(net.weights[l])
@@ -542,9 +547,22 @@ class DQNLearner:
 
     def check_errors(self):
         """Synchronise; raise if a learner launch gave up waiting for one of
-        its hand-offs (a hardware-scheduling fault, never expected)."""
+        its hand-offs (a hardware-scheduling fault, never expected).  From
+        that launch on every drl_dqn_train returns without touching the
+        block (the learner is frozen, not silently corrupted) until
+        restart()."""
         if int(self._ctr_i[13].item()):
-            raise DroneRLError("drl_dqn_train: a workgroup timed out waiting for another workgroup's hand-off")
+            raise DroneRLError("drl_dqn_train: a workgroup timed out waiting for another workgroup's hand-off; "
+                               "the learner refuses to train until restart()")
+
+    def restart(self, epsilon: Optional[float] = None):
+        """drl_dqn_init on the current parameters: Adam's moments and the
+        counters from zero (step 0, epsilon `epsilon` or hp.epsilon_start),
+        the scratch zeroed, a timeout flag cleared.  The online and target
+        parameters are kept."""
+        eps = self.hp.epsilon_start if epsilon is None else float(epsilon)
+        _check(self.L, self.L.drl_dqn_init(ctypes.byref(self.net.desc), self.hp.batch, _vp(self.block.data_ptr()),
+                                           eps, _stream(self.block.device)))
 
     def counters(self) -> dict:
         """Host copy of the device counters (synchronises)."""

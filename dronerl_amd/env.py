@@ -200,19 +200,24 @@ class BatchedDeliveryDrones:
         if obs_stream is None:
             obs_stream = self.default_obs_stream
         flags = DRL_STEP_OBS_STREAM if obs_stream else 0
+        # the refill cadence advances only once the launch is accepted: a call refused by the checks below
+        # (or by the library) leaves the env exactly as it was
+        since = self._since_refill
         if self.refill_every > 0:
-            self._since_refill += 1
-            if self._since_refill >= self.refill_every:
-                self._since_refill = 0
+            since += 1
+            if since >= self.refill_every:
+                since = 0
                 flags |= DRL_STEP_REFILL
         if replay is not None:
             if code is None or obs_k or replay_obs is None:
                 raise ValueError("replay= needs code= and replay_obs=, and obs_k=0")
             replay._add_from_step(self, actions, rewards, dones, replay_obs, code, flags)
+            self._since_refill = since
             return rewards, dones
         check(lib().drl_step_code(ctypes.byref(self._cp), ctypes.byref(s), _ptr(actions), _ptr(rewards), _ptr(dones),
                                   _ptr(obs) if obs_k else None, int(obs_k), None if code is None else _ptr(code),
                                   _ptr(self.err), flags, _stream(self.device)), "drl_step")
+        self._since_refill = since
         if obs_k:
             return rewards, dones, obs
         return rewards, dones

@@ -525,16 +525,23 @@ typedef struct drl_dqn_layout {
 } drl_dqn_layout;
 
 int drl_dqn_layout_query(const drl_qnet_desc* d, int32_t batch, drl_dqn_layout* layout);
-/* Zero the Adam moments and the counters, epsilon = epsilon_start
- * (dqn.py:116-130: optax.adam's init, epsilon_start).  The caller writes the
- * online and target parameters (the reference initialises them from
- * different keys, dqn.py:114-121). */
+/* Zero the Adam moments, the counters (a timeout flag included) and the whole
+ * scratch (the hand-off granules must start untagged, whether the block comes
+ * from hipMalloc or has trained before), epsilon = epsilon_start (dqn.py:116-130:
+ * optax.adam's init, epsilon_start).  The caller writes the online and target
+ * parameters (the reference initialises them from different keys,
+ * dqn.py:114-121).  Synchronises `stream` (a host table is uploaded). */
 int drl_dqn_init(const drl_qnet_desc* d, int32_t batch, void* d_agent, float epsilon_start, hipStream_t stream);
 /* One learner step on replay `r` holding `size` transitions (current_size,
  * 0 <= size <= capacity).  The replay's rows: f32 observations (obs_floats >=
  * in_features) for a DRL_QNET_INPUT_OBS net, policy code rows
  * (drl_policy_code_bytes / 4 words) for a DRL_QNET_INPUT_CODE one.  d_packed:
- * the online net's packed image (drl_qnet_pack of the online set). */
+ * the online net's packed image (drl_qnet_pack of the online set).
+ * The launch's grad_workgroups poll each other's hand-offs, so they must be
+ * co-resident: the call fails (-1) on a device that cannot hold them all at
+ * once (e.g. a 32-CU partition).  A workgroup that gives up on a hand-off
+ * (a bounded wait) sets internal[5] of the counters; from then on every call
+ * returns on the device without touching the block, until drl_dqn_init. */
 int drl_dqn_train(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agent, void* d_packed,
                   const struct drl_replay* r, int64_t size, hipStream_t stream);
 /* A drl_replay_add batch (its arguments; strides in elements, obs strides in

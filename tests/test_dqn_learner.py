@@ -419,6 +419,64 @@ def test_learner_fresh_batch_equals_serial(cap, E):
 
 
 @gpu
+def test_learner_handoff_timeout_is_reported_and_refused(monkeypatch):
+    """a launch whose workgroup gives up on a hand-off sets the
+    error flag; DQNLearner.check_errors raises; every later launch returns at
+    once (parameters, moments, packed image and counters frozen: an aborted
+    step's stale granules carry the same epoch and are never read); restart()
+    (drl_dqn_init) zeroes the scratch and clears the flag, and training then
+    matches the oracle again.  The hand-off is dropped with the debug knob
+    DRL_DQN_DEBUG_DROP_HANDOFF (the online tail omits the epoch word)."""
+    from dronerl_amd.handle import DroneRLError
+    env, net, learner, rb, hp = _learner_setup((294, 128, 64, 5), "code", dict(batch=8), E=64, cap=300)
+    cur, nxt = env.new_code(), env.new_code()
+    env.get_code(out=cur)
+    acts = torch.empty((64, 8), dtype=torch.int32, device="cuda")
+
+    def fill(t):
+        net.act(cur, learner.epsilon, seed=3, step=t, actions=acts, synth=(5, t))
+        r, d = env.step(acts, code=nxt)
+        rb.add_many(cur, acts, r, nxt, d)
+        cur.copy_(nxt)
+
+    fill(0)
+    learner.train(rb)
+    torch.cuda.synchronize()
+    learner.check_errors()
+    monkeypatch.setenv("DRL_DQN_DEBUG_DROP_HANDOFF", "1")
+    learner.train(rb)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("DRL_DQN_DEBUG_DROP_HANDOFF")
+    with pytest.raises(DroneRLError):
+        learner.check_errors()
+    frozen = learner.block.clone()
+    packed = net.packed.clone()
+    for t in range(1, 4):
+        fill(t)
+        learner.train(rb)
+    torch.cuda.synchronize()
+    assert torch.equal(learner.block, frozen) and torch.equal(net.packed, packed)
+    with pytest.raises(DroneRLError):
+        learner.check_errors()
+    # restart: counters from zero, the flag cleared, the granules zeroed; then bit-exact training again
+    learner.restart()
+    torch.cuda.synchronize()
+    lay = learner.layout
+    assert int(learner.block[lay.counters_off + 52:lay.counters_off + 56].view(torch.int32).item()) == 0
+    learner.check_errors()
+    st, ohp = state_from_learner(learner), oracle_hparams(hp)
+    assert st.step == 0 and st.count == 0
+    for t in range(4, 9):
+        fill(t)
+        O.learner_step(st, ohp, _host(rb.obs), _host(rb.next_obs), _host(rb.actions), _host(rb.rewards),
+                       _host(rb.dones), rb.size, 7)
+        learner.train(rb)
+        torch.cuda.synchronize()
+        assert_same(learner, st, f"after restart, step {t}")
+    learner.check_errors()
+
+
+@gpu
 @pytest.mark.parametrize("inp", ["code", "obs"])
 def test_learner_matches_torch_restatement_50_steps(inp):
     """VERDICT r4 item 1's check: 50 device learner steps (train_jax defaults:

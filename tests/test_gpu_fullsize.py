@@ -17,12 +17,15 @@
    by the kernel's actions; env state, rewards, dones and the observation are
    compared every step, and the replay ring at the end against the ring the
    oracle's transitions give.
-3. The exact loop bench.py times (`train_loop`): C3 at
-   65,536 envs, f32 nets on drone 0's policy code, a code-row replay buffer,
-   bench.TrainSegment's own calls, 100 steps, then its reset.  The oracle is
-   driven by the kernel's actions; every step compares rewards, dones and the
-   code the step wrote (decoded on the host) with the oracle's observation,
-   the state every 10 steps; the act's Q on the step's code against an f32
+3. The exact loops bench.py times (`train_loop` and `c5.train_loop`): C3 at
+   65,536 envs on the 100,000-slot ring, and C5's 64x64 / 32-drone compile-time
+   instance with more envs than ring slots (8,192 into 5,000, the regime of
+   131,072 into 100,000); f32 nets on drone 0's policy code, the fused replay
+   add, the device learner, bench.TrainSegment's own calls, then its reset.
+   The oracle is driven by the kernel's actions; every step compares rewards,
+   dones and the code the step wrote (decoded on the host) with the oracle's
+   observation, and the learner with oracle/dqn_learner.py bit for bit; the
+   state every 10 steps; the act's Q on the step's code against an f32
    forward of the oracle's observation; the code ring and sample()'s decoded
    rows against the oracle's transitions; the reset's state and first code.
 """
@@ -156,24 +159,31 @@ def test_c5_train_loop_segment_matches_oracle(E, seg):
     np.testing.assert_array_equal(env.get_obs(1).cpu().numpy(), o.obs(3, 1), err_msg="C5 loop reset obs")
 
 
-def test_c3_code_train_loop_matches_oracle():
-    """bench.TrainSegment's own calls at C3 (65,536 envs x 100 steps): the
-    env against the env oracle every step, the act against an f32 forward of
-    the live (learning) net, the learner (drl_dqn_train on the reference's
-    100,000-slot ring, train_jax.py:173) against oracle/dqn_learner.py bit for
-    bit every step, the code ring, sample() and the reset."""
+@pytest.mark.parametrize("name,G,N,E,seg,cap", [
+    ("C3", 16, 8, 65536, 100, 100_000),   # the bench's train_loop: 65,536 envs, the reference's 100,000-slot ring
+    # the bench's c5.train_loop instance (drl_step_kernel<32, Geo<64,32,3,1>, ..., fused replay>) in its
+    # E > capacity regime (131,072 envs into 100,000 slots there)
+    ("C5", 64, 32, 8192, 40, 5000),
+])
+def test_code_train_loop_matches_oracle(name, G, N, E, seg, cap):
+    """bench.TrainSegment's own calls (C3: 65,536 envs x 100 steps; C5's
+    64x64 / 32-drone instance with more envs than ring slots): the env against
+    the env oracle every step, the act against an f32 forward of the live
+    (learning) net, the learner (drl_dqn_train; train_jax.py:173 ring) against
+    oracle/dqn_learner.py bit for bit every step, the code ring, sample() and
+    the reset."""
     import bench
     from tests.test_dqn_learner import assert_same, oracle_hparams, oracle_step_on_ring, state_from_learner
     from tests.test_policy_code import decode_code
-    E, seg, N = 65536, 100, 8
-    p = EnvParams(n_drones=N, grid_size=16)
+    p = EnvParams(n_drones=N, grid_size=G)
     env = Env(p, E)
     env.reset(seed=5)
     o = OracleMulti(oparams(p), E)
     o.reset(5 + np.arange(E))
-    loop = bench.TrainSegment(env, seg, precision="f32", input="code")  # the bench's own loop (one stream, fused)
+    # the bench's own loop (one stream, fused act + fused replay add)
+    loop = bench.TrainSegment(env, seg, precision="f32", input="code", capacity=cap)
     assert loop.input == "code" and loop.net.precision == "f32" and loop.rb.code_radius == 3
-    assert loop.rb.capacity == 100_000 and loop.learner is not None
+    assert loop.rb.capacity == cap and loop.learner is not None
     assert loop.fuse_replay  # the ring is written by the step itself (drl_step_code_replay; _replay is a no-op)
     lst, ohp = state_from_learner(loop.learner), oracle_hparams(loop.learner.hp)
     W = env.layout.obs_window
@@ -188,14 +198,14 @@ def test_c3_code_train_loop_matches_oracle():
         loop._act_step(t)
         loop._replay(t)
         info = oracle_step_on_ring(lst, ohp, loop.rb, W)
-        assert info["trained"]  # 65,536 transitions from the first step on: can_sample
+        assert info["trained"]  # E >= batch transitions from the first step on: can_sample
         loop._learn()
-        assert_same(loop.learner, lst, f"C3 learner step {t}")
+        assert_same(loop.learner, lst, f"{name} learner step {t}")
         a = loop.acts[b].cpu().numpy()
         np.testing.assert_array_equal(a[:, 1:], env.synth_actions(seed=2024, step=t).cpu().numpy()[:, 1:])
         assert ((a[:, 0] >= 0) & (a[:, 0] < 5)).all()
         ro, do = o.step(a, nthreads=THREADS)
-        ctx = f"C3 code loop step {t}"
+        ctx = f"{name} code loop step {t}"
         assert_rewards(loop.rewards[b].cpu().numpy(), ro, ctx)
         np.testing.assert_array_equal(loop.dones[b].cpu().numpy().astype(bool), do, err_msg=ctx)
         nxt = o.obs(3, 1)[:, 0]
@@ -205,7 +215,7 @@ def test_c3_code_train_loop_matches_oracle():
             raise AssertionError(f"{ctx}: code differs from the oracle's observation in envs {bad[:10]}")
         if t % 10 == 9:
             assert_state(gpu_state(env), o.state(), ctx)
-        if t in (0, 57, seg - 1):  # the act on the step's code == an f32 forward of the oracle's observation
+        if t in (0, seg // 2 + 7, seg - 1):  # the act on the step's code == an f32 forward of the oracle's observation
             q = torch.empty((E, 5), device=env.device)
             tmp = torch.empty((E, 1), dtype=torch.int32, device=env.device)
             loop.net.act(loop.code[nb], 0.0, actions=tmp, q_out=q)
@@ -250,5 +260,5 @@ def test_c3_code_train_loop_matches_oracle():
     env.reset(seed=None)
     loop._first_obs()
     o.reset(None)
-    assert_state(gpu_state(env), o.state(), "C3 code loop reset")
+    assert_state(gpu_state(env), o.state(), f"{name} code loop reset")
     assert np.array_equal(decode_code(loop.code[0].cpu().numpy(), W), o.obs(3, 1)[:, 0]), "reset code"

@@ -307,6 +307,7 @@ def test_code_replay_buffer_samples_decode_to_obs_buffer():
     (24, 5, 3, 777, 2000, 1999),     # runtime geometry, n_drones % 4 != 0 (byte dones)
     (32, 16, 2, 333, 1000, 10),      # 5x5 window (64-B code rows)
     (64, 32, 4, 129, 300, 250),      # 9x9 window (192-B rows), C5's grid
+    (64, 32, 3, 6000, 5000, 4500),   # the C5 compile-time instance with num_envs > capacity (c5.train_loop)
 ])
 def test_step_code_replay_equals_step_then_add_many(side, n, radius, E, cap, cursor0):
     """drl_step_code_replay (env.step(..., replay=rb, replay_obs=prev)): the
@@ -349,12 +350,15 @@ def test_step_code_replay_argument_checks():
     rb = ReplayBuffer(100, 294, torch.device("cuda"), code_radius=3)
     c0, c1 = env.new_code(), env.new_code()
     acts = env.synth_actions(seed=1, step=0)
+    since = env._since_refill = env.refill_every - 1  # a refused call must not consume the refill cadence
     with pytest.raises(ValueError):  # the act's rows must be another buffer
         env.step(acts, code=c0, replay=rb, replay_obs=c0)
+    assert env._since_refill == since
     with pytest.raises(ValueError):  # no f32 observation with the ring
         env.step(acts, obs_k=1, code=c0, replay=rb, replay_obs=c1)
     with pytest.raises(ValueError):  # a buffer of f32 rows
         env.step(acts, code=c0, replay=ReplayBuffer(100, 294, torch.device("cuda")), replay_obs=c1)
     with pytest.raises(ValueError):  # another window radius
         env.step(acts, code=c0, replay=ReplayBuffer(100, 150, torch.device("cuda"), code_radius=2), replay_obs=c1)
+    assert env._since_refill == since and rb.cursor == 0 and rb.size == 0
     assert rb.cursor == 0 and rb.size == 0
