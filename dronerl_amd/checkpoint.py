@@ -15,7 +15,9 @@ ast.literal_eval, as the reference does.  `TorchQNetwork` rebuilds the
 reference module (same nn.Sequential names, so state dicts load unchanged)
 and its forward: dense nets flatten [B, H, W, C] row-major; conv nets permute
 to [B, C, H, W] first (dqn.py:80-81, 153-159).  `to_qnet` moves a dense net
-onto the MFMA consumer (dronerl_amd.dqn.QNetwork) when its widths allow.
+onto the MFMA consumer (dronerl_amd.dqn.QNetwork) when its widths allow;
+`save_dense` writes a (device-trained) dense net in the reference's three
+on-disk forms (jax save / save_as_torch, torch DQNAgent.save).
 """
 from __future__ import annotations
 
@@ -149,6 +151,59 @@ def save_checkpoint(path: str, net: TorchQNetwork, conv_layers=None, dense_layer
             conv_layers = tuple(_conv_meta(m) for m in net.network.children() if isinstance(m, nn.Conv2d))
         md["conv_layers"] = str(tuple(conv_layers))
     save_file(sd, path, metadata=md)
+
+
+# train_jax.py:366 --conv_layers default (its JSON key order), which save / save_as_torch write for dense nets too
+TRAIN_JAX_CONV_LAYERS = ({"kernel_size": 3, "out_channels": 8, "padding": 1, "stride": 1},)
+CHECKPOINT_FORMATS = ("torch", "jax", "torch_agent")
+
+
+def save_dense(path: str, weights, biases, obs_shape, format: str = "torch", conv_layers=TRAIN_JAX_CONV_LAYERS,
+               conv_dense_layers=(), checkpoint_format_version: float = 0.1):
+    """Write a dense Q-network (weights [out][in] / biases, torch layout, any
+    tensors or arrays) as the reference writes a trained agent:
+
+    * "torch": jax_impl/agents/dqn.py:301-357 save_as_torch (what train_jax.py:
+      242-244 writes as agent_<n>_steps_torch.safetensors): network.dense_{i}
+      .weight [out][in] / .bias (i from 1) and the metadata network_type,
+      dense_layers, conv_dense_layers, conv_layers, obs_shape, action_shape,
+      checkpoint_format "torch", checkpoint_format_version;
+    * "jax": dqn.py:282-299 save (agent_<n>_steps_jax.safetensors):
+      params.Dense_{i}.kernel [in][out] / .bias (i from 0), the same
+      metadata keys with checkpoint_format "jax";
+    * "torch_agent": torch_impl/agents/dqn.py:330-345 DQNAgent.save: the torch
+      names and only network_type, dense_layers, obs_shape, action_shape.
+
+    Every string is the reference's str() of the same Python value, so
+    ast.literal_eval in either loader reads it back."""
+    from safetensors.numpy import save_file
+    if format not in CHECKPOINT_FORMATS:
+        raise ValueError(f"format must be one of {CHECKPOINT_FORMATS}")
+    ws = [np.ascontiguousarray(np.asarray(w.detach().cpu() if torch.is_tensor(w) else w, dtype=np.float32))
+          for w in weights]
+    bs = [np.ascontiguousarray(np.asarray(b.detach().cpu() if torch.is_tensor(b) else b, dtype=np.float32))
+          for b in biases]
+    if not ws or len(ws) != len(bs) or any(w.ndim != 2 or b.shape != (w.shape[0],) for w, b in zip(ws, bs)):
+        raise ValueError("weights [out][in] and biases [out], one pair per layer")
+    if ws[0].shape[1] != int(np.prod(obs_shape)) or any(ws[i + 1].shape[1] != ws[i].shape[0] for i in range(len(ws) - 1)):
+        raise ValueError("layer widths do not chain from the observation size")
+    hidden = tuple(int(w.shape[0]) for w in ws[:-1])
+    md = {"network_type": "dense", "dense_layers": str(hidden), "obs_shape": str(tuple(int(v) for v in obs_shape)),
+          "action_shape": str((int(ws[-1].shape[0]),))}
+    if format == "torch_agent":
+        t = {}
+        for i, (w, b) in enumerate(zip(ws, bs)):
+            t[f"network.dense_{i + 1}.weight"], t[f"network.dense_{i + 1}.bias"] = w, b
+    else:
+        md.update({"conv_layers": str(tuple(conv_layers)), "conv_dense_layers": str(tuple(conv_dense_layers)),
+                   "checkpoint_format": format, "checkpoint_format_version": str(checkpoint_format_version)})
+        t = {}
+        for i, (w, b) in enumerate(zip(ws, bs)):
+            if format == "jax":
+                t[f"params.Dense_{i}.kernel"], t[f"params.Dense_{i}.bias"] = np.ascontiguousarray(w.T), b
+            else:
+                t[f"network.dense_{i + 1}.weight"], t[f"network.dense_{i + 1}.bias"] = w, b
+    save_file(t, path, metadata=md)
 
 
 def to_qnet(ck: Checkpoint, device=None):

@@ -502,6 +502,7 @@ int dqn_train_resident_capacity(size_t lds, int num_cus);
 hipError_t launch_qnet_pack(const QnetPack& p, hipStream_t s);
 hipError_t launch_dqn_train(const LearnArgs& a, size_t lds_grad, hipStream_t s);
 hipError_t launch_dqn_init(void* counters, float epsilon, hipStream_t s);
+hipError_t launch_dqn_sample(const void* counters, uint64_t seed, int batch, int64_t size, int64_t* out, hipStream_t s);
 hipError_t launch_qnet_act(const QnetArgs& a, int num_cus, hipStream_t s);
 hipError_t launch_qnet_act_code(const QnetArgs& a, int window, int num_cus, hipStream_t s);
 hipError_t launch_replay_add(const ReplayArgs& a, hipStream_t s);

@@ -975,6 +975,13 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
     if (s_flag) dq_finish(a, ctr, 1, loss, bc1, bc2);
 }
 
+// The replay slots the next drl_dqn_train launch samples (its step counter as it stands on the stream):
+// the same dq_sample draws, for a caller that gathers those rows first (the sharded global learner)
+__global__ void drl_dqn_sample_kernel(const DqnCounters* c, uint64_t seed, int batch, int64_t size, int64_t* out) {
+    const int b = threadIdx.x;
+    if (b < batch) out[b] = dq_sample(seed, c->step, b, size);
+}
+
 __global__ void drl_dqn_init_kernel(DqnCounters* c, float epsilon) {
     if (threadIdx.x == 0) {
         c->step = 0;
@@ -1005,6 +1012,12 @@ int dqn_train_resident_capacity(size_t lds, int num_cus) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, drl_dqn_train_kernel, DQN_THREADS, lds) != hipSuccess)
         return -1;
     return per_cu * num_cus;
+}
+
+hipError_t launch_dqn_sample(const void* counters, uint64_t seed, int batch, int64_t size, int64_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(drl_dqn_sample_kernel, dim3(1), dim3(64), 0, s, static_cast<const DqnCounters*>(counters), seed,
+                       batch, size, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_dqn_init(void* counters, float epsilon, hipStream_t s) {

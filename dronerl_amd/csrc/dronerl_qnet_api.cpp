@@ -753,6 +753,21 @@ int drl_dqn_train(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agen
     return dqn_train_impl(d, h, d_agent, d_packed, r, size, nullptr, stream);
 }
 
+int drl_dqn_sample_rows(const drl_qnet_desc* d, const drl_dqn_hparams* h, const void* d_agent, int64_t size,
+                        int64_t* d_slots, hipStream_t stream) {
+    drl::QnetLayout L;
+    if (qnet_layout(d, &L)) return -1;
+    if (!h) return fail("hparams is NULL");
+    DqnPlan P;
+    if (dqn_plan(d, h->batch, L, &P)) return -1;
+    if (!d_agent || (uintptr_t)d_agent % 16) return fail("the agent block must be a 16-byte aligned device pointer");
+    if (!d_slots || (uintptr_t)d_slots % 8) return fail("d_slots must be an 8-byte aligned device pointer");
+    if (size < 1) return fail("size must be >= 1 (buffers.py can_sample: nothing is drawn from an empty ring)");
+    hipError_t e = drl::launch_dqn_sample(static_cast<const uint8_t*>(d_agent) + P.pub.counters_off, h->sample_seed,
+                                          h->batch, size, d_slots, stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "drl_dqn_sample_rows launch");
+}
+
 int drl_dqn_train_fresh(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agent, void* d_packed,
                         const drl_replay* r, int64_t size, const drl_replay_batch* fresh, hipStream_t stream) {
     if (!fresh) return fail("fresh batch is NULL");

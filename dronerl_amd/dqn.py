@@ -87,6 +87,7 @@ def _bind(L):
         "drl_dqn_train": [D, ctypes.POINTER(DrlDqnHParams), _vp, _vp, ctypes.POINTER(DrlReplay), i64, _vp],
         "drl_dqn_train_fresh": [D, ctypes.POINTER(DrlDqnHParams), _vp, _vp, ctypes.POINTER(DrlReplay), i64,
                                 ctypes.POINTER(DrlReplayBatch), _vp],
+        "drl_dqn_sample_rows": [D, ctypes.POINTER(DrlDqnHParams), _vp, i64, _vp, _vp],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -545,6 +546,20 @@ class DQNLearner:
                                             _vp(self.block.data_ptr()), _vp(self.net.packed.data_ptr()),
                                             ctypes.byref(rb._c), rb.size, _stream(self.block.device)))
 
+    def sample_slots(self, size: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The replay slots (int64 [batch], in [0, size)) the next train()
+        draws (drl_dqn_sample_rows: its counter hash at the step the device
+        counters will hold; stream-ordered, no sync)."""
+        if out is None:
+            out = torch.empty(self.hp.batch, dtype=torch.int64, device=self.block.device)
+        _on(out, self.block.device, torch.int64, "out")
+        if out.numel() != self.hp.batch or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous int64 [{self.hp.batch}] tensor")
+        _check(self.L, self.L.drl_dqn_sample_rows(ctypes.byref(self.net.desc), ctypes.byref(self._hp),
+                                                  _vp(self.block.data_ptr()), int(size), _vp(out.data_ptr()),
+                                                  _stream(self.block.device)))
+        return out
+
     def check_errors(self):
         """Synchronise; raise if a learner launch gave up waiting for one of
         its hand-offs (a hardware-scheduling fault, never expected).  From
@@ -554,6 +569,18 @@ class DQNLearner:
         if int(self._ctr_i[13].item()):
             raise DroneRLError("drl_dqn_train: a workgroup timed out waiting for another workgroup's hand-off; "
                                "the learner refuses to train until restart()")
+
+    def save(self, path: str, format: str = "torch", **kw):
+        """The online net as train_jax.py:238-244 saves the trained agent
+        (dronerl_amd.checkpoint.save_dense): format "torch" (jax dqn.py
+        save_as_torch), "jax" (dqn.py save) or "torch_agent" (torch_impl
+        DQNAgent.save).  Synchronises (a host copy of the parameters)."""
+        from .checkpoint import save_dense
+        W = round((self.net.in_features / 6) ** 0.5)
+        if W * W * 6 != self.net.in_features:
+            raise ValueError("the net's input is not a W x W x 6 window")
+        ws, bs = zip(*self.params("online"))
+        save_dense(path, ws, bs, (W, W, 6), format=format, **kw)
 
     def restart(self, epsilon: Optional[float] = None):
         """drl_dqn_init on the current parameters: Adam's moments and the

@@ -566,6 +566,15 @@ typedef struct drl_replay_batch {
 int drl_dqn_train_fresh(const drl_qnet_desc* d, const drl_dqn_hparams* h, void* d_agent, void* d_packed,
                         const struct drl_replay* r, int64_t size, const drl_replay_batch* fresh, hipStream_t stream);
 
+/* The `batch` replay slots (int64, [0, size)) the next drl_dqn_train on this
+ * block draws: the same counter hash of (sample_seed, step, row), with the step
+ * the counters hold when this launch runs on `stream`.  A sharded caller
+ * gathers those rows from the ranks that own them before the train call
+ * (the global learner; jax_impl/buffers.py:79-90 sample over
+ * one global ring, train_jax.py:196-212). */
+int drl_dqn_sample_rows(const drl_qnet_desc* d, const drl_dqn_hparams* h, const void* d_agent, int64_t size,
+                        int64_t* d_slots, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -213,6 +213,7 @@ KERNEL_TESTS = {
     "drl_replay_add_rows_kernel": "test_dqn.py::test_replay_add_two_float_rows",
     "drl_dqn_train_kernel": "test_dqn_learner.py::test_learner_matches_oracle_bit_exact",
     "drl_dqn_init_kernel": "test_dqn_learner.py::test_learner_matches_oracle_bit_exact",
+    "drl_dqn_sample_kernel": "test_dqn_learner.py::test_sample_slots_are_the_learners_draws",
 }
 
 

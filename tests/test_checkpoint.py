@@ -155,3 +155,82 @@ def test_evaluator_fixture_reproduces_published_scores():
     for i in range(5):
         mean, std = PUBLISHED[i + 1]
         assert np.isclose(s[i, :, 0].mean(), mean, rtol=1e-2) and np.isclose(s[i, :, 0].std(), std, rtol=1e-2)
+
+
+# ----------------------------------------------------------- saving an agent ---
+AGENT = os.path.join(GOLD, "agent_save")
+
+
+def _meta(path):
+    from safetensors import safe_open
+    with safe_open(path, framework="numpy") as f:
+        return dict(f.metadata() or {}), {k: f.get_tensor(k) for k in f.keys()}
+
+
+def _fixture_net():
+    ck = read_checkpoint(os.path.join(AGENT, "torch_agent.safetensors"))
+    n = len(ck.dense_layers) + 1
+    return ([ck.tensors[f"network.dense_{i + 1}.weight"] for i in range(n)],
+            [ck.tensors[f"network.dense_{i + 1}.bias"] for i in range(n)], ck)
+
+
+def test_save_torch_agent_matches_reference_save(tmp_path):
+    """save_dense(format="torch_agent") of the fixture's weights == the
+    reference's own torch DQNAgent.save (torch_impl/agents/dqn.py:330-345;
+    oracle/gen_agent_golden.py): the same metadata strings, tensor names,
+    shapes and bytes."""
+    from dronerl_amd.checkpoint import save_dense
+    ws, bs, _ = _fixture_net()
+    p = str(tmp_path / "a.safetensors")
+    save_dense(p, ws, bs, (7, 7, 6), format="torch_agent")
+    md_ref, t_ref = _meta(os.path.join(AGENT, "torch_agent.safetensors"))
+    md, t = _meta(p)
+    assert md == md_ref
+    assert sorted(t) == sorted(t_ref)
+    for k in t:
+        assert t[k].dtype == t_ref[k].dtype and np.array_equal(t[k], t_ref[k]), k
+
+
+@pytest.mark.parametrize("fmt", ["torch", "jax", "torch_agent"])
+def test_save_formats_read_back(tmp_path, fmt):
+    """Each form reads back (read_checkpoint / load_qnetwork, the jax form's
+    renames and transposes undone) to the reference net's Q values; the
+    "torch" form was also read by the reference's own loader when the fixture
+    was made (q_loader == q_ref); the metadata carries jax dqn.py:282-357's
+    keys (save / save_as_torch) with train_jax.py's conv_layers default."""
+    from dronerl_amd.checkpoint import TRAIN_JAX_CONV_LAYERS, save_dense
+    ws, bs, _ = _fixture_net()
+    gold = np.load(os.path.join(AGENT, "agent_q.npz"))
+    assert np.array_equal(gold["q_loader"], gold["q_ref"]) and np.array_equal(gold["q_loader_agent"], gold["q_ref"])
+    p = str(tmp_path / f"{fmt}.safetensors")
+    save_dense(p, ws, bs, (7, 7, 6), format=fmt)
+    md, t = _meta(p)
+    base = {"network_type": "dense", "dense_layers": "(32, 32)", "obs_shape": "(7, 7, 6)", "action_shape": "(5,)"}
+    if fmt == "torch_agent":
+        assert md == base
+    else:
+        assert md == dict(base, conv_layers=str(TRAIN_JAX_CONV_LAYERS), conv_dense_layers="()",
+                          checkpoint_format=fmt, checkpoint_format_version="0.1")
+    if fmt == "jax":
+        assert sorted(t) == sorted(f"params.Dense_{i}.{k}" for i in range(3) for k in ("kernel", "bias"))
+        assert t["params.Dense_0.kernel"].shape == (294, 32)
+    ck = read_checkpoint(p)
+    for i in range(3):
+        assert np.array_equal(ck.tensors[f"network.dense_{i + 1}.weight"], ws[i])
+        assert np.array_equal(ck.tensors[f"network.dense_{i + 1}.bias"], bs[i])
+    net = load_qnetwork(p)
+    with torch.no_grad():
+        q = net(torch.from_numpy(gold["inputs"].reshape(16, 7, 7, 6))).numpy()
+    np.testing.assert_array_equal(q, gold["q_ref"])
+
+
+def test_save_dense_argument_checks(tmp_path):
+    from dronerl_amd.checkpoint import save_dense
+    ws, bs, _ = _fixture_net()
+    p = str(tmp_path / "x.safetensors")
+    with pytest.raises(ValueError):
+        save_dense(p, ws, bs, (7, 7, 6), format="onnx")
+    with pytest.raises(ValueError):
+        save_dense(p, ws, bs[:-1], (7, 7, 6))
+    with pytest.raises(ValueError):
+        save_dense(p, ws, bs, (5, 5, 6))

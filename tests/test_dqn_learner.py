@@ -419,6 +419,31 @@ def test_learner_fresh_batch_equals_serial(cap, E):
 
 
 @gpu
+def test_sample_slots_are_the_learners_draws():
+    """DQNLearner.sample_slots (drl_dqn_sample_rows) == the slots the next
+    train() draws (the oracle's sample_indices at the device step), step after
+    step, for growing sizes; refused for an empty ring."""
+    from dronerl_amd.handle import DroneRLError
+    env, net, learner, rb, hp = _learner_setup((294, 128, 64, 5), "code", dict(batch=8, sample_seed=77), E=40,
+                                               cap=300)
+    cur, nxt = env.new_code(), env.new_code()
+    env.get_code(out=cur)
+    acts = torch.empty((40, 8), dtype=torch.int32, device="cuda")
+    for t in range(12):
+        net.act(cur, learner.epsilon, seed=3, step=t, actions=acts, synth=(5, t))
+        r, d = env.step(acts, code=nxt)
+        rb.add_many(cur, acts, r, nxt, d)
+        slots = learner.sample_slots(rb.size)
+        assert slots.cpu().tolist() == O.sample_indices(77, t, 8, rb.size), t
+        learner.train(rb)
+        cur, nxt = nxt, cur
+    torch.cuda.synchronize()
+    assert learner.counters()["step"] == 12
+    with pytest.raises(DroneRLError):
+        learner.sample_slots(0)
+
+
+@gpu
 def test_learner_handoff_timeout_is_reported_and_refused(monkeypatch):
     """a launch whose workgroup gives up on a hand-off sets the
     error flag; DQNLearner.check_errors raises; every later launch returns at

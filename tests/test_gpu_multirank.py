@@ -11,6 +11,8 @@ same: contiguous env shards with env_offset = rank * E / world, train_jax.py
    states == one process stepping every env.
 3. bench.py under torch.distributed.run with 2 ranks (DRL_DIST_BACKEND=gloo)
    prints one whole-job JSON line.
+4. The global learner (dronerl_amd.global_learner): 2 ranks with half the
+   envs each == one learner over every env, bit for bit.
 """
 import json
 import os
@@ -155,3 +157,81 @@ def test_bench_gpus2_launches_its_own_ranks():
     assert d["config"]["parallelism"] == "env-shard x2"
     assert d["c5"]["config"]["num_envs_total"] == 262144 and d["c5"]["n_gpus"] == 2
     assert "torch.distributed.run" in r.stderr  # the launcher's own line
+
+
+# ------------------------------------------------- the global learner (N > 1) ---
+GL_STEPS = 20
+
+
+def _learner_run(rank, world, E, cap):
+    """train_jax.py's loop over one shard (world > 1: ShardedReplay + gather
+    before every learner step) or over every env (world == 1: the plain ring)."""
+    from dronerl_amd import BatchedDeliveryDrones
+    from dronerl_amd.distributed import shard_envs
+    from dronerl_amd.dqn import DQNHParams, DQNLearner, QNetwork, ReplayBuffer
+    from dronerl_amd.global_learner import ShardedReplay
+    sh = shard_envs(E, rank, world)
+    env = BatchedDeliveryDrones(_params(), sh.num_envs, device="cuda:0", env_offset=sh.env_offset)
+    env.reset(seed=21)
+    net = QNetwork(294, (128, 64), device="cuda:0", generator=torch.Generator().manual_seed(3), input="code")
+    learner = DQNLearner(net, DQNHParams(batch=8, target_update_interval=3), generator=torch.Generator().manual_seed(4))
+    if world > 1:
+        sr = ShardedReplay(cap, 294, torch.device("cuda:0"), E, sh.env_offset, sh.num_envs, rank, world, code_radius=3)
+        ring = sr.ring
+    else:
+        sr = ring = ReplayBuffer(cap, 294, torch.device("cuda:0"), code_radius=3)
+    cur, nxt = env.new_code(), env.new_code()
+    env.get_code(out=cur)
+    acts = torch.empty((sh.num_envs, 8), dtype=torch.int32, device="cuda:0")
+    for t in range(GL_STEPS):
+        net.act(cur, learner.epsilon, seed=9, step=t, env_offset=sh.env_offset, actions=acts, synth=(13, t))
+        r, d = env.step(acts, code=nxt)
+        sr.add_many(cur, acts, r, nxt, d)
+        if world > 1:
+            sr.gather(learner)
+        learner.train(ring)
+        cur, nxt = nxt, cur
+    torch.cuda.synchronize()
+    learner.check_errors()
+    out = {k: learner.sets[k].cpu().numpy().copy() for k in ("online", "target", "m", "v")}
+    out["counters"] = learner.counters()
+    out["packed"] = net.packed.cpu().numpy().copy()
+    return out
+
+
+def _gl_worker(rank, world, port, E, cap, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out[rank] = _learner_run(rank, world, E, cap)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("E,cap", [(512, 3000), (512, 300)])  # the ring wraps; one add overfills it (E > cap)
+def test_global_learner_two_ranks_equal_one_learner(E, cap):
+    """two ranks, each with half the envs, its own image of
+    the global ring and the row exchange before every learner step, end with
+    parameters, target, Adam moments, counters and packed image all equal, bit
+    for bit, to one learner over every env's transitions in one ring
+    (train_jax.py:59-82, :196-212; buffers.py:57-90), over 20 steps."""
+    ref = _learner_run(0, 1, E, cap)
+    assert ref["counters"]["count"] == GL_STEPS
+    ctx = mp.get_context("spawn")
+    with ctx.Manager() as man:
+        out = man.dict()
+        port = _free_port()
+        procs = [ctx.Process(target=_gl_worker, args=(r, 2, port, E, cap, out)) for r in range(2)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=300)
+            assert p.exitcode == 0, p.exitcode
+        res = dict(out)
+    for r in range(2):
+        for k in ("online", "target", "m", "v", "packed"):
+            assert np.array_equal(res[r][k].view(np.uint32), ref[k].view(np.uint32)), (r, k)
+        assert res[r]["counters"] == ref["counters"], r
