@@ -139,7 +139,7 @@ int validate(const drl_params* p, drl_layout* L) {
         L->mt_stride = DRL_MT_WORDS;
         L->obs_window = 2 * p->window_radius + 1;
         L->obs_floats = L->obs_window * L->obs_window * 6;
-        const int lg = drl::lay::gstride(p->side);  // LDS ground bytes per env
+        const int lg = drl::lay::glstride(p->side);  // LDS ground bytes per env
         L->step_group_lanes = step_group_lanes(N, lg, GG, L->obs_window);
         L->step_lds_bytes =
             wave_lds_bytes(64 / L->step_group_lanes, env_lds(lg, GG, N, 1, L->obs_window, L->step_group_lanes), true);
@@ -167,7 +167,7 @@ drl::ObsGeom obs_geom(const drl_params* p, const drl_layout& L, int k) {
     g.W = (uint32_t)L.obs_window;
     g.per = (uint32_t)L.obs_floats;
     g.env_floats = (uint32_t)(k > 0 ? k : 1) * g.per;
-    g.gstride = (uint32_t)drl::lay::gstride(p->side);
+    g.gstride = (uint32_t)drl::lay::glstride(p->side);
     g.div_env = drl::make_fastdiv(g.env_floats / 6u);  // window cells per env
     g.div_per = drl::make_fastdiv(g.W * g.W);          // cells per window
     g.div_6 = drl::make_fastdiv(6);
@@ -181,7 +181,9 @@ drl::StepArgs step_args(const drl_params* p, const drl_state* s, const drl_layou
     memset(&a, 0, sizeof a);
     a.side = p->side;
     a.n_drones = p->n_drones;
-    a.gstride = drl::lay::gstride(p->side);  // LDS (the HBM row is half: lay::pstride)
+    a.gstride = drl::lay::glstride(p->side);  // LDS (a byte per cell, or the packed HBM row: lay::gl_nib)
+    a.pstride = drl::lay::pstride(p->side);
+    a.gl_nib = drl::lay::gl_nib(p->side) ? 1 : 0;
     a.kbits = bit_length((uint32_t)p->side);
     a.charge = p->charge;
     a.discharge = p->discharge;
@@ -194,7 +196,7 @@ drl::StepArgs step_args(const drl_params* p, const drl_state* s, const drl_layou
     a.drones = s->drones;
     a.mt = s->mt;
     a.mt_index = s->mt_index;
-    const EnvLds e = env_lds(drl::lay::gstride(p->side), L.cells, p->n_drones, obs_k, L.obs_window, L.step_group_lanes);
+    const EnvLds e = env_lds(drl::lay::glstride(p->side), L.cells, p->n_drones, obs_k, L.obs_window, L.step_group_lanes);
     a.np = env_np(p->n_drones);
     a.lds_bm = e.bm;
     a.lds_paint = e.paint;
@@ -360,7 +362,7 @@ static int set_code(const drl_params* p, drl::StepArgs* a, void* d_code, const d
     a->code = static_cast<uint4*>(d_code);
     const int P = L.step_group_lanes, gpw = 64 / P;
     const int need = gpw * drl::lay::code_bytes(L.obs_window);
-    const int stage = gpw * env_lds(drl::lay::gstride(p->side), L.cells, p->n_drones, 1, L.obs_window, P).fixed;
+    const int stage = gpw * env_lds(drl::lay::glstride(p->side), L.cells, p->n_drones, 1, L.obs_window, P).fixed;
     if (!with_obs && stage % 16 == 0 && a->wave_lds - stage >= need) {
         a->code_lds = stage;
     } else {

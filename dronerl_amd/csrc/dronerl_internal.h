@@ -90,7 +90,14 @@ constexpr int np(int n_drones) { return (n_drones + 7) / 8 * 8; }             //
 // ground: packed in HBM, one nibble per cell (cell 2i in the low nibble of
 // byte i, 2i + 1 in the high one; ABI 8), unpacked to a byte per cell in LDS
 constexpr int pstride(int side) { return r16((side * side + 1) / 2); }         // HBM ground bytes per env
-constexpr int gstride(int side) { return 2 * pstride(side); }                  // LDS ground bytes per env
+constexpr int gstride(int side) { return 2 * pstride(side); }                  // byte-per-cell image bytes per env
+// drl_step's LDS image of the ground: a byte per cell below DRL_GL_NIB_MIN_SIDE, the packed nibbles (the HBM
+// row as is: half the LDS, so more waves fit a CU) from there on (round 6: C5's 64 x 64 envs)
+#ifndef DRL_GL_NIB_MIN_SIDE
+#define DRL_GL_NIB_MIN_SIDE 64
+#endif
+constexpr bool gl_nib(int side) { return side >= DRL_GL_NIB_MIN_SIDE; }
+constexpr int glstride(int side) { return gl_nib(side) ? pstride(side) : gstride(side); }  // LDS ground bytes per env
 constexpr int bm_bytes(int cells) { return r16((cells + 31) / 32 * 4); }       // occupancy bitmap
 constexpr int paint_bytes(int k, int w) { return k > 0 ? r16(k * w * w) : 0; }  // observation paint
 constexpr int nchg(int n_drones) { return 6 * n_drones + 2; }                  // changed-cell capacity
@@ -155,7 +162,8 @@ struct ObsGeom {
 };
 
 struct StepArgs {
-    int side, n_drones, gstride, kbits;  // gstride: LDS ground bytes per env (2 x the packed HBM row)
+    int side, n_drones, gstride, kbits;  // gstride: LDS ground bytes per env (lay::glstride)
+    int pstride, gl_nib;                 // packed HBM ground bytes per env; 1: the LDS image is packed nibbles
     int charge, discharge;
     float r_pickup, r_delivery, r_crash, r_charge;
     int64_t E;

@@ -249,7 +249,9 @@ struct Geo {
     __device__ int side() const { return GC > 0 ? GC : a.side; }
     __device__ uint32_t div_side(uint32_t n) const { return GC > 0 ? n / (uint32_t)GC : fdiv(n, a.div_side); }
     __device__ int kbits() const { return GC > 0 ? lay::bit_length(GC) : a.kbits; }
-    __device__ int gstride() const { return GC > 0 ? lay::gstride(GC) : a.gstride; }
+    __device__ int gstride() const { return GC > 0 ? lay::glstride(GC) : a.gstride; }      // LDS ground bytes / env
+    __device__ int pstride() const { return GC > 0 ? lay::pstride(GC) : a.pstride; }       // HBM ground bytes / env
+    __device__ bool nib() const { return GC > 0 ? lay::gl_nib(GC) : a.gl_nib != 0; }       // packed LDS image
     __device__ int lds_bm() const { return GC > 0 ? lay::bm_bytes(GC * GC) : a.lds_bm; }
     __device__ int n() const { return NC > 0 ? NC : a.n_drones; }
     __device__ int np() const { return NC > 0 ? lay::np(NC) : a.np; }
@@ -278,7 +280,8 @@ struct Geo {
     }
     static constexpr bool kObs = KC != 0;  // KC == 0: instance for steps without observation
     static constexpr int kN = NC;
-    static constexpr int kGstride = GC > 0 ? lay::gstride(GC) : 0;
+    static constexpr int kGstride = GC > 0 ? lay::glstride(GC) : 0;
+    static constexpr int kPstride = GC > 0 ? lay::pstride(GC) : 0;
 };
 using GeoRT = Geo<0, 0, 0, -1>;
 
@@ -357,9 +360,14 @@ __device__ __forceinline__ uint4 nib_pack_load(const l_u8* src) {
 
 // The wave's packed grounds (contiguous in HBM, env-major, nbytes) -> LDS,
 // runtime geometry: load, unpack, store.
-__device__ __forceinline__ void stage_ground_nib(const uint8_t* __restrict__ src, int nbytes, l_u8* gl, int lane) {
+__device__ __forceinline__ void stage_ground_nib(const uint8_t* __restrict__ src, int nbytes, l_u8* gl, int lane,
+                                                 bool nib) {
     const int nvec = nbytes / 16;
-    for (int v = lane; v < nvec; v += 64) nib_unpack_store(gl + v * 32, reinterpret_cast<const uint4*>(src)[v]);
+    for (int v = lane; v < nvec; v += 64) {
+        const uint4 x = reinterpret_cast<const uint4*>(src)[v];
+        if (nib) reinterpret_cast<l_u4*>(gl)[v] = u32x4{x.x, x.y, x.z, x.w};  // (the packed row as is)
+        else nib_unpack_store(gl + v * 32, x);
+    }
 }
 
 // Compile-time form in two halves: the loads (NV vectors, unrolled, so the
@@ -377,10 +385,13 @@ struct NibStage {
         for (int q = 0; q < Q; ++q)
             v[q] = reinterpret_cast<const uint4*>(src)[min((uint32_t)(64 * q + lane), last)];
     }
-    __device__ __forceinline__ void store(l_u8* gl, int lane) const {
+    __device__ __forceinline__ void store(l_u8* gl, int lane, bool nib) const {
 #pragma unroll
         for (int q = 0; q < Q; ++q)
-            if (NV % 64 == 0 || 64 * q + lane < NV) nib_unpack_store(gl + (64 * q + lane) * 32, v[q]);
+            if (NV % 64 == 0 || 64 * q + lane < NV) {
+                if (nib) reinterpret_cast<l_u4*>(gl)[64 * q + lane] = u32x4{v[q].x, v[q].y, v[q].z, v[q].w};
+                else nib_unpack_store(gl + (64 * q + lane) * 32, v[q]);
+            }
     }
 };
 
@@ -398,6 +409,26 @@ __device__ __forceinline__ uint32_t nib_get_l2(uint8_t* row, int cell) {  // aft
 }
 __device__ __forceinline__ void nib_clear(uint8_t* row, int cell) {
     atomicAnd(reinterpret_cast<uint32_t*>(row) + (cell >> 3), ~(15u << ((cell & 7) * 4)));
+}
+
+// One env's ground in drl_step's LDS image (GEO::nib(): packed nibbles, the HBM row as is, else a byte per
+// cell).  Nibble writes are LDS atomics on the cell's dword (two lanes may change two cells of one dword).
+template <class GEO>
+__device__ __forceinline__ int gl_get(const GEO& g, const l_u8* gl, int cell) {
+    if (g.nib()) return (gl[cell >> 1] >> ((cell & 1) << 2)) & 15;
+    return gl[cell];
+}
+template <class GEO>
+__device__ __forceinline__ void gl_clear(const GEO& g, l_u8* gl, int cell) {  // -> OBJ_EMPTY
+    if (g.nib()) __atomic_fetch_and(reinterpret_cast<l_u32*>(gl) + (cell >> 3), ~(15u << ((cell & 7) << 2)),
+                                    __ATOMIC_RELAXED);
+    else gl[cell] = OBJ_EMPTY;
+}
+template <class GEO>
+__device__ __forceinline__ void gl_put(const GEO& g, l_u8* gl, int cell, int obj) {  // an OBJ_EMPTY cell -> obj
+    if (g.nib()) __atomic_fetch_or(reinterpret_cast<l_u32*>(gl) + (cell >> 3), (uint32_t)obj << ((cell & 7) << 2),
+                                   __ATOMIC_RELAXED);
+    else gl[cell] = (uint8_t)obj;
 }
 
 // 16-B observation store.  NT: streaming (global_store_dwordx4 ... nt), for
@@ -474,7 +505,7 @@ __device__ __forceinline__ void write_obs_wave(float* __restrict__ base, int nen
             const int y = (int)(py + wy[u]) - R;
             const int x = (int)(px + wx[u]) - R;
             const bool in = (unsigned)y < (unsigned)G && (unsigned)x < (unsigned)G;
-            const uint32_t o = w.gl[e[u] * gstride + (uint32_t)(in ? y * G + x : 0)];
+            const uint32_t o = (uint32_t)gl_get(g, w.gl + e[u] * gstride, in ? y * G + x : 0);
             const uint32_t obj = in ? o : (uint32_t)OBJ_SKYSCRAPER;
             const uint32_t air = w.paint[e[u] * lpaint + rem[u]];
             if constexpr (CODE) {
@@ -743,7 +774,8 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     // the wave's slices of the state (scalar bases)
     uint32_t* const drones_w = a.drones + wenv0 * N;
     uint32_t* const mt_w = a.mt + wenv0 * MT_WORDS;
-    uint8_t* const ground_w = a.ground + wenv0 * (gstride / 2);  // packed rows: half the LDS stride
+    const int pstride = g.pstride();
+    uint8_t* const ground_w = a.ground + wenv0 * pstride;  // packed rows
     const uint32_t rl0 = (uint32_t)(grp0 * N);  // lane's env offset in [env][drone] arrays of the wave
 
     DRL_STAMP(0);
@@ -770,9 +802,9 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     const int act_ld = a.actions[wenv0 * N + li0];
 #endif
     // the packed grounds: loaded now, unpacked into LDS after the claim scan (compile-time geometry)
-    [[maybe_unused]] NibStage<(GEO::kGstride > 0 ? GPW * GEO::kGstride / 32 : 1)> nib;
-    if constexpr (GEO::kGstride > 0) nib.load(ground_w, nenv_w * (gstride / 2), lane0);
-    else stage_ground_nib(ground_w, nenv_w * (gstride / 2), W.gl, lane0);
+    [[maybe_unused]] NibStage<(GEO::kPstride > 0 ? GPW * GEO::kPstride / 16 : 1)> nib;
+    if constexpr (GEO::kPstride > 0) nib.load(ground_w, nenv_w * pstride, lane0);
+    else stage_ground_nib(ground_w, nenv_w * pstride, W.gl, lane0, g.nib());
     __builtin_amdgcn_sched_barrier(0);  // issue every load above before waiting for the MT index
     uint32_t mword = mi[0];  // the env's mt_index word: index, block, ring head / count
 #pragma unroll
@@ -895,7 +927,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     const bool claimer = inb && !earlier;
     const bool crashA = active && !claimer;
     if constexpr (GEO::kGstride > 0) {
-        if (t == 0) nib.store(W.gl, lane0);  // (a rollout stages once)
+        if (t == 0) nib.store(W.gl, lane0, g.nib());  // (a rollout stages once)
     }
     // the grounds are in LDS; wave_sync orders lanes
     wave_sync();
@@ -905,7 +937,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     float reward = 0.0f;
     bool dead = false, deliver = false;
     if (claimer) {
-        const int obj = gl[tcell];
+        const int obj = gl_get(g, gl, tcell);
         if (obj == OBJ_STATION) {
             c = min(100, c + a.charge);
             reward = a.r_charge;
@@ -916,12 +948,12 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         if (obj == OBJ_PACKET && !carry) {
             reward = a.r_pickup;
             carry = 1;
-            gl[tcell] = OBJ_EMPTY;
+            gl_clear(g, gl, tcell);
             if constexpr (!ROLL) chg_push(W, grp, nchg, tcell);
         } else if (obj == OBJ_DROPZONE && carry) {
             reward = a.r_delivery;
             carry = 0;
-            gl[tcell] = OBJ_EMPTY;
+            gl_clear(g, gl, tcell);
             deliver = true;
             if constexpr (!ROLL) chg_push(W, grp, nchg, tcell);
         }
@@ -1024,7 +1056,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
                     for (int t2 = 0; t2 < CH; ++t2) prev = (ts[t2] == tg && s0 + t2 < j) ? s0 + t2 : prev;
                 }
             }
-            const int gobj = gl[ccell];
+            const int gobj = gl_get(g, gl, ccell);
             const bool occ = bm_test(bm, ccell);
             const int bend = min(P * (r + 1), qcnt);  // end of the batch's valid entries
 #pragma unroll
@@ -1034,7 +1066,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
                 const bool isd = w < nR;
                 const int cls_end = isd ? nR : (w < nR + n_pack ? nR + n_pack : total);
                 const int need = cls_end - w;
-                const int gnow = cs == 0 ? gobj : (int)gl[ccell];  // packets placed by the previous step
+                const int gnow = cs == 0 ? gobj : gl_get(g, gl, ccell);  // packets placed by the previous step
                 const bool fresh = valid && P * r + j >= start && (prev < 0 || P * r + prev < start);
                 const bool ok = act && fresh && (isd ? (!occ && gnow != OBJ_SKYSCRAPER) : gnow == OBJ_EMPTY);
                 const GMask M = gballot<P>(ok, gshift);
@@ -1047,7 +1079,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
                         posidx[w + rank] = (uint16_t)cell;  // item slot (posidx is rewritten at write-back)
                         bm_set(bm, cell);
                     } else {
-                        gl[cell] = (w + rank < nR + n_pack) ? OBJ_PACKET : OBJ_DROPZONE;
+                        gl_put(g, gl, cell, (w + rank < nR + n_pack) ? OBJ_PACKET : OBJ_DROPZONE);
                         if constexpr (!ROLL) chg_push(W, grp, nchg, cell);
                     }
                 }
@@ -1160,7 +1192,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
             const int ycand = prevm ? rp : yv;
             candq[q] = accq[q] && (apos & 1);
             ccq[q] = candq[q] ? ycand * G + rq[q] : 0;
-            const int gobj = gl[ccq[q]];
+            const int gobj = gl_get(g, gl, ccq[q]);
             const bool occ = bm_test(bm, ccq[q]);
             okd = gballot<P>(candq[q] && !occ && gobj != OBJ_SKYSCRAPER, gshift);  // drone items
             okg = gballot<P>(candq[q] && gobj == OBJ_EMPTY, gshift);              // packet / dropzone items
@@ -1206,7 +1238,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
                         okdc &= ~same;
                     } else {
                         if (j == 0) {
-                            gl[cell] = (w < nR + n_pack) ? OBJ_PACKET : OBJ_DROPZONE;
+                            gl_put(g, gl, cell, (w < nR + n_pack) ? OBJ_PACKET : OBJ_DROPZONE);
                             if constexpr (!ROLL) chg_push(W, grp, nchg, cell);
                         }
                         okgc &= ~same;
@@ -1260,9 +1292,9 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
 #endif
     // ---- _pick_packets_after_respawn (env.py:217-224): distinct cells, parallel
     if (active && pos < 0) pos = 0;  // unreachable for valid params (respawn always finds a cell)
-    if (active && !carry && gl[pos] == OBJ_PACKET) {
+    if (active && !carry && gl_get(g, gl, pos) == OBJ_PACKET) {
         carry = 1;
-        gl[pos] = OBJ_EMPTY;
+        gl_clear(g, gl, pos);
         if constexpr (!ROLL) chg_push(W, grp, nchg, pos);
     }
 
@@ -1312,7 +1344,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     if (!ROLL && env_ok) {
         const uint32_t nc = W.cnt[grp * 4];
         const l_u16* ch = W.chg + grp * nchg;
-        uint8_t* gdst = ground_w + (uint32_t)(grp * (gstride / 2));
+        uint8_t* gdst = ground_w + (uint32_t)(grp * pstride);
         // Changes per step <= 4N (N pickups/deliveries, 2N respawned packets and
         // dropzones, N pick-after-respawn) < the list's 6N + 2 entries, so the
         // list never overflows (chg_push drops past capacity regardless).  The
@@ -1322,7 +1354,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
 #pragma clang loop unroll(disable) vectorize(disable)
         for (uint32_t q = j; q < min(nc, (uint32_t)nchg); q += P) {  // the cell's packed byte (both nibbles)
             const uint32_t e = ch[q] & ~1u;
-            gdst[e >> 1] = (uint8_t)(gl[e] | (gl[e + 1] << 4));
+            gdst[e >> 1] = g.nib() ? gl[e >> 1] : (uint8_t)(gl[e] | (gl[e + 1] << 4));
         }
 #endif
     }
@@ -1361,7 +1393,14 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         if (active0) drones_w[rl0 + j0] = stash[lane0];
         if (env_ok0 && j0 == 0) a.mt_index[wenv0 + grp0] = mword;
         uint4* dst = reinterpret_cast<uint4*>(ground_w);
-        for (int v = lane0; v < nenv_w * gstride / 32; v += 64) dst[v] = nib_pack_load(W.gl + v * 32);
+        for (int v = lane0; v < nenv_w * pstride / 16; v += 64) {
+            if (g.nib()) {
+                const u32x4 x = reinterpret_cast<const l_u4*>(W.gl)[v];
+                dst[v] = make_uint4(x[0], x[1], x[2], x[3]);
+            } else {
+                dst[v] = nib_pack_load(W.gl + v * 32);
+            }
+        }
     }
 }
 
@@ -1390,8 +1429,13 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t orig, uint32_t n) {
 // policy code (drl_step_code).
 // RING: drl_step_code_replay (its own instance: the sink costs the plain
 // step's register allocation spills).
+// (DRL_STEP_WAVES_P32: the register budget of the 32-lane (C5) instances as waves per SIMD; 1 = no cap)
+#ifndef DRL_STEP_WAVES_P32
+#define DRL_STEP_WAVES_P32 1
+#endif
 template <int P, class GEO, bool NT, bool CODE = false, bool RING = false>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : 1, 8)))
+__global__ void __launch_bounds__(64)
+__attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : (P == 32 ? DRL_STEP_WAVES_P32 : 1), 8)))
 drl_step_kernel(StepArgs a) {
     step_batch<P, GEO, false, NT, CODE, RING>(a, (int64_t)xcd_block(blockIdx.x, gridDim.x) * (64 / P));
 }
@@ -1415,9 +1459,9 @@ __global__ void __launch_bounds__(64) drl_obs_kernel(StepArgs a) {
     const int nenv_w = (int)min((int64_t)GPW, a.E - wenv0);
     if (nenv_w <= 0) return;
     const bool env_ok = grp < nenv_w;
-    const int N = g.n(), gstride = g.gstride();
+    const int N = g.n();
     const WaveLds W = carve((l_u8*)smem, GPW, P, g);
-    stage_ground_nib(a.ground + wenv0 * (gstride / 2), nenv_w * (gstride / 2), W.gl, lane);
+    stage_ground_nib(a.ground + wenv0 * g.pstride(), nenv_w * g.pstride(), W.gl, lane, g.nib());
     lds_zero(W.paint, GPW * g.lds_paint(), lane);
     const bool active = env_ok && j < N;
     const uint32_t rec = active ? a.drones[wenv0 * N + (uint32_t)(grp * N + j)] : 0u;
