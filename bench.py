@@ -380,7 +380,29 @@ def cpu_baseline(G, N, K, seconds: float):
             "cores_basis": cpu_note,
             "single_thread_value": e1 * s1 / d1,
             "single_thread_sample": f"{e1} envs x {s1} steps, 1 thread, {d1:.1f}s wall",
-            "cpu_model": cpu_model()}
+            "cpu_model": cpu_model(), "reference_torch_impl": reference_torch_impl(G, N)}
+
+
+# the reference's own torch_impl step()+WindowedGridView, timed in the build container by
+# oracle/time_reference_torch_impl.py (the reference cannot run on the GPU box): quoted, not measured here
+REFERENCE_TIMING = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                "r06_reference_torch_impl.json")
+
+
+def reference_torch_impl(G, N):
+    try:
+        with open(REFERENCE_TIMING) as f:
+            ref = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for cfg in ref.get("configs", {}).values():
+        if cfg.get("side") == G and cfg.get("n_drones") == N:
+            return {"value": cfg["step_obs_env_steps_per_s"], "unit": "env-steps/s", "cores": ref.get("cores", 1),
+                    "kind": "reference", "step_only_value": cfg["step_only_env_steps_per_s"],
+                    "hardware": ref.get("hardware"), "different_hardware": True,
+                    "sample": f"{cfg['timed_steps']} steps of one env, uniform random actions",
+                    "source": "profiles/r06_reference_torch_impl.json (oracle/time_reference_torch_impl.py)"}
+    return None
 
 
 def dqn_consumer_bench(env, actions, rewards, dones, obs, warmup, steps, stream, precision="f32", input="obs"):

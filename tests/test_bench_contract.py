@@ -254,3 +254,16 @@ def test_strong_split():
         bench.strong_split(65536, 3)
     with pytest.raises(ValueError):
         bench.strong_split(0, 2)
+
+
+def test_cpu_baseline_quotes_reference_torch_impl():
+    """the reference's own torch_impl step()+WindowedGridView,
+    timed in the build container by oracle/time_reference_torch_impl.py, is
+    quoted beside the port baseline and labelled as other hardware."""
+    import bench
+    for G, N in ((16, 8), (64, 32)):
+        r = bench.reference_torch_impl(G, N)
+        assert r is not None and r["kind"] == "reference" and r["different_hardware"] is True
+        assert r["value"] > 0 and r["step_only_value"] > r["value"] and r["cores"] == 1
+        assert "NOT the GPU box" in r["hardware"]
+    assert bench.reference_torch_impl(12, 3) is None
