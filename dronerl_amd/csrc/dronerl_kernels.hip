@@ -710,6 +710,21 @@ __device__ __forceinline__ int gshfl(int v, int src, int lane) {
 #endif
 }
 
+// The same exchange over a whole group with the source lanes known at compile time: the group's base as a
+// bpermute byte address, made opaque where a scan starts (gbase), so each source's address is that base plus
+// an immediate offset formed at its use -- not P addresses hoisted to the kernel's start and held live in
+// registers across it (at P = 32 that was 32 VGPRs of the C5 step's 114)
+template <int P>
+__device__ __forceinline__ int gbase(int lane) {
+    int b = (lane & ~(P - 1)) << 2;
+    asm volatile("" : "+v"(b));
+    return b;
+}
+template <int P>
+__device__ __forceinline__ int gshfl_at(int v, int base, int src) {
+    return __builtin_amdgcn_ds_bpermute(base + ((src & (P - 1)) << 2), v);
+}
+
 // Value of lane (lane ^ K) within each 8-lane group, K = 1..7, by DPP (no LDS
 // round trip): quad_perm for K = 1, 2, 3, row_half_mirror (lane i <- 7 - i =
 // i ^ 7) for K = 7, and half_mirror after quad_perm(K ^ 7) for K = 4, 5, 6.
@@ -760,7 +775,10 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     constexpr int D = step_draws(P);             // draws per lane per dry-ring respawn round
     constexpr int QL = step_cq(P);               // ring entries per lane per batch
     using CM = typename GMaskT<(P * D <= 32 ? 32 : 64)>::type;  // round-position masks
-    constexpr int CH = P < 16 ? P : 16;        // shuffle batch
+#ifndef DRL_SHFL_BATCH
+#define DRL_SHFL_BATCH 16
+#endif
+    constexpr int CH = P < DRL_SHFL_BATCH ? P : DRL_SHFL_BATCH;  // shuffle batch
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const GEO g{a};
     const int lane0 = threadIdx.x & 63;
@@ -859,6 +877,11 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         if (t + 1 < T) act_next = a.actions[(t + 1) * a.act_tstride + wenv0 * N + li];
     }
 
+#ifdef DRL_NIB_EARLY  // (A/B: a packed LDS image stored before the claim scan, its registers freed)
+    if constexpr (GEO::kGstride > 0 && !ROLL) {
+        if (g.nib()) nib.store(W.gl, lane0, true);
+    }
+#endif
     DRL_STAMP(1);
     const int y = rec & 255u, x = (rec >> 8) & 255u;
     const int idx = ((int)(rec >> 25) < N) ? (int)(rec >> 25) : j;  // corrupt records never index out of bounds
@@ -910,11 +933,12 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
             later_min = (same && s > j && s < later_min) ? s : later_min;
         });
     } else {
+    const int gb = gbase<P>(lane);
 #pragma unroll
     for (int s0 = 0; s0 < P; s0 += CH) {
         int ts[CH];
 #pragma unroll
-        for (int t = 0; t < CH; ++t) ts[t] = gshfl<P>(tcell, s0 + t, lane);
+        for (int t = 0; t < CH; ++t) ts[t] = gshfl_at<P>(tcell, gb, s0 + t);
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
             const int s = s0 + t;
@@ -927,7 +951,11 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     const bool claimer = inb && !earlier;
     const bool crashA = active && !claimer;
     if constexpr (GEO::kGstride > 0) {
+#ifdef DRL_NIB_EARLY
+        if (t == 0 && (ROLL || !g.nib())) nib.store(W.gl, lane0, g.nib());
+#else
         if (t == 0) nib.store(W.gl, lane0, g.nib());  // (a rollout stages once)
+#endif
     }
     // the grounds are in LDS; wave_sync orders lanes
     wave_sync();
@@ -979,14 +1007,16 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
         const int bkey = crashB ? (collided ? later_min : P + j) : 4 * P;
         if constexpr ((P == 8 || P == 16) && DRL_DPP8) {
             for_other_lanes<P>(bkey, [&](int o, int) { rankB += o < bkey; });
-        } else
+        } else {
+        const int gb = gbase<P>(lane);
 #pragma unroll
         for (int s0 = 0; s0 < P; s0 += CH) {
             int ks[CH];
 #pragma unroll
-            for (int t = 0; t < CH; ++t) ks[t] = gshfl<P>(bkey, s0 + t, lane);
+            for (int t = 0; t < CH; ++t) ks[t] = gshfl_at<P>(bkey, gb, s0 + t);
 #pragma unroll
             for (int t = 0; t < CH; ++t) rankB += (ks[t] < bkey);
+        }
         }
     }
     const int newslot = survivor ? __popcll(bS & lower)
@@ -1047,11 +1077,12 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
                     prev = (o == tg && s2 < j && s2 > prev) ? s2 : prev;
                 });
             } else {
+                const int gb = gbase<P>(lane);
 #pragma unroll
                 for (int s0 = 0; s0 < P; s0 += CH) {
                     int ts[CH];
 #pragma unroll
-                    for (int t2 = 0; t2 < CH; ++t2) ts[t2] = gshfl<P>(tg, s0 + t2, lane);
+                    for (int t2 = 0; t2 < CH; ++t2) ts[t2] = gshfl_at<P>(tg, gb, s0 + t2);
 #pragma unroll
                     for (int t2 = 0; t2 < CH; ++t2) prev = (ts[t2] == tg && s0 + t2 < j) ? s0 + t2 : prev;
                 }
@@ -1429,13 +1460,17 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t orig, uint32_t n) {
 // policy code (drl_step_code).
 // RING: drl_step_code_replay (its own instance: the sink costs the plain
 // step's register allocation spills).
-// (DRL_STEP_WAVES_P32: the register budget of the 32-lane (C5) instances as waves per SIMD; 1 = no cap)
+// (DRL_STEP_WAVES_P16 / _P32: the register budget of the 16- / 32-lane (C4 / C5) instances as waves per
+// SIMD; 1 = no cap)
+#ifndef DRL_STEP_WAVES_P16
+#define DRL_STEP_WAVES_P16 1
+#endif
 #ifndef DRL_STEP_WAVES_P32
 #define DRL_STEP_WAVES_P32 1
 #endif
 template <int P, class GEO, bool NT, bool CODE = false, bool RING = false>
 __global__ void __launch_bounds__(64)
-__attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : (P == 32 ? DRL_STEP_WAVES_P32 : 1), 8)))
+__attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : (P == 32 ? DRL_STEP_WAVES_P32 : P == 16 ? DRL_STEP_WAVES_P16 : 1), 8)))
 drl_step_kernel(StepArgs a) {
     step_batch<P, GEO, false, NT, CODE, RING>(a, (int64_t)xcd_block(blockIdx.x, gridDim.x) * (64 / P));
 }

@@ -97,6 +97,8 @@ class BatchedDeliveryDrones:
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise DroneRLError("BatchedDeliveryDrones runs on the GPU only (no CPU fallback)")
+        if self.device.index is None:  # "cuda" -> the current device (tensors made on it report their index)
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.params = params
         self.layout = params.layout()  # validates (ValueError like the reference)
         self._cp = params.to_c()
