@@ -639,7 +639,7 @@ class TrainSegment:
 
     def __init__(self, env, seg: int, parallel: bool = False, net=None, rb=None, fused: bool = True,
                  precision: str = "f32", input: str = "obs", learn: bool = True, capacity: int = MEMORY_SIZE,
-                 hp=None, fuse_replay=None):
+                 hp=None, fuse_replay=None, refill_branch: bool = True):
         from dronerl_amd.dqn import DQNHParams, DQNLearner, QNetwork, ReplayBuffer
         E, N, dev = env.num_envs, env.n_drones, env.device
         W = env.layout.obs_window
@@ -658,6 +658,7 @@ class TrainSegment:
         if fuse_replay and (input != "code" or parallel):
             raise ValueError("fuse_replay needs input='code' and parallel=False")
         self.fuse_replay = fuse_replay
+        self.refill_branch = refill_branch  # (one stream: the refill on its own graph branch, see run)
         # parallel branches need 3 rotating buffers (see above); on one stream 2
         # suffice, and the third 77 MB observation buffer costs MALL hits (C3
         # loop 79.4 vs 74.4 us per step)
@@ -715,7 +716,39 @@ class TrainSegment:
 
     def run(self):
         main = torch.cuda.current_stream(self.env.device)
-        if not self.parallel:
+        if not self.parallel and self.refill_branch and self.env.refill_every > 0:
+            # one stream, except the respawn-candidate refill (env.step()'s cadence): it only reads and writes
+            # the MT rows, which the learner and the next act do not touch, so it runs on its own branch after
+            # the step it follows and the next step waits for it (the refill's 79 / 136 us at C3 / C5 overlap
+            # the learner and the act)
+            every = self.env.refill_every
+            self.env.refill_every = 0
+            since = self.env._since_refill
+            ev_ref = None
+            try:
+                for t in range(self.seg):
+                    if not self.fused:
+                        self._synth(t)
+                    join = (lambda e=ev_ref: main.wait_event(e)) if ev_ref is not None else None
+                    self._act_step(t, before_step=join)
+                    ev_ref = None
+                    since += 1
+                    if since >= every:
+                        since = 0
+                        ev_step = torch.cuda.Event()
+                        ev_step.record(main)
+                        with torch.cuda.stream(self.s_ref):
+                            self.s_ref.wait_event(ev_step)
+                            self.env.refill()
+                            ev_ref = torch.cuda.Event()
+                            ev_ref.record(self.s_ref)
+                    self._replay(t)
+                    self._learn()
+                main.wait_stream(self.s_ref)
+            finally:
+                self.env.refill_every = every
+                self.env._since_refill = since
+        elif not self.parallel:
             for t in range(self.seg):
                 if not self.fused:
                     self._synth(t)
@@ -838,7 +871,8 @@ def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fus
                                   "sampled rows gathered across ranks every step (SURVEY.md section 8 E2; "
                                   "DESIGN.md section 6)"}
     branches = (("replay add_many" if fused else "synthetic actions and replay add_many") +
-                " on parallel graph branches, 3 rotating buffers" if parallel else "one stream") + \
+                " on parallel graph branches, 3 rotating buffers" if parallel else
+                "one stream, the refill on its own graph branch" if loop.refill_branch else "one stream") + \
         ("; synthetic actions inside the act launch" if fused else "") + \
         ("; the replay add inside the step launch (drl_step_code_replay)" if loop.fuse_replay else "")
     return {"env_steps_per_s": E * seg * reps / dt, "us_per_step": dt / (seg * reps) * 1e6,

@@ -375,15 +375,25 @@ __device__ __forceinline__ void stage_ground_nib(const uint8_t* __restrict__ src
 // valid vector and unpack into LDS the wave does not use) are issued with the
 // step's first loads, the unpack and LDS stores come after the claim scan,
 // which does not need the ground, so the loads' latency overlaps it.
-template <int NV>
+// NT: streaming (non-temporal) loads -- the large grids' rows (lay::gl_nib sides: C5's 2 KB per env), which
+// would otherwise push the step's outputs the next kernels read out of the caches (C5 train loop, one box:
+// step 113.2 -> 110.4 us, learner 28.7 -> 26.2; C3 slower, 16.6 -> 17.5: byte-image sides keep cached loads)
+template <int NV, bool NT = false>
 struct NibStage {
     static constexpr int Q = (NV + 63) / 64;
     uint4 v[Q];
     __device__ __forceinline__ void load(const uint8_t* __restrict__ src, int nbytes, int lane) {
         const uint32_t last = (uint32_t)(nbytes / 16 - 1);
 #pragma unroll
-        for (int q = 0; q < Q; ++q)
-            v[q] = reinterpret_cast<const uint4*>(src)[min((uint32_t)(64 * q + lane), last)];
+        for (int q = 0; q < Q; ++q) {
+            if constexpr (NT) {
+                const u32x4 t =
+                    __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src) + min((uint32_t)(64 * q + lane), last));
+                v[q] = make_uint4(t[0], t[1], t[2], t[3]);
+            } else {
+                v[q] = reinterpret_cast<const uint4*>(src)[min((uint32_t)(64 * q + lane), last)];
+            }
+        }
     }
     __device__ __forceinline__ void store(l_u8* gl, int lane, bool nib) const {
 #pragma unroll
@@ -820,7 +830,7 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     const int act_ld = a.actions[wenv0 * N + li0];
 #endif
     // the packed grounds: loaded now, unpacked into LDS after the claim scan (compile-time geometry)
-    [[maybe_unused]] NibStage<(GEO::kPstride > 0 ? GPW * GEO::kPstride / 16 : 1)> nib;
+    [[maybe_unused]] NibStage<(GEO::kPstride > 0 ? GPW * GEO::kPstride / 16 : 1), (GEO::kGstride == GEO::kPstride)> nib;
     if constexpr (GEO::kPstride > 0) nib.load(ground_w, nenv_w * pstride, lane0);
     else stage_ground_nib(ground_w, nenv_w * pstride, W.gl, lane0, g.nib());
     __builtin_amdgcn_sched_barrier(0);  // issue every load above before waiting for the MT index
