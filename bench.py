@@ -811,7 +811,7 @@ class TrainSegment:
 
 
 def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fused: bool = True,
-                     precision: str = "f32", input: str = "obs", learn: bool = True):
+                     precision: str = "f32", input: str = "obs", learn: bool = True, refill_branch: bool = True):
     """TrainSegment captured once as a HIP graph (no host work per step) and
     replayed.  The host-side counters (action stream step, exploration draws,
     replay cursor) are baked into the capture, so replays repeat them: the
@@ -819,7 +819,8 @@ def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fus
     learner's counters (step, Adam count, epsilon, sampled rows) live on the
     device and continue across replays."""
     dev = env.device
-    loop = TrainSegment(env, seg, parallel=parallel, fused=fused, precision=precision, input=input, learn=learn)
+    loop = TrainSegment(env, seg, parallel=parallel, fused=fused, precision=precision, input=input, learn=learn,
+                        refill_branch=refill_branch)
     side = torch.cuda.Stream(dev)
     side.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(side):
