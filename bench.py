@@ -639,7 +639,7 @@ class TrainSegment:
 
     def __init__(self, env, seg: int, parallel: bool = False, net=None, rb=None, fused: bool = True,
                  precision: str = "f32", input: str = "obs", learn: bool = True, capacity: int = MEMORY_SIZE,
-                 hp=None, fuse_replay=None, refill_branch: bool = True):
+                 hp=None, fuse_replay=None, refill_branch: bool = False):
         from dronerl_amd.dqn import DQNHParams, DQNLearner, QNetwork, ReplayBuffer
         E, N, dev = env.num_envs, env.n_drones, env.device
         W = env.layout.obs_window
@@ -717,10 +717,12 @@ class TrainSegment:
     def run(self):
         main = torch.cuda.current_stream(self.env.device)
         if not self.parallel and self.refill_branch and self.env.refill_every > 0:
-            # one stream, except the respawn-candidate refill (env.step()'s cadence): it only reads and writes
-            # the MT rows, which the learner and the next act do not touch, so it runs on its own branch after
-            # the step it follows and the next step waits for it (the refill's 79 / 136 us at C3 / C5 overlap
-            # the learner and the act)
+            # (A/B, off by default) one stream, except the respawn-candidate refill (env.step()'s cadence): it
+            # only reads and writes the MT rows, which the learner and the next act do not touch, so it can run
+            # on its own branch after the step it follows, the next step waiting for it.  Measured
+            # (gpurun_out r06i, tools/loop_refill_ab.sh): C3 71.6 / 71.1 against 70.2 / 69.6 us per step inline,
+            # C5 248.7 / 248.5 against 248.6 / 248.0 -- the refill's HBM stream slows the learner's hand-offs
+            # as much as the overlap saves
             every = self.env.refill_every
             self.env.refill_every = 0
             since = self.env._since_refill
@@ -811,7 +813,7 @@ class TrainSegment:
 
 
 def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fused: bool = True,
-                     precision: str = "f32", input: str = "obs", learn: bool = True, refill_branch: bool = True):
+                     precision: str = "f32", input: str = "obs", learn: bool = True, refill_branch: bool = False):
     """TrainSegment captured once as a HIP graph (no host work per step) and
     replayed.  The host-side counters (action stream step, exploration draws,
     replay cursor) are baked into the capture, so replays repeat them: the

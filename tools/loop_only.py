@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--input", default="code", choices=("code", "obs"))
     ap.add_argument("--precision", default="f32", choices=("f32", "bf16"))
     ap.add_argument("--lib", default="", help="alternative library (tools/variants.py)")
-    ap.add_argument("--no-refill-branch", action="store_true", help="A/B: the refill inline on the one stream")
+    ap.add_argument("--refill-branch", action="store_true", help="A/B: the refill on its own graph branch")
     args = ap.parse_args()
     if args.lib:
         import dronerl_amd._native as nat
@@ -31,7 +31,7 @@ def main():
     env = BatchedDeliveryDrones(EnvParams(n_drones=N, grid_size=G), E)
     env.reset(seed=0)
     r = bench.train_loop_bench(env, args.segments, precision=args.precision, input=args.input,
-                               refill_branch=not args.no_refill_branch)
+                               refill_branch=args.refill_branch)
     print(json.dumps({k: r[k] for k in ("us_per_step", "precision", "input")}), flush=True)
 
 
