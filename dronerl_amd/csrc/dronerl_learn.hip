@@ -486,6 +486,9 @@ __device__ __forceinline__ void dq_update_weights(const LearnArgs& a, const DqW 
 //     packed image, target blend.
 // The tails are workgroups 0 and 1 so that they are dispatched first: every
 // wait in the kernel is on work that is already running.
+// TRAINED: the launch's plan (host-known: size >= batch) as a template parameter, so the trained instance has
+// no branch at its top that the compiler could sink the weight tile's loads below (they go out first)
+template <bool TRAINED>
 __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs args) {
     // the arguments read in place from the kernarg segment (a by-value parameter that inlined code takes
     // references to can be copied into private memory: 2.4 KB of scratch traffic per workgroup)
@@ -507,22 +510,29 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
     const int in = a.in[0], in4 = a.in4, xs0 = a.xs0, out0 = a.out[0];
     const int w0 = blockIdx.x - 2, net0 = w0 / (a.tiles0 > 0 ? a.tiles0 : 1);
     const int u00 = (w0 % (a.tiles0 > 0 ? a.tiles0 : 1)) * DQN_TILE, nu0 = min(DQN_TILE, out0 - u00);
-    const bool l0wg = a.trained && blockIdx.x >= 2;
+    const bool l0wg = TRAINED && blockIdx.x >= 2;
     const int nw0 = l0wg ? nu0 * in : 0;
     float w0r[DQN_W0R];
     {
-        const float* src = (net0 ? a.target : a.online) + a.woff[0] + (int64_t)u00 * in;
+        // unconditional loads at clamped indices (no exec-mask branch around them, so the counters' wait stays
+        // vmcnt(DQN_W0R) instead of vmcnt(0)); the tails read the online set's first float and discard it
+        const float* src = l0wg ? (net0 ? a.target : a.online) + a.woff[0] + (int64_t)u00 * in : a.online;
 #pragma unroll
         for (int q = 0; q < DQN_W0R; ++q) {
             const int e = threadIdx.x + q * DQN_THREADS;
-            w0r[q] = e < nw0 ? ((gcf32*)src)[e] : 0.0f;
+            const float v = ((gcf32*)src)[e < nw0 ? e : 0];
+            w0r[q] = e < nw0 ? v : 0.0f;
         }
     }
-    // a learner whose block carries the timeout flag does nothing until drl_dqn_init clears it: the aborted
-    // launch left granules tagged with this step's epoch and the arrive ticket part-counted
-    if (__hip_atomic_load((gu32*)&a.ctr->pad[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
-    // the counters as this step starts (the online tail writes them at the end)
+    // the counters as this step starts (the online tail writes them at the end): scalar loads (lgkmcnt), so
+    // the sample -> row-pointer chain below waits for them only, not for the weight tile issued before them
+    // (vmcnt), whose LDS store now follows the rows' staging
     DqnCounters ctr;
+    // (a learner whose block carries the timeout flag does nothing until drl_dqn_init clears it: the aborted
+    // launch left granules tagged with this step's epoch and the arrive ticket part-counted.  Each path returns
+    // before its first global write or hand-off; no early branch here, where the compiler would sink the weight
+    // loads above below it, behind this load)
+    const int32_t flag = a.ctr->pad[0];
     ctr.step = a.ctr->step;
     ctr.count = a.ctr->count;
     ctr.epsilon = a.ctr->epsilon;
@@ -536,7 +546,8 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
         a.stamps[1001] = wall_clock64();
     }
 #endif
-    if (!a.trained) {  // buffer.can_sample is false: no train_step this step (loss 0); the target blend when due
+    if constexpr (!TRAINED) {  // buffer.can_sample is false: no train_step this step (loss 0); the target blend when due
+        if (flag != 0) return;
         if (due)
             for (int64_t i = tid; i < a.n_params; i += nt) a.target[i] = dq_blend(a, a.online[i], a.target[i]);
         dq_finish(a, ctr, 0, 0.0f, 0.0f, 0.0f);
@@ -585,18 +596,20 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
             s_start[1] = nu;
             s_start[2] = nu + s_seg[1].n;
         }
+        for (int e = tid; e < B * (in4 - in); e += nt) X[(e / (in4 - in)) * in4 + in + e % (in4 - in)] = 0.0f;
+        __syncthreads();
+        DQ_STAMP(1);
+        dq_stage_segs(lds, s_seg, s_start, 2, s_tab);
+        // the registers' weights -> rows of xs0 (after the rows' loads are issued: the weights landed first)
 #pragma unroll
-        for (int q = 0; q < DQN_W0R; ++q) {  // the registers' weights -> rows of xs0
+        for (int q = 0; q < DQN_W0R; ++q) {
             const int e = tid + q * nt;
             if (e < nw0) {
                 const int r = (int)__umulhi((uint32_t)e, a.rm_in);
                 Wt[r * xs0 + (e - r * in)] = w0r[q];
             }
         }
-        for (int e = tid; e < B * (in4 - in); e += nt) X[(e / (in4 - in)) * in4 + in + e % (in4 - in)] = 0.0f;
-        __syncthreads();
-        DQ_STAMP(1);
-        dq_stage_segs(lds, s_seg, s_start, 2, s_tab);
+        if (flag != 0) return;  // (uniform; nothing written or handed off yet)
         __syncthreads();
         DQ_STAMP(2);
         // the online tile's columns of W_1 (it forms its own layer-0 deltas from them, 3. below): loaded into
@@ -809,6 +822,7 @@ __global__ void __launch_bounds__(DQN_THREADS) drl_dqn_train_kernel(LearnArgs ar
     }
 
     // ---- 2. the tails: workgroup 0 the online net, 1 the target net
+    if (flag != 0) return;
     const int n = blockIdx.x == 0 ? 0 : 1;
     const int mw = a.maxw;
     float* Pa = lds;                   // [B][mw] activations of the current layer
@@ -1001,15 +1015,15 @@ __global__ void drl_dqn_init_kernel(DqnCounters* c, float epsilon) {
 
 hipError_t launch_dqn_train(const LearnArgs& a, size_t lds, hipStream_t s) {
     if (a.trained)
-        hipLaunchKernelGGL(drl_dqn_train_kernel, dim3((unsigned)a.nblk0 + 2), dim3(DQN_THREADS), lds, s, a);
+        hipLaunchKernelGGL(drl_dqn_train_kernel<true>, dim3((unsigned)a.nblk0 + 2), dim3(DQN_THREADS), lds, s, a);
     else
-        hipLaunchKernelGGL(drl_dqn_train_kernel, dim3(1), dim3(DQN_THREADS), 0, s, a);
+        hipLaunchKernelGGL(drl_dqn_train_kernel<false>, dim3(1), dim3(DQN_THREADS), 0, s, a);
     return hipGetLastError();
 }
 
 int dqn_train_resident_capacity(size_t lds, int num_cus) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, drl_dqn_train_kernel, DQN_THREADS, lds) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, drl_dqn_train_kernel<true>, DQN_THREADS, lds) != hipSuccess)
         return -1;
     return per_cu * num_cus;
 }
