@@ -869,10 +869,12 @@ def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fus
                            "update and epsilon decay on the device (train_jax.py:68-98); us_per_launch_alone: 50 "
                            "launches back to back after the loop (latency-bound: DESIGN.md section 4 has the "
                            "phase times)",
-                   "parallelism": "one learner per rank, on that rank's env shard and replay (replicas): the "
-                                  "reference's sharded jit run trains one global learner, which would need the "
-                                  "sampled rows gathered across ranks every step (SURVEY.md section 8 E2; "
-                                  "DESIGN.md section 6)"}
+                   "parallelism": "one learner per rank, on that rank's env shard and replay (replicas). The "
+                                  "reference's sharded jit run trains one global learner: that mode is "
+                                  "dronerl_amd.global_learner (each rank's image of the one global ring, the "
+                                  "sampled rows gathered from their owners, ~2 KB all_gather per step; bit-exact "
+                                  "against one learner in tests/test_gpu_multirank.py), not timed here "
+                                  "(DESIGN.md section 6)"}
     branches = (("replay add_many" if fused else "synthetic actions and replay add_many") +
                 " on parallel graph branches, 3 rotating buffers" if parallel else
                 "one stream, the refill on its own graph branch" if loop.refill_branch else "one stream") + \
