@@ -25,6 +25,10 @@ def main():
                     help="envs per wave pass of the stamped code act (64: v4 kernel, 32: DRL_QN_CODE=2|3)")
     ap.add_argument("--flush", action="store_true",
                     help="overwrite 256 MB between launches (cold L2/MALL, as after a step) and time each launch")
+    ap.add_argument("--rewrite", action="store_true", help="with --flush: rewrite the input rows after the flush "
+                    "(freshly written, as the step leaves its codes)")
+    ap.add_argument("--repack", action="store_true", help="with --flush: re-pack the net after the flush "
+                    "(a freshly written packed image, as the learner leaves it)")
     args = ap.parse_args()
     if args.lib:
         import dronerl_amd._native as nat
@@ -55,8 +59,13 @@ def main():
     if args.flush:
         junk = torch.empty(64 << 20, dtype=torch.float32, device="cuda")
         tot = 0.0
+        keep = flat.clone() if args.rewrite else None
         for t in range(args.iters):
             junk.fill_(float(t))
+            if args.rewrite:
+                flat.copy_(keep)
+            if args.repack:
+                net.pack()
             e0.record()
             net.act(flat, 0.1, step=t, actions=a, synth=syn(t))
             e1.record()
