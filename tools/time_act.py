@@ -29,6 +29,8 @@ def main():
                     "(freshly written, as the step leaves its codes)")
     ap.add_argument("--repack", action="store_true", help="with --flush: re-pack the net after the flush "
                     "(a freshly written packed image, as the learner leaves it)")
+    ap.add_argument("--retouch", action="store_true", help="with --flush: rewrite the packed image with a torch "
+                    "copy (the same bytes, whole-line stores)")
     args = ap.parse_args()
     if args.lib:
         import dronerl_amd._native as nat
@@ -66,6 +68,8 @@ def main():
                 flat.copy_(keep)
             if args.repack:
                 net.pack()
+            if args.retouch:
+                net.packed.copy_(net.packed.clone())
             e0.record()
             net.act(flat, 0.1, step=t, actions=a, synth=syn(t))
             e1.record()
