@@ -416,12 +416,16 @@ static_assert(sizeof(DqnCounters) == 64, "drl_dqn_counters is 64 bytes");
 
 constexpr int DQN_MAX_BATCH = 64;
 constexpr int DQN_TILE = 8;       // layer-0 units per workgroup of the learner kernel
-constexpr int DQN_THREADS = 512;  // the learner kernel's workgroup
+#ifndef DRL_DQN_THREADS
+#define DRL_DQN_THREADS 512
+#endif
+constexpr int DQN_THREADS = DRL_DQN_THREADS;  // the learner kernel's workgroup (DRL_DQN_THREADS: A/B knob)
 constexpr int DQN_STAGE = 12;     // loads each thread keeps in flight when the learner stages data
 constexpr int DQN_MAX_SEGS = 28;  // copy segments of the learner kernel's prefetch
 constexpr int DQN_UB = 4;         // weights whose loads a thread issues together in the update phase
 constexpr int DQN_PF = 8;         // weights per thread whose operands are loaded before the epoch wait
-constexpr int DQN_W0R = 8;        // layer-0 tile weights per thread loaded into registers at the launch's start
+constexpr int DQN_W0R = 4096 / DQN_THREADS;  // layer-0 tile weights per thread in registers at the launch's start
+                                             // (a tile of 8 units x up to 512 inputs)
 
 // One segment of the learner kernel's one-round staging into LDS: element
 // i < n lands at LDS float dst + (pad ? (i / row) * (row + pad) + i % row :

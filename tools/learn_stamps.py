@@ -39,11 +39,12 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--build", action="store_true")
+    ap.add_argument("--lib", default="", help="another stamps build (default tools/var_dqnstamps.so)")
     args = ap.parse_args()
     if args.build:
         build()
         return
-    os.environ["DRL_LIB"] = LIB
+    os.environ["DRL_LIB"] = os.path.abspath(args.lib) if args.lib else LIB
     import numpy as np
     import torch
     import bench
