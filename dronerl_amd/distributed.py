@@ -73,10 +73,16 @@ def init_from_env(backend: Optional[str] = None):
 
 
 def allreduce_sum(t: torch.Tensor) -> torch.Tensor:
-    """In-place sum over ranks (no-op without an initialised process group)."""
+    """In-place sum over ranks (no-op without an initialised process group).
+    A device tensor under gloo is reduced through a host copy."""
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        if t.device.type != "cpu" and dist.get_backend() == "gloo":
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t
 
 
