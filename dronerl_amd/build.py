@@ -26,9 +26,19 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
+
+
 def compile_cmd(out: str):
-    return [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-            "-Wno-unused-function", "-I", os.path.join(REPO, "include"), "-o", out] + SOURCES
+    """The whole library in one hipcc command (tools/variants.py's form)."""
+    return [hipcc(), f"--offload-arch={ARCH}"] + FLAGS + ["-shared", "-I", os.path.join(REPO, "include"),
+                                                         "-o", out] + SOURCES
+
+
+def object_cmd(src: str, obj: str):
+    """One translation unit (host + gfx950 device code) -> an object; every kernel is launched from its own
+    unit, so the units link as they are (no relocatable device code)."""
+    return [hipcc(), f"--offload-arch={ARCH}"] + FLAGS + ["-c", "-I", os.path.join(REPO, "include"), "-o", obj, src]
 
 
 def source_digest() -> str:
@@ -56,11 +66,26 @@ def build(force: bool = False, verbose: bool = False) -> str:
     library whose digest does not match the sources beside it)."""
     if not force and up_to_date():
         return LIB
-    cmd = compile_cmd(LIB + ".tmp")
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
     digest = source_digest()
-    subprocess.run(cmd, check=True)
+    with tempfile.TemporaryDirectory(prefix="drl_build_") as tmp:
+        objs = [os.path.join(tmp, os.path.basename(src) + ".o") for src in SOURCES]
+        cmds = [object_cmd(src, obj) for src, obj in zip(SOURCES, objs)]
+        if verbose:
+            for c in cmds:
+                print(" ".join(c), file=sys.stderr)
+        # the units compile in parallel (the kernels' unit dominates the wall time)
+        with ThreadPoolExecutor(max(1, min(len(cmds), os.cpu_count() or 1))) as ex:
+            for r in ex.map(lambda c: subprocess.run(c, capture_output=not verbose, text=True), cmds):
+                if r.returncode:
+                    if not verbose:  # (the compiler's messages, which were captured)
+                        sys.stderr.write((r.stdout or "") + (r.stderr or ""))
+                    raise subprocess.CalledProcessError(r.returncode, r.args, r.stdout, r.stderr)
+        link = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs
+        if verbose:
+            print(" ".join(link), file=sys.stderr)
+        subprocess.run(link, check=True)
     os.replace(LIB + ".tmp", LIB)
     with open(HASH, "w") as f:
         f.write(digest + "\n")
