@@ -38,22 +38,39 @@ class TrainResult:
 
 def train(params: EnvParams, num_envs: int, num_steps: int, hidden: Sequence[int] = (128, 64), hp=None,
           reset_env_every: int = 100, memory_size: int = 100_000, seed: int = 0, env_offset: int = 0,
-          action_seed: int = 2024, act_seed: int = 7, device=None) -> TrainResult:
+          action_seed: int = 2024, act_seed: int = 7, device=None, rank: int = 0, world: int = 1,
+          group=None) -> TrainResult:
     """train_jax.py's training loop (see the module docstring).  hp: a
     dqn.DQNHParams (default: train_jax.py's defaults with num_steps, so
-    epsilon decays as :133-134 schedules it)."""
+    epsilon decays as :133-134 schedules it).
+
+    world > 1 (one process per GPU, an initialised torch.distributed group):
+    train_jax.py --use_sharding (:196-212) -- this rank steps envs
+    rank * num_envs / world .. (num_envs % world == 0, :401-402), the one
+    replay ring is sharded (global_learner.ShardedReplay) and every rank runs
+    the same learner; env_offset is then ignored.  The returned rate counts
+    every rank's envs."""
     from .dqn import DQNHParams, DQNLearner, QNetwork, ReplayBuffer
+    from .distributed import shard_envs
     from .env import BatchedDeliveryDrones
+    from .global_learner import ShardedReplay
     if num_steps < 1 or reset_env_every < 1:
         raise ValueError("num_steps and reset_env_every must be >= 1")
-    env = BatchedDeliveryDrones(params, num_envs, device=device, env_offset=env_offset)
+    shard = shard_envs(num_envs, rank, world) if world > 1 else None
+    env = BatchedDeliveryDrones(params, shard.num_envs if shard else num_envs, device=device,
+                                env_offset=shard.env_offset if shard else env_offset)
     env.reset(seed=seed)
     dev, E, N = env.device, env.num_envs, env.n_drones
     r = params.window_radius
     D = (2 * r + 1) ** 2 * 6
     net = QNetwork(D, tuple(hidden), device=dev, generator=torch.Generator().manual_seed(seed), input="code")
     learner = DQNLearner(net, hp or DQNHParams(num_steps=num_steps), generator=torch.Generator().manual_seed(seed + 1))
-    rb = ReplayBuffer(memory_size, D, dev, code_radius=r)
+    if shard:
+        rb = ShardedReplay(memory_size, D, dev, num_envs, shard.env_offset, shard.num_envs, rank, world,
+                           code_radius=r, group=group)
+        ring = rb.ring
+    else:
+        rb = ring = ReplayBuffer(memory_size, D, dev, code_radius=r)
     code = [env.new_code(), env.new_code()]
     env.get_code(out=code[0])
     acts = torch.empty((E, N), dtype=torch.int32, device=dev)
@@ -65,8 +82,13 @@ def train(params: EnvParams, num_envs: int, num_steps: int, hidden: Sequence[int
         b, nb = t & 1, (t + 1) & 1
         net.act(code[b], learner.epsilon, seed=act_seed, step=t, env_offset=env.env_offset, actions=acts,
                 synth=(action_seed, t))
-        env.step(acts, rewards=rew, dones=don, code=code[nb], replay=rb, replay_obs=code[b])
-        learner.train(rb)
+        if shard:
+            env.step(acts, rewards=rew, dones=don, code=code[nb])
+            rb.add_many(code[b], acts, rew, code[nb], don)
+            rb.gather(learner)
+        else:  # (the step lands its transitions in the ring itself: drl_step_code_replay)
+            env.step(acts, rewards=rew, dones=don, code=code[nb], replay=rb, replay_obs=code[b])
+        learner.train(ring)
         if t % reset_env_every == 0:  # train_jax.py:101-113 (step 0 included)
             env.reset(seed=None)
             env.get_code(out=code[nb])
@@ -76,7 +98,10 @@ def train(params: EnvParams, num_envs: int, num_steps: int, hidden: Sequence[int
     net.check_errors()
     learner.check_errors()
     dt = e0.elapsed_time(e1) / 1e3
-    return TrainResult(env, net, learner, rb, num_steps, E * num_steps / dt)
+    if world > 1:
+        from .distributed import max_over_ranks
+        dt = max_over_ranks(dt, device=dev if torch.distributed.get_backend(group) == "nccl" else None)
+    return TrainResult(env, net, learner, ring, num_steps, num_envs * num_steps / dt)
 
 
 def greedy_policy(qnet):
@@ -99,3 +124,127 @@ def evaluate(params: EnvParams, qnet, num_evals: int = 5, num_eval_steps: int = 
     run = gpu_episode_runner(params, num_eval_steps, eval_seed, policy=greedy_policy(qnet), action_seed=eval_seed,
                              device=device)
     return evaluate_sharded(run, num_evals, rank, world, device=device)
+
+
+def parse_args(argv=None):
+    """train_jax.py's command line (:335-390) for the options this driver
+    implements: the env, training and eval options and
+    --save_final_checkpoint; the dense net's widths must be multiples of 32
+    in [32, 128] (the device act's tiles), so --hidden_layers defaults to the
+    benchmark net (128, 64) instead of (16, 16).  --use_sharding runs under
+    torchrun (one process per GPU)."""
+    import argparse
+    ap = argparse.ArgumentParser(formatter_class=argparse.ArgumentDefaultsHelpFormatter)
+    ap.add_argument("--n_drones", type=int, default=4)
+    ap.add_argument("--grid_size", type=int, default=9)
+    ap.add_argument("--window_radius", type=int, default=3)
+    ap.add_argument("--packets_factor", type=int, default=3)
+    ap.add_argument("--dropzones_factor", type=int, default=2)
+    ap.add_argument("--stations_factor", type=int, default=2)
+    ap.add_argument("--skyscrapers_factor", type=int, default=3)
+    ap.add_argument("--num_envs", type=int, default=1)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--num_steps", type=int, default=1000)
+    ap.add_argument("--batch_size", type=int, default=8)
+    ap.add_argument("--learning_rate", type=float, default=1e-3)
+    ap.add_argument("--memory_size", type=int, default=100_000)
+    ap.add_argument("--epsilon_start", type=float, default=1.0)
+    ap.add_argument("--epsilon_decay", type=float, default=None)
+    ap.add_argument("--epsilon_decay_half_life_fraction", type=float, default=0.2)
+    ap.add_argument("--epsilon_end", type=float, default=0.01)
+    ap.add_argument("--epsilon_decay_every", type=int, default=5)
+    ap.add_argument("--target_update_interval", type=int, default=10)
+    ap.add_argument("--gamma", type=float, default=0.9)
+    ap.add_argument("--reset_env_every", type=int, default=100)
+    ap.add_argument("--tau", type=float, default=1.0)
+    ap.add_argument("--save_final_checkpoint", action="store_true", default=False)
+    ap.add_argument("--use_sharding", action="store_true", default=False)
+    ap.add_argument("--network_type", choices=["dense"], default="dense")
+    ap.add_argument("--hidden_layers", nargs="+", type=int, default=(128, 64))
+    ap.add_argument("--pickup_reward", type=float, default=0.0)
+    ap.add_argument("--delivery_reward", type=float, default=1.0)
+    ap.add_argument("--crash_reward", type=float, default=-1.0)
+    ap.add_argument("--charge_reward", type=float, default=-0.1)
+    ap.add_argument("--eval_n_drones", type=int, default=None)
+    ap.add_argument("--eval_grid_size", type=int, default=None)
+    ap.add_argument("--eval_seed", type=int, default=0)
+    ap.add_argument("--num_eval_steps", type=int, default=10_000)
+    ap.add_argument("--num_evals", type=int, default=5)
+    ap.add_argument("--output_dir", default="output")
+    args = ap.parse_args(argv)
+    # train_jax.py:393-402's validations
+    if args.num_envs <= 0:
+        raise ValueError("Number of envs need to be at least 1")
+    if args.num_steps <= 0:
+        raise ValueError("Number of steps need to be at least 1")
+    if args.use_sharding and args.num_envs <= 1:
+        raise ValueError("When using --use_sharding you need to provide num_envs > 1")
+    return args
+
+
+def env_params_of(args, eval_env: bool = False) -> EnvParams:
+    n = args.eval_n_drones if eval_env and args.eval_n_drones is not None else args.n_drones
+    g = args.eval_grid_size if eval_env and args.eval_grid_size is not None else args.grid_size
+    return EnvParams(n_drones=n, grid_size=g, window_radius=args.window_radius, pickup_reward=args.pickup_reward,
+                     delivery_reward=args.delivery_reward, crash_reward=args.crash_reward,
+                     charge_reward=args.charge_reward, packets_factor=args.packets_factor,
+                     dropzones_factor=args.dropzones_factor, stations_factor=args.stations_factor,
+                     skyscrapers_factor=args.skyscrapers_factor)
+
+
+def hparams_of(args):
+    from .dqn import DQNHParams
+    if args.epsilon_decay is None:  # train_jax.py:133-134
+        decay = (1 - 0.5 * (1 - args.epsilon_end / args.epsilon_start)) ** (
+            1 / (args.epsilon_decay_half_life_fraction * args.num_steps))
+    else:
+        decay = args.epsilon_decay
+    return DQNHParams(batch=args.batch_size, gamma=args.gamma, learning_rate=args.learning_rate, tau=args.tau,
+                      target_update_interval=args.target_update_interval, epsilon_start=args.epsilon_start,
+                      epsilon_decay=decay, epsilon_end=args.epsilon_end,
+                      epsilon_decay_every=args.epsilon_decay_every, num_steps=args.num_steps,
+                      sample_seed=args.seed)
+
+
+def main(argv=None) -> dict:
+    """`python -m dronerl_amd.train [train_jax.py options]`: train, save
+    (train_jax.py:238-244: agent_<n>_steps_jax / _torch.safetensors under
+    output/jax_run_<time>), evaluate (:247-256).  Returns the metrics."""
+    import json
+    import os
+    from datetime import datetime
+
+    from .checkpoint import read_checkpoint, to_qnet
+    from .distributed import init_from_env
+    args = parse_args(argv)
+    rank, world, local = init_from_env() if args.use_sharding else (0, 1, 0)
+    if args.use_sharding and args.num_envs % world:
+        raise ValueError(f"The number of envs (={args.num_envs}) needs to be divisible by the number of devices "
+                         f"(={world})")
+    dev = torch.device("cuda", local if world > 1 else torch.cuda.current_device())
+    res = train(env_params_of(args), args.num_envs, args.num_steps, hidden=tuple(args.hidden_layers),
+                hp=hparams_of(args), reset_env_every=args.reset_env_every, memory_size=args.memory_size,
+                seed=args.seed, device=dev, rank=rank, world=world)
+    metrics = {"obs_per_sec": res.env_steps_per_s, "time_taken": args.num_envs * args.num_steps / res.env_steps_per_s,
+               "num_gpus": world}
+    run_dir = os.path.join(args.output_dir, f"jax_run_{datetime.now().strftime('%Y%m%d_%H%M%S')}")
+    if args.save_final_checkpoint and rank == 0:
+        os.makedirs(run_dir, exist_ok=True)
+        for fmt in ("jax", "torch"):
+            path = os.path.join(run_dir, f"agent_{args.num_steps}_steps_{fmt}.safetensors")
+            res.learner.save(path, format=fmt)
+            metrics[f"checkpoint_{fmt}"] = path
+    # the final eval with the trained net (the online parameters, as eval_jax uses ag_state)
+    from .dqn import QNetwork
+    qnet = QNetwork(res.net.in_features, res.net.hidden, device=dev, precision="f32")
+    qnet.load(*zip(*res.learner.params("online")))
+    (am, asd), (rm, rsd), _ = evaluate(env_params_of(args, eval_env=True), qnet, args.num_evals, args.num_eval_steps,
+                                      args.eval_seed, rank=rank, world=world, device=dev)
+    metrics.update(eval_reward_mean=am, eval_reward_std=asd, random_reward_mean=rm, random_reward_std=rsd)
+    if rank == 0:
+        print(json.dumps(metrics), flush=True)
+    return metrics
+
+
+if __name__ == "__main__":
+    main()

@@ -169,3 +169,21 @@ def test_global_learner_scheme_two_ranks_equal_one_learner_oracle(cap):
         for k in ("online", "target", "m", "v"):
             assert np.array_equal(res[r][k].view(np.uint32), ref[k].view(np.uint32)), (r, k)
         assert res[r]["counters"] == ref["counters"]
+
+
+def test_train_cli_mirrors_train_jax():
+    """dronerl_amd.train's command line: train_jax.py's option names and
+    defaults (:335-390), its epsilon-decay formula (:133-134) and its
+    validations (:393-402)."""
+    from dronerl_amd import train as T
+    a = T.parse_args([])
+    assert (a.n_drones, a.grid_size, a.window_radius, a.num_envs, a.num_steps, a.batch_size) == (4, 9, 3, 1, 1000, 8)
+    assert (a.memory_size, a.gamma, a.target_update_interval, a.reset_env_every, a.tau) == (100_000, 0.9, 10, 100, 1.0)
+    hp = T.hparams_of(a)
+    assert hp.epsilon_decay == pytest.approx((1 - 0.5 * (1 - 0.01 / 1.0)) ** (1 / (0.2 * 1000)), rel=0, abs=0)
+    assert hp.batch == 8 and hp.learning_rate == 1e-3 and hp.epsilon_decay_every == 5
+    p = T.env_params_of(T.parse_args(["--eval_grid_size", "16", "--eval_n_drones", "8"]), eval_env=True)
+    assert (p.side, p.n_drones) == (16, 8)
+    for bad in (["--num_envs", "0"], ["--num_steps", "0"], ["--use_sharding", "--num_envs", "1"]):
+        with pytest.raises(ValueError):
+            T.parse_args(bad)

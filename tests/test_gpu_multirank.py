@@ -235,3 +235,46 @@ def test_global_learner_two_ranks_equal_one_learner(E, cap):
         for k in ("online", "target", "m", "v", "packed"):
             assert np.array_equal(res[r][k].view(np.uint32), ref[k].view(np.uint32)), (r, k)
         assert res[r]["counters"] == ref["counters"], r
+
+
+def _train_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+    from dronerl_amd import EnvParams
+    from dronerl_amd.dqn import DQNHParams
+    from dronerl_amd.train import train
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = train(EnvParams(n_drones=4, grid_size=9), 256, 30, hp=DQNHParams(num_steps=30), reset_env_every=10,
+                    memory_size=1000, device="cuda:0", rank=rank, world=world)
+        out[rank] = {k: res.learner.sets[k].cpu().numpy().copy() for k in ("online", "target", "m", "v")}
+    finally:
+        dist.destroy_process_group()
+
+
+def test_train_use_sharding_equals_one_process():
+    """dronerl_amd.train.train with world = 2 (train_jax.py --use_sharding:
+    the envs sharded, the one replay ring sharded, the same learner on every
+    rank) == world = 1 over the same 256 envs, bit for bit, through resets."""
+    from dronerl_amd import EnvParams
+    from dronerl_amd.dqn import DQNHParams
+    from dronerl_amd.train import train
+    ref = train(EnvParams(n_drones=4, grid_size=9), 256, 30, hp=DQNHParams(num_steps=30), reset_env_every=10,
+                memory_size=1000, device="cuda:0")
+    want = {k: ref.learner.sets[k].cpu().numpy() for k in ("online", "target", "m", "v")}
+    ctx = mp.get_context("spawn")
+    with ctx.Manager() as man:
+        out = man.dict()
+        port = _free_port()
+        procs = [ctx.Process(target=_train_worker, args=(r, 2, port, out)) for r in range(2)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=300)
+            assert p.exitcode == 0, p.exitcode
+        res = dict(out)
+    for r in range(2):
+        for k, v in want.items():
+            assert np.array_equal(res[r][k].view(np.uint32), v.view(np.uint32)), (r, k)

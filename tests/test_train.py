@@ -49,3 +49,17 @@ def test_trained_agent_saves_reloads_and_beats_random(tmp_path):
     print(f"eval after 300 steps: agent {agent[0]:.4f} +- {agent[1]:.4f}, random {rnd[0]:.4f} +- {rnd[1]:.4f}")
     assert table.shape == (5, 2)
     assert agent[0] > rnd[0] + 0.05, (agent, rnd)  # measured: -0.093 against -0.192
+
+
+def test_train_main_cli_end_to_end(tmp_path):
+    """`python -m dronerl_amd.train` (train_jax.py's options): train, save the
+    jax and torch checkpoints under output_dir/jax_run_*, run the final eval."""
+    from dronerl_amd.checkpoint import read_checkpoint
+    from dronerl_amd.train import main
+    m = main(["--num_envs", "512", "--num_steps", "60", "--hidden_layers", "64", "32", "--save_final_checkpoint",
+              "--num_evals", "3", "--num_eval_steps", "200", "--output_dir", str(tmp_path)])
+    assert m["obs_per_sec"] > 0 and m["num_gpus"] == 1
+    for fmt in ("jax", "torch"):
+        ck = read_checkpoint(m[f"checkpoint_{fmt}"])
+        assert ck.dense_layers == (64, 32) and m[f"checkpoint_{fmt}"].endswith(f"agent_60_steps_{fmt}.safetensors")
+    assert -1.0 <= m["eval_reward_mean"] <= 1.0 and -1.0 <= m["random_reward_mean"] <= 1.0
