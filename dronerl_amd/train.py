@@ -243,6 +243,8 @@ def main(argv=None) -> dict:
     metrics.update(eval_reward_mean=am, eval_reward_std=asd, random_reward_mean=rm, random_reward_std=rsd)
     if rank == 0:
         print(json.dumps(metrics), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
     return metrics
 
 
