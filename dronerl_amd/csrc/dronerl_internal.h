@@ -92,9 +92,10 @@ constexpr int np(int n_drones) { return (n_drones + 7) / 8 * 8; }             //
 constexpr int pstride(int side) { return r16((side * side + 1) / 2); }         // HBM ground bytes per env
 constexpr int gstride(int side) { return 2 * pstride(side); }                  // byte-per-cell image bytes per env
 // drl_step's LDS image of the ground: a byte per cell below DRL_GL_NIB_MIN_SIDE, the packed nibbles (the HBM
-// row as is: half the LDS, so more waves fit a CU) from there on (round 6: C5's 64 x 64 envs)
+// row as is: half the LDS, so more waves fit a CU) from there on (round 6: C5's 64 x 64 envs, then C4's
+// 32 x 32: 41.2 -> 39.7 us; at C3's 16 x 16 it measured slower, 29.3 -> 31.5 us, tools/ab.py)
 #ifndef DRL_GL_NIB_MIN_SIDE
-#define DRL_GL_NIB_MIN_SIDE 64
+#define DRL_GL_NIB_MIN_SIDE 32
 #endif
 constexpr bool gl_nib(int side) { return side >= DRL_GL_NIB_MIN_SIDE; }
 constexpr int glstride(int side) { return gl_nib(side) ? pstride(side) : gstride(side); }  // LDS ground bytes per env
