@@ -789,7 +789,10 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
 #define DRL_SHFL_BATCH 16
 #endif
     constexpr int CH = P < DRL_SHFL_BATCH ? P : DRL_SHFL_BATCH;  // shuffle batch
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
+    // this wave's LDS image (workgroups of one wave, or of step_wpb(P) waves: see drl_step_kernel)
+    unsigned char* const smem = smem_all + (size_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) *
+                                               (size_t)((a.wave_lds + 15) & ~15);
     const GEO g{a};
     const int lane0 = threadIdx.x & 63;
     const int grp0 = lane0 / P;
@@ -1478,11 +1481,23 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t orig, uint32_t n) {
 #ifndef DRL_STEP_WAVES_P32
 #define DRL_STEP_WAVES_P32 1
 #endif
+// (DRL_STEP_WPB_P16 / _P32: waves per workgroup of the 16- / 32-lane instances, each wave its own batch and
+// LDS image, no workgroup barrier; 1 = one-wave workgroups)
+#ifndef DRL_STEP_WPB_P16
+#define DRL_STEP_WPB_P16 1
+#endif
+#ifndef DRL_STEP_WPB_P32
+#define DRL_STEP_WPB_P32 1
+#endif
+constexpr int step_wpb(int P) { return P == 32 ? DRL_STEP_WPB_P32 : P == 16 ? DRL_STEP_WPB_P16 : 1; }
 template <int P, class GEO, bool NT, bool CODE = false, bool RING = false>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64 * step_wpb(P))
 __attribute__((amdgpu_waves_per_eu(P <= 8 ? 8 : (P == 32 ? DRL_STEP_WAVES_P32 : P == 16 ? DRL_STEP_WAVES_P16 : 1), 8)))
 drl_step_kernel(StepArgs a) {
-    step_batch<P, GEO, false, NT, CODE, RING>(a, (int64_t)xcd_block(blockIdx.x, gridDim.x) * (64 / P));
+    constexpr int WPB = step_wpb(P);
+    const int64_t batch = WPB == 1 ? (int64_t)xcd_block(blockIdx.x, gridDim.x)
+                                   : (int64_t)blockIdx.x * WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    step_batch<P, GEO, false, NT, CODE, RING>(a, batch * (64 / P));
 }
 
 // drl_rollout: a.steps steps per launch, same wave layout (P >= 16).
@@ -2499,6 +2514,9 @@ template <int P, class GEO>
 static hipError_t launch_step_t(const StepArgs& a, hipStream_t s, int mode) {
     const int64_t blocks = (a.E + (64 / P) - 1) / (64 / P);
     const dim3 grid((unsigned)blocks), block(64);
+    constexpr int WPB = step_wpb(P);  // drl_step_kernel's workgroups (the obs and rollout kernels: one wave)
+    const dim3 sgrid((unsigned)((blocks + WPB - 1) / WPB)), sblock(64 * WPB);
+    const size_t slds = WPB == 1 ? (size_t)a.wave_lds : (size_t)WPB * (size_t)((a.wave_lds + 15) & ~15);
     if (mode == kObsMode) {
         if constexpr (GEO::kObs) hipLaunchKernelGGL((drl_obs_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
         else return hipErrorInvalidValue;
@@ -2506,14 +2524,14 @@ static hipError_t launch_step_t(const StepArgs& a, hipStream_t s, int mode) {
         if constexpr (P >= kRolloutNoObsMinLanes) hipLaunchKernelGGL((drl_rollout_kernel<P, GEO>), grid, block, a.wave_lds, s, a);
         else return hipErrorInvalidValue;
     } else if (GEO::kObs && a.code && a.ring_next) {  // drl_step_code_replay (no f32 observation)
-        hipLaunchKernelGGL((drl_step_kernel<P, GEO, false, GEO::kObs, GEO::kObs>), grid, block, a.wave_lds, s, a);
+        hipLaunchKernelGGL((drl_step_kernel<P, GEO, false, GEO::kObs, GEO::kObs>), sgrid, sblock, slds, s, a);
     } else if (GEO::kObs && a.code) {  // (obs NULL: the code alone)
-        if (a.obs_nt) hipLaunchKernelGGL((drl_step_kernel<P, GEO, GEO::kObs, GEO::kObs>), grid, block, a.wave_lds, s, a);
-        else hipLaunchKernelGGL((drl_step_kernel<P, GEO, false, GEO::kObs>), grid, block, a.wave_lds, s, a);
+        if (a.obs_nt) hipLaunchKernelGGL((drl_step_kernel<P, GEO, GEO::kObs, GEO::kObs>), sgrid, sblock, slds, s, a);
+        else hipLaunchKernelGGL((drl_step_kernel<P, GEO, false, GEO::kObs>), sgrid, sblock, slds, s, a);
     } else if (GEO::kObs && a.obs && a.obs_nt) {
-        hipLaunchKernelGGL((drl_step_kernel<P, GEO, GEO::kObs>), grid, block, a.wave_lds, s, a);
+        hipLaunchKernelGGL((drl_step_kernel<P, GEO, GEO::kObs>), sgrid, sblock, slds, s, a);
     } else {
-        hipLaunchKernelGGL((drl_step_kernel<P, GEO, false>), grid, block, a.wave_lds, s, a);
+        hipLaunchKernelGGL((drl_step_kernel<P, GEO, false>), sgrid, sblock, slds, s, a);
     }
     return hipGetLastError();
 }
