@@ -502,6 +502,50 @@ def test_learner_handoff_timeout_is_reported_and_refused(monkeypatch):
 
 
 @gpu
+def test_learner_beside_co_running_kernels():
+    """the learner's workgroups hand off to each other, so
+    they must all become resident.  Each learner step here is launched on its
+    own stream while a second stream keeps the device full: C5-sized env steps
+    (131,072 envs, one-wave workgroups holding LDS on every CU) and a 1 GiB
+    copy.  Every step still completes bit-exact against the oracle, with no
+    hand-off timeout."""
+    from dronerl_amd import BatchedDeliveryDrones, EnvParams
+    env, net, learner, rb, hp = _learner_setup((294, 128, 64, 5), "code", dict(batch=8), E=64, cap=300)
+    st, ohp = state_from_learner(learner), oracle_hparams(hp)
+    big = BatchedDeliveryDrones(EnvParams(n_drones=32, grid_size=64), 131072)
+    big.reset(seed=2)
+    src = torch.empty(1 << 28, dtype=torch.float32, device="cuda").fill_(1.0)
+    dst = torch.empty_like(src)
+    busy, side = torch.cuda.Stream(), torch.cuda.Stream()
+    cur, nxt = env.new_code(), env.new_code()
+    env.get_code(out=cur)
+    acts = torch.empty((64, 8), dtype=torch.int32, device="cuda")
+    for t in range(6):
+        net.act(cur, learner.epsilon, seed=3, step=t, actions=acts, synth=(5, t))
+        r, d = env.step(acts, code=nxt)
+        rb.add_many(cur, acts, r, nxt, d)
+        torch.cuda.synchronize()
+        O.learner_step(st, ohp, _host(rb.obs), _host(rb.next_obs), _host(rb.actions), _host(rb.rewards),
+                       _host(rb.dones), rb.size, 7)
+        # even steps: the learner goes in while the env steps run (the host
+        # enqueues faster than they execute); odd steps: behind the copy
+        for k in range(12):
+            with torch.cuda.stream(busy):
+                if t % 2 and k == 0:
+                    dst.copy_(src)
+                big.step(big.synth_actions(seed=9, step=12 * t + k))
+            if k == 6:
+                with torch.cuda.stream(side):
+                    learner.train(rb)
+        torch.cuda.synchronize()
+        learner.check_errors()
+        assert_same(learner, st, f"co-running, step {t}")
+        cur, nxt = nxt, cur
+    big.check_errors()
+    assert learner.counters()["count"] == 6
+
+
+@gpu
 @pytest.mark.parametrize("inp", ["code", "obs"])
 def test_learner_matches_torch_restatement_50_steps(inp):
     """VERDICT r4 item 1's check: 50 device learner steps (train_jax defaults:
