@@ -639,7 +639,8 @@ class TrainSegment:
 
     def __init__(self, env, seg: int, parallel: bool = False, net=None, rb=None, fused: bool = True,
                  precision: str = "f32", input: str = "obs", learn: bool = True, capacity: int = MEMORY_SIZE,
-                 hp=None, fuse_replay=None, refill_branch: bool = False):
+                 hp=None, fuse_replay=None, refill_branch: bool = False, synth_branch: bool = False,
+                 synth_in_step=None):
         from dronerl_amd.dqn import DQNHParams, DQNLearner, QNetwork, ReplayBuffer
         E, N, dev = env.num_envs, env.n_drones, env.device
         W = env.layout.obs_window
@@ -658,7 +659,20 @@ class TrainSegment:
         if fuse_replay and (input != "code" or parallel):
             raise ValueError("fuse_replay needs input='code' and parallel=False")
         self.fuse_replay = fuse_replay
+        # synth_in_step (with fuse_replay; the default there): the fused step draws drones 1..N-1's synthetic
+        # actions itself (drl_step_code_replay_synth) and the act writes drone 0's column only -- the act no
+        # longer computes and writes N - 1 columns that the step reads back
+        if synth_in_step is None:
+            synth_in_step = fuse_replay and not synth_branch
+        if synth_in_step and not fuse_replay:
+            raise ValueError("synth_in_step needs the fused replay step")
+        self.synth_in_step = synth_in_step
         self.refill_branch = refill_branch  # (one stream: the refill on its own graph branch, see run)
+        # synth_branch (one stream, unfused): the synthetic actions of step t + 1 on their own graph branch,
+        # forked after step t and joined before act t + 1, so they run beside learner t (see run)
+        if synth_branch and (fused or parallel):
+            raise ValueError("synth_branch needs fused=False and parallel=False")
+        self.synth_branch = synth_branch
         # parallel branches need 3 rotating buffers (see above); on one stream 2
         # suffice, and the third 77 MB observation buffer costs MALL hits (C3
         # loop 79.4 vs 74.4 us per step)
@@ -692,12 +706,12 @@ class TrainSegment:
         x = self.code[b] if self.input == "code" else self.obs[b].reshape(self.E, -1)
         eps = self.learner.epsilon if self.learner is not None else 0.1
         self.net.act(x, eps, seed=7, step=t, env_offset=self.env.env_offset,
-                     actions=self.acts[b], synth=(2024, t) if self.fused else None)
+                     actions=self.acts[b], synth=(2024, t) if self.fused and not self.synth_in_step else None)
         if before_step is not None:  # (parallel: the refill branch joins here)
             before_step()
         if self.fuse_replay:
             self.env.step(self.acts[b], rewards=self.rewards[b], dones=self.dones[b], code=self.code[nb],
-                          replay=self.rb, replay_obs=self.code[b])
+                          replay=self.rb, replay_obs=self.code[b], synth=(2024, t) if self.synth_in_step else None)
         elif self.input == "code":
             self.env.step(self.acts[b], rewards=self.rewards[b], dones=self.dones[b], code=self.code[nb])
         else:
@@ -750,6 +764,26 @@ class TrainSegment:
             finally:
                 self.env.refill_every = every
                 self.env._since_refill = since
+        elif not self.parallel and self.synth_branch:
+            # acts[(t + 1) % 2] was last read by step t - 1, which precedes the fork after step t
+            def fork(t):
+                ev = torch.cuda.Event()
+                ev.record(main)
+                with torch.cuda.stream(self.s_syn):
+                    self.s_syn.wait_event(ev)
+                    self._synth(t)
+                    done = torch.cuda.Event()
+                    done.record(self.s_syn)
+                return done
+            ev_syn = fork(0)
+            for t in range(self.seg):
+                main.wait_event(ev_syn)  # (the act writes column 0 of the same rows)
+                self._act_step(t)
+                self._replay(t)
+                if t + 1 < self.seg:
+                    ev_syn = fork(t + 1)
+                self._learn()
+            main.wait_stream(self.s_syn)
         elif not self.parallel:
             for t in range(self.seg):
                 if not self.fused:
@@ -813,7 +847,8 @@ class TrainSegment:
 
 
 def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fused: bool = True,
-                     precision: str = "f32", input: str = "obs", learn: bool = True, refill_branch: bool = False):
+                     precision: str = "f32", input: str = "obs", learn: bool = True, refill_branch: bool = False,
+                     synth_branch: bool = False, synth_in_step=None):
     """TrainSegment captured once as a HIP graph (no host work per step) and
     replayed.  The host-side counters (action stream step, exploration draws,
     replay cursor) are baked into the capture, so replays repeat them: the
@@ -822,7 +857,7 @@ def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fus
     device and continue across replays."""
     dev = env.device
     loop = TrainSegment(env, seg, parallel=parallel, fused=fused, precision=precision, input=input, learn=learn,
-                        refill_branch=refill_branch)
+                        refill_branch=refill_branch, synth_branch=synth_branch, synth_in_step=synth_in_step)
     side = torch.cuda.Stream(dev)
     side.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(side):

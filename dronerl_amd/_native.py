@@ -40,6 +40,7 @@ EXPORTS = ["drl_abi_version", "drl_last_error", "drl_side_from_density", "drl_la
            # DQN consumer
            "drl_qnet_packed_bytes", "drl_qnet_pack", "drl_qnet_act", "drl_qnet_act_synth", "drl_qnet_act_code",
            "drl_replay_add", "drl_qnet_act_eps", "drl_step_code_replay",
+           "drl_step_code_replay_synth",
            # DQN learner (train_step / update_target / update_epsilon / sample)
            "drl_dqn_layout_query", "drl_dqn_init", "drl_dqn_train", "drl_dqn_train_fresh", "drl_dqn_sample_rows",
            # measurement helper (the measured copy-kernel peak)

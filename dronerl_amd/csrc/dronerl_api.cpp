@@ -388,9 +388,31 @@ int drl_step_code(const drl_params* p, const drl_state* s, const int32_t* d_acti
     return step_code_impl(p, s, d_actions, d_rewards, d_dones, d_obs, obs_k, d_code, d_err, flags, stream, nullptr);
 }
 
+static int step_code_replay_impl(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
+                                 uint8_t* d_dones, void* d_code, const void* d_code_prev, const drl_replay* r,
+                                 int64_t cursor, int32_t* d_err, uint32_t flags, hipStream_t stream, int synth,
+                                 uint64_t synth_seed, uint64_t synth_step, int64_t env_offset);
+
 int drl_step_code_replay(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
                          uint8_t* d_dones, void* d_code, const void* d_code_prev, const drl_replay* r, int64_t cursor,
                          int32_t* d_err, uint32_t flags, hipStream_t stream) {
+    return step_code_replay_impl(p, s, d_actions, d_rewards, d_dones, d_code, d_code_prev, r, cursor, d_err, flags,
+                                 stream, 0, 0, 0, 0);
+}
+
+int drl_step_code_replay_synth(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
+                               uint8_t* d_dones, void* d_code, const void* d_code_prev, const drl_replay* r,
+                               int64_t cursor, uint64_t synth_seed, uint64_t synth_step, int64_t env_offset,
+                               int32_t* d_err, uint32_t flags, hipStream_t stream) {
+    if (env_offset < 0) return fail("env_offset must be >= 0");
+    return step_code_replay_impl(p, s, d_actions, d_rewards, d_dones, d_code, d_code_prev, r, cursor, d_err, flags,
+                                 stream, 1, synth_seed, synth_step, env_offset);
+}
+
+static int step_code_replay_impl(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
+                                 uint8_t* d_dones, void* d_code, const void* d_code_prev, const drl_replay* r,
+                                 int64_t cursor, int32_t* d_err, uint32_t flags, hipStream_t stream, int synth,
+                                 uint64_t synth_seed, uint64_t synth_step, int64_t env_offset) {
     if (!d_code || !d_code_prev) return fail("code and code_prev must be non-NULL");
     if (d_code == d_code_prev) return fail("code_prev must be another buffer than code (the act's input rows)");
     if ((uintptr_t)d_code_prev % 16) return fail("code_prev must be 16-byte aligned");
@@ -414,6 +436,10 @@ int drl_step_code_replay(const drl_params* p, const drl_state* s, const int32_t*
     ring.ring_rew = r->rewards;
     ring.ring_done = r->dones;
     ring.code_prev = static_cast<const uint4*>(d_code_prev);
+    ring.synth = synth;
+    ring.synth_seed = synth_seed;
+    ring.synth_step = synth_step;
+    ring.env_offset = env_offset;
     return step_code_impl(p, s, d_actions, d_rewards, d_dones, nullptr, 0, d_code, d_err, flags, stream, &ring);
 }
 
@@ -450,6 +476,10 @@ static int step_code_impl(const drl_params* p, const drl_state* s, const int32_t
         a.ring_first = ring->ring_first;
         a.ring_base = ring->ring_base;
         a.ring_cap = ring->ring_cap;
+        a.synth = ring->synth;
+        a.env_offset = ring->env_offset;
+        a.synth_seed = ring->synth_seed;
+        a.synth_step = ring->synth_step;
     }
     hipError_t e = drl::launch_step(a, L.step_group_lanes, stream, drl::kStepMode);
     if (e != hipSuccess) return hip_fail(e, "drl_step launch");

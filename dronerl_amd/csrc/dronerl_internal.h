@@ -199,6 +199,11 @@ struct StepArgs {
     uint8_t* ring_done;
     const uint4* code_prev;  // the transitions' obs: the code rows the act read (not `code`)
     int64_t ring_first, ring_base, ring_cap;
+    // drl_step_code_replay_synth (with the ring): drone indices >= 1 act as drl_synth_actions(synth_seed,
+    // synth_step, env_offset) writes them, computed in the step; actions is read at column 0 only
+    int synth;
+    int64_t env_offset;
+    uint64_t synth_seed, synth_step;
     uint32_t max_rounds;
     FastDiv div_side;
     ObsGeom og;

@@ -777,6 +777,19 @@ __device__ __forceinline__ void for_other_lanes(int v, F&& f) {
 // writer's registers would otherwise spill in the plain step at 64 VGPRs).
 // RING (with CODE): also land drone 0's transitions in a replay ring
 // (drl_step_code_replay, step_ring_sink).
+// The synthetic action stream (drl_synth_actions, the oracle's synth_actions): drone `drone` of global env
+// `genv` at (seed, step) -- a counter hash, so any kernel can draw any element.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ int synth_action(uint64_t seed, uint64_t step, uint64_t genv, uint64_t drone) {
+    const uint64_t h = splitmix64(seed ^ splitmix64((step << 40) ^ (genv << 8) ^ drone));
+    return (int)(((h >> 32) * 5ull) >> 32);
+}
+
 template <int P, class GEO, bool ROLL, bool NT, bool CODE = false, bool RING = false>
 __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
     using GMask = typename GMaskT<P>::type;
@@ -830,18 +843,29 @@ __device__ __forceinline__ void step_batch(const StepArgs& a, int64_t wenv0) {
 #ifdef DRL_DIAG_ACT_U8  // bytes-only diagnostic build (wrong actions): one byte per action
     const int act_ld = reinterpret_cast<const uint8_t*>(a.actions)[wenv0 * N + li0] % 5;
 #else
-    const int act_ld = a.actions[wenv0 * N + li0];
+    // (drl_step_code_replay_synth: column 0 only; drone indices >= 1 take the counter hash below)
+    const int act_ld = a.actions[(RING && a.synth) ? (wenv0 + min(grp0, nenv_w - 1)) * (int64_t)N
+                                                   : wenv0 * N + li0];
 #endif
     // the packed grounds: loaded now, unpacked into LDS after the claim scan (compile-time geometry)
     [[maybe_unused]] NibStage<(GEO::kPstride > 0 ? GPW * GEO::kPstride / 16 : 1), (GEO::kGstride == GEO::kPstride)> nib;
     if constexpr (GEO::kPstride > 0) nib.load(ground_w, nenv_w * pstride, lane0);
     else stage_ground_nib(ground_w, nenv_w * pstride, W.gl, lane0, g.nib());
     __builtin_amdgcn_sched_barrier(0);  // issue every load above before waiting for the MT index
+    // the synthetic actions of drone indices >= 1 (drl_step_code_replay_synth), while the loads are in flight
+    [[maybe_unused]] int syn_act = 0;
+    if constexpr (RING) {
+        if (a.synth) syn_act = synth_action(a.synth_seed, a.synth_step, (uint64_t)(a.env_offset + wenv0 + grp0),
+                                            (uint64_t)j0);
+    }
     uint32_t mword = mi[0];  // the env's mt_index word: index, block, ring head / count
 #pragma unroll
     for (int e = 1; e < GPW; ++e) mword = (grp0 >= e) ? mi[e] : mword;
     uint32_t rec = active0 ? rec_ld : 0u;
     int my_action = active0 ? act_ld : 4;
+    if constexpr (RING) {
+        if (a.synth && j0 != 0 && active0) my_action = syn_act;
+    }
     if (!env_ok0) mword = (uint32_t)MT_N;
     // the stream position is read only after the ring's entries (they carry
     // it along), so nothing holds it across the claim phase; a rollout keeps
@@ -2484,12 +2508,6 @@ __global__ void __launch_bounds__(64 * NW) drl_refill_list_kernel(RefillArgs a) 
 }
 
 // ------------------------------------------------------- synthetic actions ---
-__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
-    z += 0x9e3779b97f4a7c15ull;
-    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-    return z ^ (z >> 31);
-}
 
 __global__ void drl_synth_actions_kernel(uint64_t seed, uint64_t step, int64_t env_offset, int64_t total, int N,
                                          FastDiv dn, int fast, int32_t* out) {

@@ -82,6 +82,8 @@ def _bind(L):
         "drl_qnet_act_eps": [D, _vp, _vp, i64, i64, _vp, u64, u64, i64, _vp, i64, i32, u64, u64, _vp, _vp, _vp],
         "drl_step_code_replay": [ctypes.POINTER(DrlParams), ctypes.POINTER(DrlState), _vp, _vp, _vp, _vp, _vp,
                                  ctypes.POINTER(DrlReplay), i64, _vp, ctypes.c_uint32, _vp],
+        "drl_step_code_replay_synth": [ctypes.POINTER(DrlParams), ctypes.POINTER(DrlState), _vp, _vp, _vp, _vp, _vp,
+                                       ctypes.POINTER(DrlReplay), i64, u64, u64, i64, _vp, ctypes.c_uint32, _vp],
         "drl_dqn_layout_query": [D, i32, ctypes.POINTER(DrlDqnLayout)],
         "drl_dqn_init": [D, i32, _vp, f32, _vp],
         "drl_dqn_train": [D, ctypes.POINTER(DrlDqnHParams), _vp, _vp, ctypes.POINTER(DrlReplay), i64, _vp],
@@ -382,11 +384,13 @@ class ReplayBuffer:
         return batch
 
     def _add_from_step(self, env, actions: torch.Tensor, rewards: torch.Tensor, dones: torch.Tensor,
-                       code_prev: torch.Tensor, code: torch.Tensor, flags: int):
+                       code_prev: torch.Tensor, code: torch.Tensor, flags: int, synth=None):
         """BatchedDeliveryDrones.step(..., code=code, replay=self, replay_obs=code_prev): the step and the
         add_many(code_prev, actions, rewards, code, dones) of its drone-0 transitions in one launch
         (drl_step_code_replay; train_jax.py:55-62's env.step + buffer.add_many pair).  The ring ends up
-        bit-identical to step + add_many.  Returns the batch's description (as add_many)."""
+        bit-identical to step + add_many.  synth=(seed, step): drone indices >= 1 act as
+        env.synth_actions(seed, step) would write them, drawn in the step (drl_step_code_replay_synth;
+        only actions[:, 0] is read).  Returns the batch's description (as add_many)."""
         E, N = env.num_envs, env.n_drones
         if not self.code_radius or self.code_radius != env.params.window_radius:
             raise ValueError("replay= needs a code buffer of the env's window radius (ReplayBuffer(code_radius=...))")
@@ -396,11 +400,18 @@ class ReplayBuffer:
         if code_prev.data_ptr() == code.data_ptr():
             raise ValueError("replay_obs must be another buffer than code (the rows the act read)")
         s = env.state.c()
-        _check(self.L, self.L.drl_step_code_replay(ctypes.byref(env._cp), ctypes.byref(s), _vp(actions.data_ptr()),
-                                                   _vp(rewards.data_ptr()), _vp(dones.data_ptr()),
-                                                   _vp(code.data_ptr()), _vp(code_prev.data_ptr()),
-                                                   ctypes.byref(self._c), self.cursor, _vp(env.err.data_ptr()),
-                                                   flags, _stream(self.obs.device)))
+        if synth is None:
+            _check(self.L, self.L.drl_step_code_replay(
+                ctypes.byref(env._cp), ctypes.byref(s), _vp(actions.data_ptr()), _vp(rewards.data_ptr()),
+                _vp(dones.data_ptr()), _vp(code.data_ptr()), _vp(code_prev.data_ptr()), ctypes.byref(self._c),
+                self.cursor, _vp(env.err.data_ptr()), flags, _stream(self.obs.device)))
+        else:
+            seed, step = synth
+            _check(self.L, self.L.drl_step_code_replay_synth(
+                ctypes.byref(env._cp), ctypes.byref(s), _vp(actions.data_ptr()), _vp(rewards.data_ptr()),
+                _vp(dones.data_ptr()), _vp(code.data_ptr()), _vp(code_prev.data_ptr()), ctypes.byref(self._c),
+                self.cursor, int(seed), int(step), int(env.env_offset), _vp(env.err.data_ptr()), flags,
+                _stream(self.obs.device)))
         w = self.code_bytes // 4
         batch = DrlReplayBatch(self.cursor, E, code_prev.data_ptr(), w, code.data_ptr(), w, actions.data_ptr(), N,
                                rewards.data_ptr(), N, dones.data_ptr(), N)

@@ -161,7 +161,7 @@ class BatchedDeliveryDrones:
     def step(self, actions: torch.Tensor, obs_k: int = 0, rewards: Optional[torch.Tensor] = None,
              dones: Optional[torch.Tensor] = None, obs: Optional[torch.Tensor] = None,
              obs_stream: Optional[bool] = None, code: Optional[torch.Tensor] = None, replay=None,
-             replay_obs: Optional[torch.Tensor] = None):
+             replay_obs: Optional[torch.Tensor] = None, synth=None):
         """env.py:112-215 for every env.  actions int32 [E, N] by drone index.
 
         Returns (rewards f32 [E,N], dones bool-as-uint8 [E,N]) and, when
@@ -182,6 +182,10 @@ class BatchedDeliveryDrones:
         ring, exactly as a following ``replay.add_many`` would, in the same
         launch (drl_step_code_replay; obs_k must be 0).  The batch
         description is left in ``replay.last_batch``.
+        synth=(seed, step) (with replay=): drone indices 1..N-1 act as
+        ``synth_actions(seed, step)`` would write them, drawn inside the step
+        (drl_step_code_replay_synth); only actions[:, 0] is read (the
+        agent's), the other columns are neither read nor written.
         """
         E, N = self.num_envs, self.n_drones
         actions = self._check(actions, torch.int32, (E, N), "actions")
@@ -210,10 +214,12 @@ class BatchedDeliveryDrones:
             if since >= self.refill_every:
                 since = 0
                 flags |= DRL_STEP_REFILL
+        if synth is not None and replay is None:
+            raise ValueError("synth= needs replay= (drl_step_code_replay_synth)")
         if replay is not None:
             if code is None or obs_k or replay_obs is None:
                 raise ValueError("replay= needs code= and replay_obs=, and obs_k=0")
-            replay._add_from_step(self, actions, rewards, dones, replay_obs, code, flags)
+            replay._add_from_step(self, actions, rewards, dones, replay_obs, code, flags, synth=synth)
             self._since_refill = since
             return rewards, dones
         check(lib().drl_step_code(ctypes.byref(self._cp), ctypes.byref(s), _ptr(actions), _ptr(rewards), _ptr(dones),

@@ -452,6 +452,16 @@ int drl_replay_add(const drl_replay* r, int64_t cursor, int64_t n, const float* 
 int drl_step_code_replay(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
                          uint8_t* d_dones, void* d_code, const void* d_code_prev, const drl_replay* r, int64_t cursor,
                          int32_t* d_err, uint32_t flags, hipStream_t stream);
+/* drl_step_code_replay whose drone indices 1..n_drones-1 act as drl_synth_actions(synth_seed, synth_step,
+ * env_offset) writes them (train_jax.py:45-49: every drone but drone 0 acts at random; the same counter hash,
+ * drawn inside the step): d_actions is read at column 0 only (d_actions[e * n_drones], the agent's action), its
+ * other columns are neither read nor written.  Bit for bit drl_synth_actions into d_actions' columns >= 1 +
+ * drl_step_code_replay.  In the train loop it replaces drl_qnet_act_synth's columns (no 4 B per drone written
+ * by the act and read back by the step). */
+int drl_step_code_replay_synth(const drl_params* p, const drl_state* s, const int32_t* d_actions, float* d_rewards,
+                               uint8_t* d_dones, void* d_code, const void* d_code_prev, const drl_replay* r,
+                               int64_t cursor, uint64_t synth_seed, uint64_t synth_step, int64_t env_offset,
+                               int32_t* d_err, uint32_t flags, hipStream_t stream);
 
 
 /* drl_qnet_act / drl_qnet_act_code with epsilon read from device memory

@@ -148,6 +148,14 @@ def test_step_code_replay_validates_before_device_work():
     assert call(good, cursor=-1) != 0 and b"cursor" in L.drl_last_error()
     assert call(DrlReplay(100, 294, 64, 64, 64, 64, 64)) != 0 and b"obs_floats" in L.drl_last_error()
 
+    # drl_step_code_replay_synth (drone indices >= 1 drawn in the step): the same checks, and env_offset >= 0
+    def call_synth(r, prev=vp(2048), env_offset=0):
+        return L.drl_step_code_replay_synth(ctypes.byref(p), ctypes.byref(s), vp(64), vp(64), vp(64), vp(1024), prev,
+                                            None if r is None else ctypes.byref(r), 0, 3, 4, env_offset, None, 0, None)
+    assert call_synth(good, env_offset=-1) != 0 and b"env_offset" in L.drl_last_error()
+    assert call_synth(good, prev=vp(1024)) != 0 and b"another buffer" in L.drl_last_error()
+    assert call_synth(None) != 0 and b"replay is NULL" in L.drl_last_error()
+
 
 @pytest.mark.parametrize("val,ok", [("0", False), ("-3", False), ("x", False), ("", False), ("7", True)])
 def test_refill_cadence_override_must_be_positive(monkeypatch, val, ok):

@@ -763,6 +763,53 @@ def test_train_segment_code_fused_replay_matches_separate_add():
         assert torch.equal(l0.net.packed, l1.net.packed), name
 
 
+@pytest.mark.parametrize("G,N,E", [(16, 8, 3000), (64, 32, 600)])
+def test_train_segment_synth_branch_graph_matches_fused(G, N, E):
+    """bench.TrainSegment(synth_branch=True): the synthetic actions of step
+    t + 1 on their own graph branch beside learner t (drl_synth_actions,
+    joined before act t + 1), captured and replayed as train_loop_bench does,
+    leave the same env state, ring, learner and packed net as the fused act
+    (drl_qnet_act_synth) run eagerly: two segments each."""
+    from bench import TrainSegment
+    p = EnvParams(n_drones=N, grid_size=G)
+    seg = 13
+    runs = []
+    for branch in (False, True):
+        env = Env(p, E)
+        env.reset(seed=6)
+        loop = TrainSegment(env, seg, input="code", capacity=5000, fused=not branch, synth_branch=branch)
+        if branch:
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                loop.run()
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                loop.run()
+            g.replay()
+        else:
+            loop.run()
+            loop.run()
+        torch.cuda.synchronize()
+        env.check_errors()
+        loop.net.check_errors()
+        runs.append((gpu_state(env), loop))
+    (g0, l0), (g1, l1) = runs
+    assert_state(g1, g0, "synth branch (graph) vs fused")
+    for k in ("obs", "next_obs", "actions", "rewards", "dones"):
+        assert torch.equal(getattr(l0.rb, k), getattr(l1.rb, k)), k
+    assert l0.rb.cursor == l1.rb.cursor and l0.rb.size == l1.rb.size
+    for b in range(2):  # (drone 0's column: the fused run draws the others inside its step)
+        assert torch.equal(l0.acts[b][:, 0], l1.acts[b][:, 0]), b
+    for k in ("online", "target", "m", "v"):
+        for (w0, b0), (w1, b1) in zip(l0.learner.params(k), l1.learner.params(k)):
+            assert torch.equal(w0, w1) and torch.equal(b0, b1), k
+    assert l0.learner.counters() == l1.learner.counters()
+    assert torch.equal(l0.net.packed, l1.net.packed)
+
+
 @pytest.mark.parametrize("kernel", list(RESET_KERNELS))
 @pytest.mark.parametrize("name", ["c1_g8_n4", "c3_g16_n8", "c4_g32_n16", "c5_g64_n32", "t_g5_n1", "t_g7_n2",
                                   "t_g11_n6", "t_g13_n8"])

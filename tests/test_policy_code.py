@@ -80,9 +80,9 @@ def decode_code(code: np.ndarray, W: int) -> np.ndarray:
     return out.reshape(E, W, W, 6)
 
 
-def _env(side, n, radius, E, seed=0):
+def _env(side, n, radius, E, seed=0, env_offset=0):
     from dronerl_amd import BatchedDeliveryDrones, EnvParams
-    env = BatchedDeliveryDrones(EnvParams(n_drones=n, grid_size=side, window_radius=radius), E)
+    env = BatchedDeliveryDrones(EnvParams(n_drones=n, grid_size=side, window_radius=radius), E, env_offset=env_offset)
     env.reset(seed=seed)
     return env
 
@@ -309,15 +309,20 @@ def test_code_replay_buffer_samples_decode_to_obs_buffer():
     (64, 32, 4, 129, 300, 250),      # 9x9 window (192-B rows), C5's grid
     (64, 32, 3, 6000, 5000, 4500),   # the C5 compile-time instance with num_envs > capacity (c5.train_loop)
 ])
-def test_step_code_replay_equals_step_then_add_many(side, n, radius, E, cap, cursor0):
+@pytest.mark.parametrize("synth", [False, True])
+def test_step_code_replay_equals_step_then_add_many(side, n, radius, E, cap, cursor0, synth):
     """drl_step_code_replay (env.step(..., replay=rb, replay_obs=prev)): the
     step's outputs and state and the whole ring -- obs, next_obs, actions,
     rewards, dones, cursor, size -- equal drl_step_code followed by
     drl_replay_add of the same transitions, bit for bit, over steps that wrap
-    the ring."""
+    the ring.  synth: drl_step_code_replay_synth (env.step(..., synth=(seed,
+    t))) draws drone indices >= 1 itself; its actions' other columns hold an
+    invalid action (9) that must not be read (env_offset 1000: the draws
+    follow the global env index)."""
     from dronerl_amd.dqn import ReplayBuffer
     D = (2 * radius + 1) ** 2 * 6
-    a, b = _env(side, n, radius, E, seed=11), _env(side, n, radius, E, seed=11)
+    off = 1000 if synth else 0
+    a, b = _env(side, n, radius, E, seed=11, env_offset=off), _env(side, n, radius, E, seed=11, env_offset=off)
     ra_ = ReplayBuffer(cap, D, torch.device("cuda"), code_radius=radius)
     rb_ = ReplayBuffer(cap, D, torch.device("cuda"), code_radius=radius)
     for r in (ra_, rb_):
@@ -329,7 +334,13 @@ def test_step_code_replay_equals_step_then_add_many(side, n, radius, E, cap, cur
     b.get_obs(1, code=cb[0])
     for t in range(6):
         acts = a.synth_actions(seed=8, step=t)
-        rw_a, dn_a = a.step(acts, code=ca[(t + 1) & 1], replay=ra_, replay_obs=ca[t & 1])
+        if synth:
+            only0 = torch.full_like(acts, 9)
+            only0[:, 0] = acts[:, 0]
+            rw_a, dn_a = a.step(only0, code=ca[(t + 1) & 1], replay=ra_, replay_obs=ca[t & 1], synth=(8, t))
+            assert (only0[:, 1:] == 9).all()  # (neither read nor written)
+        else:
+            rw_a, dn_a = a.step(acts, code=ca[(t + 1) & 1], replay=ra_, replay_obs=ca[t & 1])
         rw_b, dn_b = b.step(acts, code=cb[(t + 1) & 1])
         rb_.add_many(cb[t & 1], acts, rw_b, cb[(t + 1) & 1], dn_b)
         assert torch.equal(rw_a, rw_b) and torch.equal(dn_a, dn_b), t

@@ -23,6 +23,11 @@ def main():
     ap.add_argument("--precision", default="f32", choices=("f32", "bf16"))
     ap.add_argument("--lib", default="", help="alternative library (tools/variants.py)")
     ap.add_argument("--refill-branch", action="store_true", help="A/B: the refill on its own graph branch")
+    ap.add_argument("--synth-in-act", action="store_true",
+                    help="A/B: the act writes drones 1..N-1's synthetic columns (drl_qnet_act_synth) instead of the "
+                    "step drawing them (drl_step_code_replay_synth, the default)")
+    ap.add_argument("--synth-branch", action="store_true",
+                    help="A/B: synthetic actions unfused, on their own graph branch beside the learner")
     args = ap.parse_args()
     if args.lib:
         import dronerl_amd._native as nat
@@ -31,7 +36,8 @@ def main():
     env = BatchedDeliveryDrones(EnvParams(n_drones=N, grid_size=G), E)
     env.reset(seed=0)
     r = bench.train_loop_bench(env, args.segments, precision=args.precision, input=args.input,
-                               refill_branch=args.refill_branch)
+                               refill_branch=args.refill_branch, synth_branch=args.synth_branch,
+                               fused=not args.synth_branch, synth_in_step=False if args.synth_in_act else None)
     print(json.dumps({k: r[k] for k in ("us_per_step", "precision", "input")}), flush=True)
 
 
