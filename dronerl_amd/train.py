@@ -80,14 +80,17 @@ def train(params: EnvParams, num_envs: int, num_steps: int, hidden: Sequence[int
     e0.record()
     for t in range(num_steps):
         b, nb = t & 1, (t + 1) & 1
+        # drones 1..N-1 act at random (train_jax.py:45-49): written by the act beside drone 0's action when the
+        # step reads them, or drawn by the step itself (drl_step_code_replay_synth; the same counter hash)
         net.act(code[b], learner.epsilon, seed=act_seed, step=t, env_offset=env.env_offset, actions=acts,
-                synth=(action_seed, t))
+                synth=(action_seed, t) if shard else None)
         if shard:
             env.step(acts, rewards=rew, dones=don, code=code[nb])
             rb.add_many(code[b], acts, rew, code[nb], don)
             rb.gather(learner)
         else:  # (the step lands its transitions in the ring itself: drl_step_code_replay)
-            env.step(acts, rewards=rew, dones=don, code=code[nb], replay=rb, replay_obs=code[b])
+            env.step(acts, rewards=rew, dones=don, code=code[nb], replay=rb, replay_obs=code[b],
+                     synth=(action_seed, t))
         learner.train(ring)
         if t % reset_env_every == 0:  # train_jax.py:101-113 (step 0 included)
             env.reset(seed=None)

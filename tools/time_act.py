@@ -18,7 +18,9 @@ def main():
     ap.add_argument("--stride", type=int, default=294, help="obs row stride in floats (296: 16-B aligned rows)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--input", default="obs", choices=["obs", "code"], help="code: drl_qnet_act_code (f32)")
-    ap.add_argument("--synth", action="store_true", help="also write drones 1..7's synthetic actions (act_synth)")
+    ap.add_argument("--synth", action="store_true", help="also write drones 1..N-1's synthetic actions (act_synth)")
+    ap.add_argument("--drones", type=int, default=8, help="action columns (N; the train loop's act writes N - 1 "
+                    "synthetic ones with --synth: 31 at C5)")
     ap.add_argument("--stamps", action="store_true", help="library built with -DDRL_QC_STAMPS: phase cycles")
     ap.add_argument("--slices", type=int, default=0, help="v4 stamps: layer-0 slices per pass to print (10 at 7x7)")
     ap.add_argument("--group", type=int, default=64,
@@ -40,7 +42,7 @@ def main():
     obs = torch.rand((E, 1, 7, 7, 6), device="cuda")
     net = QNetwork(294, tuple(int(x) for x in args.hidden.split(",")), generator=torch.Generator().manual_seed(0),
                    precision=args.precision, input=args.input)
-    a = torch.zeros((E, 8), dtype=torch.int32, device="cuda")
+    a = torch.zeros((E, args.drones), dtype=torch.int32, device="cuda")
     flat = obs.reshape(E, -1)
     if args.stride != 294:
         big = torch.zeros((E, args.stride), device="cuda")
