@@ -80,7 +80,7 @@ def train(params: EnvParams, num_envs: int, num_steps: int, hidden: Sequence[int
     e0.record()
     for t in range(num_steps):
         b, nb = t & 1, (t + 1) & 1
-        # drones 1..N-1 act at random (train_jax.py:45-49): written by the act beside drone 0's action when the
+        # drones 1..N-1 act at random (train_jax.py:42-49): written by the act beside drone 0's action when the
         # step reads them, or drawn by the step itself (drl_step_code_replay_synth; the same counter hash)
         net.act(code[b], learner.epsilon, seed=act_seed, step=t, env_offset=env.env_offset, actions=acts,
                 synth=(action_seed, t) if shard else None)

@@ -21,6 +21,7 @@
  *   train_jax.py:68-98             the scan body's learner block   drl_dqn_train
  *   jax_impl/buffers.py:57-77      ReplayBuffer.add_many  drl_replay_add
  *   train_jax.py:55-62             env.step + add_many    drl_step_code_replay (one launch)
+ *   train_jax.py:42-62             + the random drones    drl_step_code_replay_synth (drawn in the step)
  *
  * Two layers: stateless calls on caller-owned buffers (drl_reset, drl_step,
  * ...) and library-owned env handles (drl_env_*) that
@@ -453,7 +454,7 @@ int drl_step_code_replay(const drl_params* p, const drl_state* s, const int32_t*
                          uint8_t* d_dones, void* d_code, const void* d_code_prev, const drl_replay* r, int64_t cursor,
                          int32_t* d_err, uint32_t flags, hipStream_t stream);
 /* drl_step_code_replay whose drone indices 1..n_drones-1 act as drl_synth_actions(synth_seed, synth_step,
- * env_offset) writes them (train_jax.py:45-49: every drone but drone 0 acts at random; the same counter hash,
+ * env_offset) writes them (train_jax.py:42-49: every drone but drone 0 acts at random; the same counter hash,
  * drawn inside the step): d_actions is read at column 0 only (d_actions[e * n_drones], the agent's action), its
  * other columns are neither read nor written.  Bit for bit drl_synth_actions into d_actions' columns >= 1 +
  * drl_step_code_replay.  In the train loop it replaces drl_qnet_act_synth's columns (no 4 B per drone written
