@@ -1248,6 +1248,9 @@ constexpr int QC4_WAVES = 4;
 #ifndef DRL_QC4_DMALOOP
 #define DRL_QC4_DMALOOP 0  // A/B knob: stage slices >= 2 inside layer 0 (measured slower: 17.6 vs 16.5 us at C3)
 #endif
+#ifndef DRL_QC4_XCD
+#define DRL_QC4_XCD 0  // A/B knob: XCD-contiguous env groups (with the step's DRL_XCD_REMAP: codes read from the L2 they were written to)
+#endif
 #ifndef DRL_QC4_EARLYSPLIT
 #define DRL_QC4_EARLYSPLIT 1  // layer 1's first split inside layer 0's last slice (16.33-16.53 vs 16.44-16.75 us, g19)
 #endif
@@ -1377,7 +1380,19 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
     const int c = lane & 15, g = lane >> 4;
     const int64_t ntiles = (a.E + 15) / 16;
     const int64_t ngroups = (ntiles + TP - 1) / TP;
+#if DRL_QC4_XCD
+    // (A/B) XCD-contiguous groups: the workgroups of XCD x (blockIdx % 8 == x) take a contiguous eighth of the
+    // groups, each wave its passes at stride NW -- the envs whose codes a step built with DRL_XCD_REMAP wrote
+    // on the same XCD (its L2)
+    const int64_t passes = (ngroups + (int64_t)gridDim.x * NW - 1) / ((int64_t)gridDim.x * NW);
+    const uint32_t bq = gridDim.x / 8, br = gridDim.x % 8, bxx = blockIdx.x % 8;
+    const int64_t bx = (int64_t)((bxx < br ? bxx * (bq + 1) : br * (bq + 1) + (bxx - br) * bq) + blockIdx.x / 8);
+    const int64_t gstride = NW;
+    const int64_t gend = min(ngroups, (bx + 1) * NW * passes);
+#else
     const int64_t gstride = (int64_t)gridDim.x * NW;
+    const int64_t gend = ngroups;
+#endif
     constexpr float kLo = 1.0f / 2048.0f;
     const f16x2 kLo2 = {(_Float16)kLo, (_Float16)kLo};
     // the codes through a buffer resource: 32-bit lane offsets (the launch keeps E * code bytes < 2^31), so no
@@ -1400,7 +1415,11 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) load_vec(tile, v, dst);
     };
+#if DRL_QC4_XCD
+    const int64_t grp0 = bx * NW * passes + wave;
+#else
     const int64_t grp0 = (int64_t)blockIdx.x * NW + wave;
+#endif
 #ifdef DRL_QC_STAMPS
     const uint64_t t_entry = __builtin_amdgcn_s_memtime();
 #endif
@@ -1450,7 +1469,7 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
     // landed (in-order vmcnt) and every wave's (the barrier)
     constexpr int KE = KP < 2 ? KP : 2;
     uint32_t cw[TP][4 * NV];
-    const int64_t gl0 = grp0 < ngroups ? grp0 : 0;
+    const int64_t gl0 = grp0 < gend ? grp0 : 0;
 #if DRL_QC4_EARLYVEC
 #pragma unroll
     for (int h = 0; h < TP; ++h) load_vec(TP * gl0 + h, 0, cw[h]);
@@ -1483,7 +1502,7 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
     // fragments issued at steps <= 16 - PD of slice T - 1 are younger than slice T's.
     static_assert(!DRL_QC4_EARLYVEC && KE == 2, "DMALOOP stages slices >= 2 in the loop");
     constexpr int NDY = (1 <= 16 - PD) + (5 <= 16 - PD) + (9 <= 16 - PD) + (13 <= 16 - PD);
-    if (grp0 >= ngroups) {  // a wave without a pass still stages its fragments
+    if (grp0 >= gend) {  // a wave without a pass still stages its fragments
 #pragma unroll
         for (int t = KE; t < KP; ++t) dma(t);
     }
@@ -1499,7 +1518,7 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
     // latency exposed at the second pass's start (C5 act 42 us in the loop against 28 back to back).
     // Unconditional (past the last pass the first pass's again, from L2), so every wait count is static.
 #pragma unroll
-    for (int h = 0; h < TP; ++h) load_codes(TP * (grp0 + gstride < ngroups ? grp0 + gstride : gl0) + h, ncw[h]);
+    for (int h = 0; h < TP; ++h) load_codes(TP * (grp0 + gstride < gend ? grp0 + gstride : gl0) + h, ncw[h]);
     constexpr int NNX = TP * NV;
 #else
     constexpr int NNX = 0;
@@ -1520,10 +1539,10 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
     const bool bias_group = g == 0;
 
     bool first = true;
-    if (grp0 >= ngroups) {  // no group: still take part in the staging barriers
+    if (grp0 >= gend) {  // no group: still take part in the staging barriers
         qc3_for<0, KP>([&](auto t_c) { slice_ready(t_c); });
     }
-    for (int64_t grp = grp0; grp < ngroups; grp += gstride) {
+    for (int64_t grp = grp0; grp < gend; grp += gstride) {
 #ifdef DRL_QC_STAMPS
         __builtin_amdgcn_sched_barrier(0);
         const uint64_t ts0 = __builtin_amdgcn_s_memtime();
@@ -1665,7 +1684,7 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
 #pragma unroll
         for (int t = 0; t < KT1; ++t) {
             if (t + 1 < KT1) ld1(t + 1, (t + 1) & 1);
-            if (t + 1 == KT1 && ngrp < ngroups && !(DRL_QC4_EARLYNEXT && grp == grp0)) {  // the next pass's codes (the
+            if (t + 1 == KT1 && ngrp < gend && !(DRL_QC4_EARLYNEXT && grp == grp0)) {  // the next pass's codes (the
                 // first pass's successor was loaded in the prologue), into their own registers and younger than
                 // every layer-1 fragment (the compiler's wait counts for those then ignore them); copied at the end
 #pragma unroll
@@ -1771,7 +1790,7 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
             for (int t = 0; t < KP; ++t) sl[t] = slice_ts[t];
         }
 #endif
-        if (ngrp < ngroups) {
+        if (ngrp < gend) {
 #pragma unroll
             for (int h = 0; h < TP; ++h)
 #pragma unroll
@@ -1784,7 +1803,7 @@ drl_qnet_act_code4_kernel(QnetArgs a) {
     if (a.synth_n > 1) {  // as in drl_qnet_act_kernel (TP 16-env tiles per group)
         const uint32_t nd = (uint32_t)a.synth_n - 1u;
         const uint32_t per = (uint32_t)(TP * 16) * nd;
-        for (int64_t gg = grp0; gg < ngroups; gg += gstride) {
+        for (int64_t gg = grp0; gg < gend; gg += gstride) {
             for (uint32_t k = (uint32_t)lane; k < per; k += 64u) {
                 const uint32_t el = k / nd;
                 const int64_t env = TP * 16 * gg + el;
