@@ -913,7 +913,9 @@ def train_loop_bench(env, reps: int, seg: int = 100, parallel: bool = False, fus
     branches = (("replay add_many" if fused else "synthetic actions and replay add_many") +
                 " on parallel graph branches, 3 rotating buffers" if parallel else
                 "one stream, the refill on its own graph branch" if loop.refill_branch else "one stream") + \
-        ("; synthetic actions inside the act launch" if fused else "") + \
+        ("; drones 1..N-1's synthetic actions drawn inside the step launch (drl_step_code_replay_synth)"
+         if loop.synth_in_step else "; synthetic actions inside the act launch" if fused else
+         "; synthetic actions on their own graph branch beside the learner" if loop.synth_branch else "") + \
         ("; the replay add inside the step launch (drl_step_code_replay)" if loop.fuse_replay else "")
     return {"env_steps_per_s": E * seg * reps / dt, "us_per_step": dt / (seg * reps) * 1e6,
             "segments": reps, "steps_per_segment": seg, "precision": precision, "input": input,
