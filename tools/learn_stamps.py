@@ -87,6 +87,13 @@ def main():
            "layer0_us": {name: med(bl[:, :, i].max(1)) for i, name in
                          [(0, "start"), (1, "setup"), (2, "staged"), (3, "z0_handed"), (4, "deltas_in"),
                           (6, "deltas_staged"), (7, "registers_written"), (5, "weights_done")]},
+           # the same, split: online-side workgroups (layer-0 weights) and target-side ones (the later layers)
+           "layer0_online_side_us": {name: med(bl[:, :nblk // 2, i].max(1)) for i, name in
+                                     [(4, "deltas_in"), (6, "deltas_staged"), (7, "registers_written"),
+                                      (5, "weights_done")]},
+           "layer0_target_side_us": {name: med(bl[:, nblk // 2:, i].max(1)) for i, name in
+                                     [(4, "deltas_in"), (6, "deltas_staged"), (7, "registers_written"),
+                                      (5, "weights_done")]},
            "target_tail_us": {name: med(tg[:, i]) for i, name in TAIL if i < 5 or 7 <= i < 11},
            "online_tail_us": {name: med(on[:, i]) for i, name in TAIL}}
     print(json.dumps(out, indent=1))
