@@ -421,7 +421,10 @@ struct DqnCounters {
 static_assert(sizeof(DqnCounters) == 64, "drl_dqn_counters is 64 bytes");
 
 constexpr int DQN_MAX_BATCH = 64;
-constexpr int DQN_TILE = 8;       // layer-0 units per workgroup of the learner kernel
+#ifndef DRL_DQN_TILE
+#define DRL_DQN_TILE 4  // (8 until round 6: C3 train loop 69.3 -> 67.5 us per step with 4; 2: 68.6)
+#endif
+constexpr int DQN_TILE = DRL_DQN_TILE;  // layer-0 units per workgroup of the learner kernel
 #ifndef DRL_DQN_THREADS
 #define DRL_DQN_THREADS 512
 #endif
@@ -431,7 +434,7 @@ constexpr int DQN_MAX_SEGS = 28;  // copy segments of the learner kernel's prefe
 constexpr int DQN_UB = 4;         // weights whose loads a thread issues together in the update phase
 constexpr int DQN_PF = 8;         // weights per thread whose operands are loaded before the epoch wait
 constexpr int DQN_W0R = 4096 / DQN_THREADS;  // layer-0 tile weights per thread in registers at the launch's start
-                                             // (a tile of 8 units x up to 512 inputs)
+                                             // (a tile of up to 8 units x up to 512 inputs)
 
 // One segment of the learner kernel's one-round staging into LDS: element
 // i < n lands at LDS float dst + (pad ? (i / row) * (row + pad) + i % row :

@@ -15,7 +15,7 @@
 //
 // One launch (drl_dqn_train_kernel) per learner step: workgroups split
 // layer 0 of both nets (online on the sampled obs, target on next_obs) in
-// 8-unit tiles and hand their pre-activations over with write-through
+// DQN_TILE-unit tiles and hand their pre-activations over with write-through
 // stores and a ticket counter; two more workgroups (the tails, one per net)
 // prefetch everything else into LDS meanwhile, wait for the tickets, and run
 // their net's later layers; the online tail then runs the TD error, the loss
@@ -341,7 +341,7 @@ __device__ __forceinline__ void dq_mm(const float* X, int xs, int xk, const floa
 
 // The same dot products with one output per lane quad (lane c: k = c mod 4):
 // four times the lanes of dq_mm and a quarter of its per-lane chain, for
-// the layer-0 workgroups' small output tiles (8 units x B rows).
+// the layer-0 workgroups' small output tiles (DQN_TILE units x B rows).
 template <class Out>
 __device__ __forceinline__ void dq_mm1(const float* X, int xs, const float* W, int wr, int wk, int n, int B, int J,
                                        Out out) {

@@ -194,7 +194,7 @@ def test_dqn_layout_query():
     assert lay.n_params == 294 * 128 + 128 + 128 * 64 + 64 + 320 + 8 and n > 0
     assert (lay.online_off, lay.target_off, lay.m_off, lay.v_off) == tuple(i * 4 * lay.n_params for i in range(4))
     assert lay.counters_off == 16 * lay.n_params and lay.scratch_off == lay.counters_off + 64
-    assert lay.bytes % 16 == 0 and lay.grad_workgroups == 2 + 2 * 128 // 8 and lay.grad_lds_bytes <= 159 * 1024
+    assert lay.bytes % 16 == 0 and lay.grad_workgroups == 2 + 2 * 128 // 4 and lay.grad_lds_bytes <= 159 * 1024
     for b, ok in ((0, False), (1, True), (64, True), (65, False)):
         assert (L.drl_dqn_layout_query(ctypes.byref(_desc(294, (128, 64), 1)), b, ctypes.byref(lay)) == 0) == ok
     # 8-unit layer-0 tiles: the widest input the nets take (512) fits a batch of 64 within 150 KB
